@@ -1,0 +1,141 @@
+"""ctypes binding of libghs_mst.so (the C-ABI declared in include/ghs_mst.h).
+
+The product path has exactly one implementation of the MST: the gfx950 HIP kernels in this
+library. There is no CPU fallback — if the library is missing or no GPU is visible, every
+compute entry point raises. (The CPU restatement used to CHECK results lives in oracle/, which
+this package never imports.)
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GHS_MST_LIB", os.path.join(_HERE, "lib", "libghs_mst.so"))
+
+GHS_OK = 0
+GHS_E_ARG = -1
+GHS_E_NONCANON = -2
+GHS_E_HIP = -3
+GHS_E_ROUNDCAP = -4
+GHS_E_NODEVICE = -5
+GHS_E_NOMEM = -6
+GHS_E_STATE = -7
+GHS_MAX_ROUND_STATS = 64
+
+_ERR_NAMES = {
+    GHS_E_ARG: "GHS_E_ARG", GHS_E_NONCANON: "GHS_E_NONCANON", GHS_E_HIP: "GHS_E_HIP",
+    GHS_E_ROUNDCAP: "GHS_E_ROUNDCAP", GHS_E_NODEVICE: "GHS_E_NODEVICE", GHS_E_NOMEM: "GHS_E_NOMEM",
+    GHS_E_STATE: "GHS_E_STATE",
+}
+
+# every symbol include/ghs_mst.h declares (tests check the .so exports all of them)
+EXPORTED_SYMBOLS = (
+    "ghs_abi_version", "ghs_last_error", "ghs_device_count", "ghs_mst_host",
+    "ghs_build_arcs_temp_bytes", "ghs_count_arcs_range", "ghs_build_arcs_range", "ghs_build_arcs",
+    "ghs_workspace_bytes", "ghs_mst_device",
+    "ghs_solver_create", "ghs_solver_minedge", "ghs_solver_pack_best", "ghs_solver_unpack_best",
+    "ghs_solver_contract", "ghs_solver_finish", "ghs_solver_destroy",
+    "ghs_rmat_temp_bytes", "ghs_rmat_generate", "ghs_grid_generate",
+)
+
+
+class GHSError(RuntimeError):
+    """A negative GHS_E_* return code from libghs_mst.so."""
+
+    def __init__(self, code, message):
+        super().__init__(f"{_ERR_NAMES.get(code, code)}: {message}")
+        self.code = code
+
+
+class RoundStats(ctypes.Structure):
+    _fields_ = [
+        ("live_arcs", ctypes.c_uint64),
+        ("active_components", ctypes.c_uint64),
+        ("hooks", ctypes.c_uint64),
+        ("ms_minedge", ctypes.c_float),
+        ("ms_hook", ctypes.c_float),
+        ("ms_jump", ctypes.c_float),
+        ("ms_active", ctypes.c_float),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class Result(ctypes.Structure):
+    _fields_ = [
+        ("num_mst_edges", ctypes.c_uint64),
+        ("total_weight", ctypes.c_uint64),
+        ("rounds", ctypes.c_uint32),
+        ("num_stats", ctypes.c_uint32),
+        ("ms_total", ctypes.c_double),
+    ]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load the library once; raise loudly if it is missing (no fallback)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libghs_mst.so not found at {LIB_PATH}; build it with "
+                "`make -C distributed_ghs_implementation_amd/csrc` (or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        u32, u64, i32, sz, vp = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
+        P = ctypes.POINTER
+        sigs = {
+            "ghs_abi_version": (i32, []),
+            "ghs_last_error": (ctypes.c_char_p, []),
+            "ghs_device_count": (i32, [P(i32)]),
+            "ghs_mst_host": (i32, [u32, u64, vp, vp, vp, vp, P(Result), P(RoundStats)]),
+            "ghs_build_arcs_temp_bytes": (sz, [u32, u64]),
+            "ghs_count_arcs_range": (i32, [u32, u64, vp, vp, u32, u32, vp, sz, vp, P(u64)]),
+            "ghs_build_arcs_range": (i32, [u32, u64, vp, vp, vp, u32, u32, vp, vp, vp, u64, vp, sz, vp, P(u64)]),
+            "ghs_build_arcs": (i32, [u32, u64, vp, vp, vp, vp, vp, vp, vp, sz, vp]),
+            "ghs_workspace_bytes": (sz, [u32, u64, u64]),
+            "ghs_mst_device": (i32, [u32, u64, vp, vp, vp, vp, vp, u64, vp, sz, vp, vp, P(Result), P(RoundStats)]),
+            "ghs_solver_create": (i32, [u32, u64, vp, vp, vp, vp, vp, u64, vp, sz, vp, vp, P(vp)]),
+            "ghs_solver_minedge": (i32, [vp, P(u64)]),
+            "ghs_solver_pack_best": (i32, [vp, vp]),
+            "ghs_solver_unpack_best": (i32, [vp, vp]),
+            "ghs_solver_contract": (i32, [vp, P(i32)]),
+            "ghs_solver_finish": (i32, [vp, P(Result), P(RoundStats)]),
+            "ghs_solver_destroy": (i32, [vp]),
+            "ghs_rmat_temp_bytes": (sz, [u32, u32]),
+            "ghs_rmat_generate": (i32, [u32, u32, u64, u64, vp, vp, vp, P(u64), vp, sz, vp]),
+            "ghs_grid_generate": (i32, [u32, u32, u64, vp, vp, vp, vp]),
+        }
+        for name, (res, args) in sigs.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.ghs_abi_version() != 1:
+            raise ImportError(f"libghs_mst.so ABI {L.ghs_abi_version()} != 1")
+        _lib = L
+        return _lib
+
+
+def check(rc):
+    """Raise GHSError for a negative return code."""
+    if rc != GHS_OK:
+        msg = load().ghs_last_error()
+        raise GHSError(rc, msg.decode() if msg else "")
+    return rc
+
+
+def device_count():
+    c = ctypes.c_int(0)
+    check(load().ghs_device_count(ctypes.byref(c)))
+    return c.value
+
+
+def require_gpu():
+    """The product path runs only on a GPU: fail loudly, never fall back to the CPU."""
+    if device_count() == 0:
+        raise GHSError(GHS_E_NODEVICE, "no HIP device visible: the MST engine runs only on MI355X (gfx950)")

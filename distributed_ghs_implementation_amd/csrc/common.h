@@ -1,0 +1,53 @@
+// Shared definitions for libghs_mst.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/ghs_mst.h"
+
+namespace ghs {
+
+constexpr uint64_t KEY_NONE = ~0ull;       // "no outgoing edge" (reference: best_weight = inf)
+constexpr uint32_t LABEL_NONE = 0xffffffffu;
+constexpr int WAVE = 64;                   // CDNA wavefront
+constexpr int BLOCK = 256;                 // 4 waves
+constexpr int ARCS_PER_THREAD = 4;         // one 16-B load of src / dst per lane
+constexpr int ARCS_PER_BLOCK = BLOCK * ARCS_PER_THREAD;
+
+void set_error(const std::string &msg);
+
+// bijective 32-bit mixer (xorshift-multiply; every step is invertible on u32)
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9e3779b97f4a7c15ull;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+
+}  // namespace ghs
+
+#define GHS_HIP_CHECK(expr)                                                                     \
+  do {                                                                                          \
+    hipError_t _e = (expr);                                                                     \
+    if (_e != hipSuccess) {                                                                     \
+      ::ghs::set_error(std::string(#expr) + ": " + hipGetErrorString(_e) + " (" __FILE__ ":" + \
+                       std::to_string(__LINE__) + ")");                                         \
+      return GHS_E_HIP;                                                                         \
+    }                                                                                           \
+  } while (0)
+
+#define GHS_FAIL(code, msg)          \
+  do {                               \
+    ::ghs::set_error(msg);           \
+    return (code);                   \
+  } while (0)

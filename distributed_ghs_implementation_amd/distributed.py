@@ -1,0 +1,134 @@
+"""Multi-GPU MST: one process per GPU, torch.distributed (backend "nccl" == RCCL over xGMI).
+
+Replaces the reference's MPI path (ghs_implementation_mpi.py:884-954: one rank PER VERTEX,
+pickled point-to-point messages, bcast/Barrier/gather) with one rank per GPU and ONE collective
+per round:
+
+  * partition: rank r owns the arcs whose source lies in the vertex range
+    [r*n/N, (r+1)*n/N) (ghs_build_arcs_range); the canonical edge list (needed to resolve a
+    chosen edge's endpoints) and the fragment state are replicated;
+  * per round: local min-edge over the rank's arcs -> dense best[] slots of the active
+    fragments -> all_reduce(MIN) -> identical hook / pointer-jump / next-list on every rank;
+  * result: in_mst is identical on every rank by construction (same inputs, same decisions);
+    rank 0 writes the output (the reference gathered BRANCH edges to rank 0,
+    ghs_implementation_mpi.py:760-779).
+
+The round loop (`run_rounds`) is written against a small stepper interface so that the same
+orchestration can be exercised on CPU with the gloo backend in tests (tests inject a CPU
+stepper from oracle/); the product stepper is `HipStepper` (libghs_mst.so).
+"""
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from . import _native
+from .device import DeviceEdges, DeviceMST, _ptr, _stream
+
+
+def vertex_range(n, rank, world):
+    """Contiguous source-vertex range owned by `rank` (equal vertex counts; the seeded vertex
+    permutation of the R-MAT generator spreads hubs evenly)."""
+    return (n * rank) // world, (n * (rank + 1)) // world
+
+
+class HipStepper:
+    """The stepwise solver of include/ghs_mst.h (ghs_solver_*) over one rank's arcs."""
+
+    def __init__(self, engine):
+        self.e = engine
+        L = self.L = engine.L
+        ed = engine.edges
+        h = ctypes.c_void_p(0)
+        _native.check(L.ghs_solver_create(ed.n, ed.m, _ptr(ed.u), _ptr(ed.v), _ptr(engine.asrc), _ptr(engine.adst),
+                                          _ptr(engine.akey), engine.num_arcs, _ptr(engine.ws), engine.ws_bytes,
+                                          _ptr(engine.in_mst), _stream(), ctypes.byref(h)))
+        self.h = h
+        self.dense = torch.empty(max(ed.n, 1), dtype=torch.int64, device=ed.device)
+
+    def minedge(self):
+        c = ctypes.c_uint64(0)
+        _native.check(self.L.ghs_solver_minedge(self.h, ctypes.byref(c)))
+        return int(c.value)
+
+    def pack(self, count):
+        _native.check(self.L.ghs_solver_pack_best(self.h, _ptr(self.dense)))
+        return self.dense[:count]
+
+    def unpack(self, dense):
+        _native.check(self.L.ghs_solver_unpack_best(self.h, _ptr(dense)))
+
+    def contract(self):
+        d = ctypes.c_int(0)
+        _native.check(self.L.ghs_solver_contract(self.h, ctypes.byref(d)))
+        return bool(d.value)
+
+    def finish(self):
+        res = _native.Result()
+        stats = (_native.RoundStats * _native.GHS_MAX_ROUND_STATS)()
+        _native.check(self.L.ghs_solver_finish(self.h, ctypes.byref(res), stats))
+        return res, [stats[i].as_dict() for i in range(res.num_stats)]
+
+    def close(self):
+        if self.h:
+            self.L.ghs_solver_destroy(self.h)
+            self.h = ctypes.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def run_rounds(stepper, allreduce_min, max_rounds=64):
+    """The level loop shared by every backend: min-edge, all-reduce MIN, contract.
+
+    `allreduce_min(tensor)` reduces in place across ranks (identity for one rank). Returns the
+    number of rounds executed. Raises RuntimeError past `max_rounds` (hang guard; Boruvka needs
+    at most ceil(log2 n) + 1)."""
+    rounds = 0
+    while True:
+        count = stepper.minedge()
+        if count:
+            dense = stepper.pack(count)
+            allreduce_min(dense)
+            stepper.unpack(dense)
+        done = stepper.contract()
+        rounds += 1
+        if done:
+            return rounds
+        if rounds >= max_rounds:
+            raise RuntimeError("round cap exceeded")
+
+
+def torch_allreduce_min(group=None):
+    def fn(t):
+        if dist.is_initialized() and dist.get_world_size(group) > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return fn
+
+
+class DistributedMST:
+    """One rank's share of a multi-GPU MST over a replicated DeviceEdges graph."""
+
+    def __init__(self, edges, rank=None, world=None, group=None):
+        self.rank = dist.get_rank(group) if rank is None else rank
+        self.world = dist.get_world_size(group) if world is None else world
+        self.group = group
+        lo, hi = vertex_range(edges.n, self.rank, self.world)
+        self.engine = DeviceMST(edges, lo, hi)
+        self.edges = edges
+
+    def run(self):
+        """Arc build for the owned range + the round loop. Returns (Result, stats)."""
+        self.engine.build_arcs()
+        st = HipStepper(self.engine)
+        try:
+            run_rounds(st, torch_allreduce_min(self.group))
+            return st.finish()
+        finally:
+            st.close()
+
+    def in_mst_host(self):
+        return self.engine.in_mst_host()

@@ -1,0 +1,160 @@
+/*
+ * ghs_mst.h — C-ABI of the MI355X-native MST engine (libghs_mst.so).
+ *
+ * The reference (Trisanu-007/Distributed_GHS_Implementation) computes an MST with the GHS
+ * message protocol: one Python thread (ghs_implementation.py:46-413) or one MPI rank
+ * (ghs_implementation_mpi.py:37-757) per vertex exchanging CONNECT/INITIATE/TEST/ACCEPT/
+ * REJECT/REPORT/CHANGEROOT. It has no FFI; its path sits behind two call surfaces:
+ *   (1) GHSAlgorithm(num_nodes, edges).run(timeout) -> [(u, v)]   ghs_implementation.py:417-490
+ *   (2) MPINode(...).run() + collect_results() -> [(u, v, w)]       ghs_implementation_mpi.py:673-779
+ * This library replaces the protocol with a level-synchronous Boruvka fragment contraction
+ * (one GHS level == one Boruvka round) in hand-written gfx950 HIP kernels. Every entry point
+ * below names the reference interface it stands in for. Conventions:
+ *   - all functions return GHS_OK (0) or a negative GHS_E_* code and never abort;
+ *     ghs_last_error() returns a thread-local message for the last failure;
+ *   - "canonical edge list": u[e] < v[e] < n, strictly ascending (u, v), no duplicates;
+ *     eid = e. Ties resolve under the strict key (w, u, v) == (w, eid) — the order in which
+ *     NetworkX Kruskal (the reference's verifier, ghs_implementation.py:746) visits edges on a
+ *     canonically built graph. The result is a minimum spanning FOREST.
+ *   - d_* pointers are device pointers (HIP / torch device memory) on the current device;
+ *     `stream` is a hipStream_t passed as void* (NULL = default stream);
+ *   - 64-bit keys: key = (uint64)w << 32 | eid; UINT64_MAX = "no outgoing edge" (the
+ *     reference's best_weight = float('inf'), ghs_implementation.py:61).
+ */
+#ifndef GHS_MST_H
+#define GHS_MST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GHS_MST_ABI_VERSION 1
+
+#define GHS_OK 0
+#define GHS_E_ARG (-1)        /* bad argument (null pointer, size, alignment) */
+#define GHS_E_NONCANON (-2)   /* input edge list is not canonical */
+#define GHS_E_HIP (-3)        /* HIP runtime error */
+#define GHS_E_ROUNDCAP (-4)   /* round cap exceeded (never expected: hang guard) */
+#define GHS_E_NODEVICE (-5)   /* no usable gfx950 device */
+#define GHS_E_NOMEM (-6)      /* workspace too small / allocation failed */
+#define GHS_E_STATE (-7)      /* solver handle used out of order */
+
+#define GHS_MAX_ROUND_STATS 64
+
+/* Per-round record (one GHS level). */
+typedef struct ghs_round_stats {
+  uint64_t live_arcs;         /* arcs scanned by the min-edge kernel this round */
+  uint64_t active_components; /* fragments that searched for an outgoing edge */
+  uint64_t hooks;             /* fragments that merged (== MST edges added) */
+  float ms_minedge;           /* min-outgoing-edge (+ fused compaction) kernel */
+  float ms_hook;              /* hook (CONNECT) kernel */
+  float ms_jump;              /* pointer-jump relabel (INITIATE) kernel */
+  float ms_active;            /* next-fragment-list compaction kernel */
+} ghs_round_stats_t;
+
+typedef struct ghs_result {
+  uint64_t num_mst_edges;     /* n - (#components) */
+  uint64_t total_weight;      /* sum of w over MST edges */
+  uint32_t rounds;            /* Boruvka rounds (GHS levels) executed */
+  uint32_t num_stats;         /* entries filled in the stats array (<= GHS_MAX_ROUND_STATS) */
+  double ms_total;            /* wall time of the MST loop (device-resident input -> flags) */
+} ghs_result_t;
+
+/* ---- library / device ------------------------------------------------------------------- */
+int ghs_abi_version(void);
+const char *ghs_last_error(void);
+/* number of visible HIP devices (0 on a host without GPU; never an error) */
+int ghs_device_count(int *count);
+
+/* ---- host-buffer convenience -------------------------------------------------------------
+ * Replaces GHSAlgorithm.run (ghs_implementation.py:442-490: starts n threads, polls
+ * termination, sweeps BRANCH edges) and MPINode.run + collect_results
+ * (ghs_implementation_mpi.py:673-779). Input: canonical edge list on the HOST. Output:
+ * in_mst[e] = 1 iff canonical edge e is in the MSF (m bytes, host). Copies in/out, runs on the
+ * current device, serialised per process. stats may be NULL (else GHS_MAX_ROUND_STATS entries). */
+int ghs_mst_host(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t *v, const uint32_t *w,
+                 uint8_t *in_mst, ghs_result_t *result, ghs_round_stats_t *stats);
+
+/* ---- device-resident API -----------------------------------------------------------------
+ * The canonical device graph is the symmetric ARC list: each canonical edge (u, v, w) appears as
+ * arcs u->v and v->u, arcs grouped by source vertex (the per-node neighbour lists of the
+ * reference's node_<id>.json files, create_graph_files.py:56-74), with key = w<<32 | eid.
+ * SoA: asrc[A], adst[A] (uint32), akey[A] (uint64), A = 2m. Pointers must be 16-byte aligned. */
+
+/* temp bytes for ghs_build_arcs / ghs_build_arcs_range / ghs_count_arcs_range */
+size_t ghs_build_arcs_temp_bytes(uint32_t n, uint64_t m);
+/* number of arcs whose source lies in [src_lo, src_hi) (a rank's share for multi-GPU) */
+int ghs_count_arcs_range(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, uint32_t src_lo,
+                         uint32_t src_hi, void *d_temp, size_t temp_bytes, void *stream, uint64_t *num_arcs);
+/* arcs with source in [src_lo, src_hi) only, grouped by source; *num_arcs = count written.
+ * Multi-GPU ranks own disjoint source ranges, so every fragment's arcs are split over ranks
+ * and the per-round all-reduce MIN combines them. */
+int ghs_build_arcs_range(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
+                         uint32_t src_lo, uint32_t src_hi, uint32_t *d_asrc, uint32_t *d_adst, uint64_t *d_akey,
+                         uint64_t arc_capacity, void *d_temp, size_t temp_bytes, void *stream, uint64_t *num_arcs);
+/* canonical edges (device) -> symmetric arc list grouped by source (device). Validates
+ * canonicity on the device and returns GHS_E_NONCANON when it does not hold. */
+int ghs_build_arcs(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
+                   uint32_t *d_asrc, uint32_t *d_adst, uint64_t *d_akey, void *d_temp, size_t temp_bytes,
+                   void *stream);
+
+/* workspace bytes for ghs_mst_device / the solver handle; num_arcs = arcs this device scans */
+size_t ghs_workspace_bytes(uint32_t n, uint64_t m, uint64_t num_arcs);
+
+/* Whole MST on one device. d_u/d_v (canonical endpoints, m entries) are read by the hook stage
+ * to find the other fragment of a chosen edge; arcs as above; d_in_mst: m bytes (written).
+ * Blocks the calling thread until done (one host sync per round for the termination test). */
+int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v,
+                   const uint32_t *d_asrc, const uint32_t *d_adst, const uint64_t *d_akey, uint64_t num_arcs,
+                   void *d_workspace, size_t workspace_bytes, uint8_t *d_in_mst, void *stream,
+                   ghs_result_t *result, ghs_round_stats_t *stats);
+
+/* ---- stepwise solver (multi-GPU: one process per GPU, RCCL all-reduce between steps) ------
+ * Replaces the per-rank protocol loop of ghs_implementation_mpi.py:673-748 and its
+ * collectives (:907 bcast, :929 Barrier, :766 gather). Each rank scans ITS slice of the arc
+ * list; the per-fragment best keys are combined with an all-reduce MIN by the caller:
+ *   h = ghs_solver_create(...)
+ *   loop: ghs_solver_minedge(h, &C)            local min-edge per fragment
+ *         ghs_solver_pack_best(h, d_dense)     C int64 slots, order-preserving (key ^ 2^63)
+ *         <caller: all_reduce(d_dense[0:C], MIN)>
+ *         ghs_solver_unpack_best(h, d_dense)
+ *         ghs_solver_contract(h, &done)        hook + pointer-jump + next fragment list
+ *   ghs_solver_finish(h, result); ghs_solver_destroy(h)
+ * Identical inputs on every rank => identical hook decisions => replicated in_mst. */
+typedef struct ghs_solver ghs_solver_t;
+int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v,
+                      const uint32_t *d_asrc, const uint32_t *d_adst, const uint64_t *d_akey, uint64_t num_arcs,
+                      void *d_workspace, size_t workspace_bytes, uint8_t *d_in_mst, void *stream,
+                      ghs_solver_t **out);
+/* runs the min-edge kernel; *num_active = fragments whose best slot must be all-reduced */
+int ghs_solver_minedge(ghs_solver_t *h, uint64_t *num_active);
+int ghs_solver_pack_best(ghs_solver_t *h, int64_t *d_dense);
+int ghs_solver_unpack_best(ghs_solver_t *h, const int64_t *d_dense);
+/* hook + jump + next list; *done = 1 when no fragment has an outgoing edge */
+int ghs_solver_contract(ghs_solver_t *h, int *done);
+int ghs_solver_finish(ghs_solver_t *h, ghs_result_t *result, ghs_round_stats_t *stats);
+int ghs_solver_destroy(ghs_solver_t *h);
+
+/* ---- synthetic graph generators (device; BASELINE.json configs 3-5) ----------------------
+ * R-MAT (Graph500 A,B,C,D = .57,.19,.19,.05, edgefactor ef, 2^scale vertices, seeded vertex
+ * permutation), self-loops dropped, duplicates removed, canonical order, unique weights
+ * w = bijective_hash32(eid ^ wseed) (distinct by construction). d_u/d_v/d_w must hold
+ * edgefactor * 2^scale entries (the tuple count, an upper bound); *m_out = canonical edge count.
+ * d_temp: ghs_rmat_temp_bytes(scale, edgefactor) bytes. */
+size_t ghs_rmat_temp_bytes(uint32_t scale, uint32_t edgefactor);
+int ghs_rmat_generate(uint32_t scale, uint32_t edgefactor, uint64_t seed, uint64_t wseed,
+                      uint32_t *d_u, uint32_t *d_v, uint32_t *d_w, uint64_t *m_out,
+                      void *d_temp, size_t temp_bytes, void *stream);
+/* k x k grid, vertex r*k+c, right + down edges (m = 2k(k-1)), canonical order.
+ * mode 0: unique hashed weights; mode 1: "road-like" gradient weights w = eid (unique, forces
+ * long hook chains). */
+int ghs_grid_generate(uint32_t k, uint32_t mode, uint64_t wseed, uint32_t *d_u, uint32_t *d_v, uint32_t *d_w,
+                      void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GHS_MST_H */

@@ -1,0 +1,88 @@
+"""Host logic of the product package (no GPU): canonicalisation, reference file formats,
+binary format, result schema. Checked against the oracle's independent restatement."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, fixture_names, load_fixture
+from distributed_ghs_implementation_amd import graph as G
+from oracle import oracle
+
+
+@pytest.mark.parametrize("name", fixture_names())
+def test_canonicalize_matches_oracle(name):
+    fx = load_fixture(name)
+    g = G.canonicalize(fx["num_nodes"], edges=fx["edges"])
+    assert g.edge_triples() == oracle.canonicalize_py(fx["num_nodes"], fx["edges"])
+    g.check()
+
+
+def test_canonicalize_random_duplicates_last_write_wins():
+    rng = random.Random(3)
+    for _ in range(50):
+        n = rng.randint(1, 30)
+        edges = [(rng.randrange(n), rng.randrange(n), rng.randint(0, 5)) for _ in range(rng.randint(0, 80))]
+        g = G.canonicalize(n, edges=edges)
+        assert g.edge_triples() == oracle.canonicalize_py(n, edges)
+
+
+def test_canonicalize_validation():
+    with pytest.raises(ValueError):
+        G.canonicalize(3, edges=[(0, 3, 1)])
+    with pytest.raises(ValueError):
+        G.canonicalize(3, edges=[(0, 1, -1)])
+    with pytest.raises(ValueError):
+        G.canonicalize(3, edges=[(0, 1, 1.5)])
+    with pytest.raises(ValueError):
+        G.canonicalize(3, edges=[(0, 1, 1 << 32)])
+    g = G.canonicalize(3, edges=[(0, 1, 2.0)])
+    assert g.edge_triples() == [(0, 1, 2)]
+    assert G.canonicalize(0, edges=[]).m == 0
+
+
+def test_read_reference_graph_dir():
+    # directory written by the reference's own create_node_files (create_graph_files.py:43-89)
+    d = os.path.join(GOLDEN, "graph_data_n6")
+    g = G.read_graph_dir(d)
+    fx = load_fixture("cgf_n6.json")
+    assert g.n == 6 and g.edge_triples() == oracle.canonicalize_py(6, fx["edges"])
+    g2 = G.read_node_files(d)  # the MPI ranks' view (ghs_implementation_mpi.py:74-92)
+    assert g2.edge_triples() == g.edge_triples()
+
+
+def test_write_graph_dir_roundtrip(tmp_path):
+    fx = load_fixture("thread_cfg5.json")
+    g = G.canonicalize(fx["num_nodes"], edges=fx["edges"])
+    G.write_graph_dir(g, str(tmp_path))
+    assert G.read_graph_dir(str(tmp_path)).edge_triples() == g.edge_triples()
+    os.remove(tmp_path / "graph_metadata.json")
+    assert G.read_graph_dir(str(tmp_path)).edge_triples() == g.edge_triples()
+    node0 = json.load(open(tmp_path / "node_0.json"))
+    assert set(node0) == {"node_id", "neighbors", "num_neighbors"}
+
+
+def test_missing_graph_dir_raises(tmp_path):
+    with pytest.raises(FileNotFoundError):
+        G.read_graph_dir(str(tmp_path))
+
+
+def test_mstbin_roundtrip(tmp_path):
+    fx = load_fixture("ties_4.json")
+    g = G.canonicalize(fx["num_nodes"], edges=fx["edges"])
+    p = str(tmp_path / "g.mstbin")
+    G.write_mstbin(p, g)
+    h = G.read_mstbin(p)
+    assert h.n == g.n and np.array_equal(h.u, g.u) and np.array_equal(h.v, g.v) and np.array_equal(h.w, g.w)
+
+
+def test_result_schema(tmp_path):
+    res = G.write_result(str(tmp_path / "ghs_mst.json"), [(3, 5, 2), (0, 2, 2), (0, 3, 1)])
+    on_disk = json.load(open(tmp_path / "ghs_mst.json"))
+    assert on_disk == res
+    # same keys as ghs_implementation_mpi.py:811-816
+    assert set(res) == {"mst_edges", "total_weight", "num_edges", "algorithm"}
+    assert res["mst_edges"] == [[0, 2, 2], [0, 3, 1], [3, 5, 2]]
+    assert res["total_weight"] == 5 and res["num_edges"] == 3
