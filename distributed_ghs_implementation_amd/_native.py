@@ -31,8 +31,9 @@ _ERR_NAMES = {
 # every symbol include/ghs_mst.h declares (tests check the .so exports all of them)
 EXPORTED_SYMBOLS = (
     "ghs_abi_version", "ghs_last_error", "ghs_device_count", "ghs_mst_host",
+    "ghs_default_config", "ghs_workspace_bytes", "ghs_mst_device",
     "ghs_build_arcs_temp_bytes", "ghs_count_arcs_range", "ghs_build_arcs_range", "ghs_build_arcs",
-    "ghs_workspace_bytes", "ghs_mst_device",
+    "ghs_check_canonical",
     "ghs_solver_create", "ghs_solver_minedge", "ghs_solver_pack_best", "ghs_solver_unpack_best",
     "ghs_solver_contract", "ghs_solver_finish", "ghs_solver_destroy",
     "ghs_rmat_temp_bytes", "ghs_rmat_generate", "ghs_grid_generate",
@@ -49,6 +50,9 @@ class GHSError(RuntimeError):
 
 class RoundStats(ctypes.Structure):
     _fields_ = [
+        ("level", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+        ("level_arcs", ctypes.c_uint64),
         ("live_arcs", ctypes.c_uint64),
         ("active_components", ctypes.c_uint64),
         ("hooks", ctypes.c_uint64),
@@ -59,7 +63,7 @@ class RoundStats(ctypes.Structure):
     ]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
 
 
 class Result(ctypes.Structure):
@@ -68,8 +72,32 @@ class Result(ctypes.Structure):
         ("total_weight", ctypes.c_uint64),
         ("rounds", ctypes.c_uint32),
         ("num_stats", ctypes.c_uint32),
+        ("levels", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
         ("ms_total", ctypes.c_double),
     ]
+
+
+class Config(ctypes.Structure):
+    """ghs_config_t: the weight-level plan of the filter (speed only; results never change)."""
+    _fields_ = [
+        ("max_levels", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+        ("level1_edges_per_vertex", ctypes.c_double),
+        ("level_growth", ctypes.c_double),
+    ]
+
+
+def make_config(max_levels=None, level1_edges_per_vertex=None, level_growth=None):
+    c = Config()
+    load().ghs_default_config(ctypes.byref(c))
+    if max_levels is not None:
+        c.max_levels = int(max_levels)
+    if level1_edges_per_vertex is not None:
+        c.level1_edges_per_vertex = float(level1_edges_per_vertex)
+    if level_growth is not None:
+        c.level_growth = float(level_growth)
+    return c
 
 
 _lib = None
@@ -82,6 +110,13 @@ def load():
     with _lock:
         if _lib is not None:
             return _lib
+        # Load torch's HIP runtime first when torch is installed: libghs_mst.so then binds to the
+        # same libamdhip64.so.7 (same SONAME) instead of bringing up a second runtime, so torch's
+        # device pointers and streams are valid in both.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError(
                 f"libghs_mst.so not found at {LIB_PATH}; build it with "
@@ -94,13 +129,15 @@ def load():
             "ghs_last_error": (ctypes.c_char_p, []),
             "ghs_device_count": (i32, [P(i32)]),
             "ghs_mst_host": (i32, [u32, u64, vp, vp, vp, vp, P(Result), P(RoundStats)]),
+            "ghs_default_config": (None, [P(Config)]),
+            "ghs_check_canonical": (i32, [u32, u64, vp, vp, vp, P(i32)]),
             "ghs_build_arcs_temp_bytes": (sz, [u32, u64]),
             "ghs_count_arcs_range": (i32, [u32, u64, vp, vp, u32, u32, vp, sz, vp, P(u64)]),
             "ghs_build_arcs_range": (i32, [u32, u64, vp, vp, vp, u32, u32, vp, vp, vp, u64, vp, sz, vp, P(u64)]),
             "ghs_build_arcs": (i32, [u32, u64, vp, vp, vp, vp, vp, vp, vp, sz, vp]),
             "ghs_workspace_bytes": (sz, [u32, u64, u64]),
-            "ghs_mst_device": (i32, [u32, u64, vp, vp, vp, vp, vp, u64, vp, sz, vp, vp, P(Result), P(RoundStats)]),
-            "ghs_solver_create": (i32, [u32, u64, vp, vp, vp, vp, vp, u64, vp, sz, vp, vp, P(vp)]),
+            "ghs_mst_device": (i32, [u32, u64, vp, vp, vp, P(Config), vp, sz, vp, vp, P(Result), P(RoundStats)]),
+            "ghs_solver_create": (i32, [u32, u64, vp, vp, vp, u64, u64, P(Config), vp, sz, vp, vp, P(vp)]),
             "ghs_solver_minedge": (i32, [vp, P(u64)]),
             "ghs_solver_pack_best": (i32, [vp, vp]),
             "ghs_solver_unpack_best": (i32, [vp, vp]),

@@ -1,5 +1,5 @@
 // Level-synchronous Boruvka fragment contraction on gfx950 — the MI355X restatement of the
-// reference's GHS level loop. One round here == one GHS level of the reference:
+// reference's GHS level loop. One Boruvka round here == one GHS level of the reference:
 //
 //   reference (thread / MPI path)                               this file
 //   test/handle_test/accept/reject/report/handle_report         k_minedge: every fragment's minimum
@@ -11,34 +11,54 @@
 //                                                                 smaller label is the new core
 //   handle_initiate broadcast of the new fragment id             k_jump: pointer jumping to the root
 //     (:201-233; _mpi:289-351)
-//   termination (:389-413, :492-552; _mpi:685-743)               k_flag_next + select: fragments with an
-//                                                                 outgoing edge; none left => done
+//   termination (:389-413, :492-552; _mpi:685-743)               k_flag_next + select: fragments with
+//                                                                 an outgoing edge; none left => done
 //   BRANCH sweep u<v (:481-490; _mpi:750-779)                    in_mst[eid] set by k_hook
 //
-// Data layout in HBM (all SoA, 256-B aligned):
-//   arcs   src[A] u32 | dst[A] u32 | key[A] u64     key = w << 32 | eid, grouped by src
-//   lab[n]  u32  fragment label map (see "label invariant" below)
-//   best[n] u64  per-fragment minimum outgoing key (atomicMin target)
-//   par[n]  u32  hook parent
-//   act[2][n] u32 active fragment lists (double buffer)
-//   arc double buffers for the compacted, relabelled arcs of rounds >= 2
+// Weight levels (filter). The rounds run on one WEIGHT LEVEL of the edges at a time, lightest
+// level first: level i holds the canonical edges with tau_{i-1} <= w < tau_i. Kruskal's order
+// makes MSF(G) restricted to keys < tau exactly the MSF of the lighter levels, so once a level
+// has run to completion its fragments are final for every lighter edge, and an edge of a later
+// level whose ends already share a fragment can never enter the MSF (cycle property). The
+// level pass (k_level_select) drops those edges BEFORE they are ever turned into arcs: the
+// reference's REJECT, applied to a whole weight class at once. On R-MAT most heavy edges fall
+// inside the giant fragment; they are rejected through a 1-bit-per-vertex membership bitmap
+// (n/8 bytes: 2 MiB at scale 24, resident in every XCD's 4 MiB L2) instead of a 64 MiB label
+// gather.
 //
-// Label invariant. Round 1 scans the input arcs with the identity labelling. From round 2 on
-// the min-edge kernel rewrites every surviving arc as (lab[src], lab[dst], key), so the arcs of
-// round r carry the labels of the fragments that were active at the START of round r-1, and
-// lab[x] for exactly those labels is refreshed every round to the current root (k_jump).
-// A vertex's current fragment is found by following lab[] to a fixpoint (find_lab): roots
-// satisfy lab[x] == x, and the chain is at most one hop longer per round.
+// Data layout in HBM (SoA, 256-B aligned carves of one workspace):
+//   canonical edges  u[m] v[m] w[m] u32 (caller's)         eid = position, key = w << 32 | eid
+//   arcs X / Y       src[C] dst[C] u32, key[C] u64        a level's arcs, grouped by source
+//   segments X / Y   start[G] count[G] prefix[G+1] u64    block-private output regions
+//   lab[n] u32  fragment label map        best[n] u64  per-fragment min outgoing key
+//   par[n] u32  hook parent               act[2][n] u32 active fragment lists
+//   flags[n] u8 select flags              bits[n/64] u64 giant-fragment bitmap
+//
+// Compaction without hot atomics. A compacting kernel runs a fixed grid of G blocks; block b
+// owns a contiguous virtual input range and writes its survivors, in order, to the FRONT of the
+// same range of the output buffer, then records its count (padded to a multiple of 4 with dead
+// arcs, so every 4-arc group stays 16-B aligned). The next round reads these G segments through
+// the prefix table. No same-address atomics (they serialise at ~12 ns each on MI355X, measured),
+// and the output is deterministic.
+//
+// Label invariant. Each level's arcs carry the fragment roots current at the level start
+// (lab[root] == root), so a level's first round needs no gathers. From its second round on, the
+// min-edge kernel rewrites surviving arcs as (lab[src], lab[dst], key): arcs of round r carry the
+// labels of the fragments active at the start of round r-1, and lab[x] for exactly those labels
+// is refreshed every round by k_jump. A vertex's fragment is found by following lab[] to a
+// fixpoint (find_lab); k_resolve compresses every vertex to its root between levels.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
-
-#include <hipcub/hipcub.hpp>
 
 #include "common.h"
 
@@ -47,75 +67,137 @@ namespace ghs {
 static thread_local std::string g_err;
 void set_error(const std::string &msg) { g_err = msg; }
 
-__device__ __forceinline__ uint32_t wave_prefix_count(uint64_t ballot) {
-  // number of set bits of `ballot` in lanes below this one
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(ballot >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ballot, 0u));
-}
+constexpr uint32_t SEG_G = 2048;   // blocks of a compacting kernel (8 per CU) = output segments
+constexpr int FIND_LAB_MAX_HOPS = 256;
+constexpr uint32_t JUMP_MAX_STEPS = 1u << 26;
 
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
+// Block-wide exclusive offsets for a compaction step: each lane contributes `mine` items and
+// gets the count of items of lower lanes of the whole block; *total = block total.
+// Every thread of the block must call it (two barriers).
+__device__ __forceinline__ uint32_t block_offsets(uint32_t mine, uint32_t *s_wcnt, uint32_t *total) {
+  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+  uint32_t incl = mine;
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const uint32_t o = __shfl_up(incl, d);
+    if (lane >= d) incl += o;
+  }
+  if (lane == WAVE - 1) s_wcnt[wid] = incl;
+  __syncthreads();
+  uint32_t before = incl - mine, t = 0;
+#pragma unroll
+  for (int w = 0; w < BLOCK / WAVE; ++w) {
+    if (w < wid) before += s_wcnt[w];
+    t += s_wcnt[w];
+  }
+  *total = t;
+  __syncthreads();
+  return before;
+}
+
 // ------------------------------------------------------------------------------------------
-// Stage 1: minimum outgoing edge per fragment (+ fused self-loop filter / stream compaction).
+// Segmented input: virtual index v in [0, total) lives in segment s with
+// prefix[s] <= v < prefix[s+1], physical index start[s] + (v - prefix[s]).
+// ------------------------------------------------------------------------------------------
+struct SegView {
+  const uint64_t *start;
+  const uint64_t *prefix;  // nseg + 1 entries
+  uint32_t nseg;
+  uint64_t total;
+};
+
+__device__ __forceinline__ uint32_t seg_find(const uint64_t *__restrict__ prefix, uint32_t lo, uint32_t hi, uint64_t v) {
+  // largest s in [lo, hi] with prefix[s] <= v
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (prefix[mid] <= v) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// ------------------------------------------------------------------------------------------
+// Stage 1: minimum outgoing edge per fragment (+ fused REJECT filter / stream compaction).
 //
 // Each lane owns 4 consecutive arcs (16-B loads of src/dst, 2x16-B of key). Arcs are grouped by
 // source, so equal source labels form runs; a wave-wide segmented min-scan over its 256 arcs
 // (in-lane serial + 6-step cross-lane scan) leaves one candidate per run, and only run tails
-// touch best[] — with a plain read first, since best only ever decreases (a stale read can only
-// be larger than the true value, so skipping on `best <= cand` is always correct).
-// IDENT: round 1, labels are vertex ids (no gathers, dst not read). COMPACT: write surviving
-// arcs relabelled; block-local order is preserved, blocks claim output ranges atomically.
+// touch best[] — after a plain read, since best only ever decreases (a stale read is never
+// smaller than the true value, so skipping on `best <= cand` is always safe).
+// IDENT: labels are already current roots (a level's first round): no gathers, dst not read.
+// COMPACT: survivors (inter-fragment arcs) are written relabelled to this block's output segment.
+// Dead arcs (src == LABEL_NONE) pad segments and are skipped.
 // ------------------------------------------------------------------------------------------
 template <bool IDENT, bool COMPACT>
 __global__ __launch_bounds__(BLOCK) void k_minedge(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
-                                                   const uint64_t *__restrict__ key, uint64_t A,
+                                                   const uint64_t *__restrict__ key, SegView in,
                                                    const uint32_t *__restrict__ lab, uint64_t *__restrict__ best,
                                                    uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
-                                                   uint64_t *__restrict__ okey, unsigned long long *__restrict__ out_count) {
+                                                   uint64_t *__restrict__ okey, uint64_t *__restrict__ oseg_start,
+                                                   uint64_t *__restrict__ oseg_count) {
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
-  __shared__ unsigned long long s_base;
+  __shared__ uint32_t s_seg[2];
   const int lane = threadIdx.x & (WAVE - 1);
-  const int wid = threadIdx.x / WAVE;
-  const uint64_t nchunks = (A + ARCS_PER_BLOCK - 1) / ARCS_PER_BLOCK;
+  const uint64_t T = in.total;
+  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;  // multiple of 4
+  const uint64_t vb = Q * blockIdx.x;
+  const uint64_t ve = (vb + Q < T) ? vb + Q : T;
+  if (threadIdx.x == 0) {
+    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
+    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
+  }
+  __syncthreads();
+  const uint32_t slo = s_seg[0], shi = s_seg[1];
+  uint64_t out_n = 0;  // survivors written so far by this block
 
-  for (uint64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
-    const uint64_t i0 = chunk * ARCS_PER_BLOCK + (uint64_t)threadIdx.x * ARCS_PER_THREAD;
+  for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
+    const uint64_t v = v0 + (uint64_t)threadIdx.x * ARCS_PER_THREAD;
     uint32_t L[4], D[4];
     uint64_t K[4];
     bool valid[4];
-    if (i0 + 4 <= A) {
-      const uint4 s4 = *reinterpret_cast<const uint4 *>(src + i0);
-      L[0] = s4.x; L[1] = s4.y; L[2] = s4.z; L[3] = s4.w;
-      if (!IDENT) {
-        const uint4 d4 = *reinterpret_cast<const uint4 *>(dst + i0);
-        D[0] = d4.x; D[1] = d4.y; D[2] = d4.z; D[3] = d4.w;
-      }
-      const ulonglong2 k01 = *reinterpret_cast<const ulonglong2 *>(key + i0);
-      const ulonglong2 k23 = *reinterpret_cast<const ulonglong2 *>(key + i0 + 2);
-      K[0] = k01.x; K[1] = k01.y; K[2] = k23.x; K[3] = k23.y;
+    if (v < ve) {
+      const uint32_t s = (slo == shi) ? slo : seg_find(in.prefix, slo, shi, v);
+      const uint64_t seg_end = in.prefix[s + 1];
+      const uint64_t i0 = in.start[s] + (v - in.prefix[s]);
+      if (v + 4 <= seg_end && v + 4 <= ve && (i0 & 3) == 0) {
+        const uint4 s4 = *reinterpret_cast<const uint4 *>(src + i0);
+        L[0] = s4.x; L[1] = s4.y; L[2] = s4.z; L[3] = s4.w;
+        if (!IDENT) {
+          const uint4 d4 = *reinterpret_cast<const uint4 *>(dst + i0);
+          D[0] = d4.x; D[1] = d4.y; D[2] = d4.z; D[3] = d4.w;
+        }
+        const ulonglong2 k01 = *reinterpret_cast<const ulonglong2 *>(key + i0);
+        const ulonglong2 k23 = *reinterpret_cast<const ulonglong2 *>(key + i0 + 2);
+        K[0] = k01.x; K[1] = k01.y; K[2] = k23.x; K[3] = k23.y;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) valid[j] = true;
+        for (int j = 0; j < 4; ++j) valid[j] = L[j] != LABEL_NONE;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool in_range = v + j < ve && v + j < seg_end;
+          L[j] = in_range ? src[i0 + j] : LABEL_NONE;
+          D[j] = (!IDENT && in_range) ? dst[i0 + j] : 0u;
+          K[j] = in_range ? key[i0 + j] : KEY_NONE;
+          valid[j] = L[j] != LABEL_NONE;
+        }
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        valid[j] = i0 + j < A;
-        L[j] = valid[j] ? src[i0 + j] : 0u;
-        D[j] = (!IDENT && valid[j]) ? dst[i0 + j] : 0u;
-        K[j] = valid[j] ? key[i0 + j] : KEY_NONE;
+        L[j] = LABEL_NONE; D[j] = 0; K[j] = KEY_NONE; valid[j] = false;
       }
     }
     uint64_t V[4];
     if (IDENT) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        V[j] = valid[j] ? K[j] : KEY_NONE;  // canonical arcs are never self-loops
-        L[j] = valid[j] ? L[j] : LABEL_NONE;
-      }
+      for (int j = 0; j < 4; ++j) V[j] = valid[j] ? K[j] : KEY_NONE;  // level arcs: src != dst
     } else {
       uint32_t cs[4], cd[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {  // 8 independent gathers in flight per lane
-        cs[j] = lab[L[j]];
-        cd[j] = lab[D[j]];
+        cs[j] = lab[valid[j] ? L[j] : 0u];
+        cd[j] = lab[valid[j] ? D[j] : 0u];
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -125,7 +207,7 @@ __global__ __launch_bounds__(BLOCK) void k_minedge(const uint32_t *__restrict__ 
       }
     }
 
-    // ---- wave-wide segmented min over the 256 arcs, segments = runs of equal source label
+    // ---- wave-wide segmented min over 256 arcs, segments = runs of equal source label
     const uint32_t prevL3 = __shfl_up(L[3], 1);
     bool H[4];
     H[0] = (lane == 0) || (L[0] != prevL3);
@@ -162,25 +244,12 @@ __global__ __launch_bounds__(BLOCK) void k_minedge(const uint32_t *__restrict__ 
     }
 
     if (COMPACT) {
-      // ---- ballot + prefix-sum stream compaction of inter-fragment arcs (REJECT filter)
-      uint32_t before = 0, wave_total = 0;
+      uint32_t mine = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint64_t b = __ballot(V[j] != KEY_NONE);
-        before += wave_prefix_count(b);
-        wave_total += (uint32_t)__popcll(b);
-      }
-      if (lane == 0) s_wcnt[wid] = wave_total;
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        uint32_t t = 0;
-#pragma unroll
-        for (int w = 0; w < BLOCK / WAVE; ++w) t += s_wcnt[w];
-        s_base = t ? atomicAdd(out_count, (unsigned long long)t) : 0ull;
-      }
-      __syncthreads();
-      uint64_t pos = s_base + before;
-      for (int w = 0; w < wid; ++w) pos += s_wcnt[w];
+      for (int j = 0; j < 4; ++j) mine += (V[j] != KEY_NONE) ? 1u : 0u;
+      uint32_t total;
+      const uint32_t before = block_offsets(mine, s_wcnt, &total);
+      uint64_t pos = vb + out_n + before;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (V[j] != KEY_NONE) {
@@ -190,15 +259,52 @@ __global__ __launch_bounds__(BLOCK) void k_minedge(const uint32_t *__restrict__ 
           ++pos;
         }
       }
-      __syncthreads();
+      out_n += total;
+    }
+  }
+  if (COMPACT) {
+    // pad to a multiple of 4 with dead arcs; stays inside [vb, vb + Q) and below the capacity
+    // (the workspace reserves 4 * SEG_G spare arcs)
+    const uint64_t padded = (out_n + 3) & ~3ull;
+    if (threadIdx.x < padded - out_n) {
+      const uint64_t pos = vb + out_n + threadIdx.x;
+      osrc[pos] = LABEL_NONE;
+      odst[pos] = 0;
+      okey[pos] = KEY_NONE;
+    }
+    if (threadIdx.x == 0) {
+      oseg_start[blockIdx.x] = vb;
+      oseg_count[blockIdx.x] = (vb < T) ? padded : 0;
     }
   }
 }
 
-// Bounded walks: a chain longer than these bounds means a broken invariant; the kernel sets
-// the error word (checked by the host after every round) instead of spinning forever.
-constexpr int FIND_LAB_MAX_HOPS = 256;        // >= rounds + 2 (rounds <= 64)
-constexpr uint32_t JUMP_MAX_STEPS = 1u << 26;
+// exclusive scan of count[0..n) into prefix[0..n]; one block of 1024 threads
+__global__ __launch_bounds__(1024) void k_scan_counts(const uint64_t *__restrict__ count, uint32_t n,
+                                                      uint64_t *__restrict__ prefix, unsigned long long *__restrict__ total) {
+  __shared__ uint64_t s_part[1024];
+  const uint32_t per = (n + 1023) / 1024;
+  const uint32_t b = threadIdx.x * per;
+  uint64_t sum = 0;
+  for (uint32_t i = 0; i < per && b + i < n; ++i) sum += count[b + i];
+  s_part[threadIdx.x] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const uint64_t o = threadIdx.x >= (unsigned)d ? s_part[threadIdx.x - d] : 0;
+    __syncthreads();
+    s_part[threadIdx.x] += o;
+    __syncthreads();
+  }
+  uint64_t run = s_part[threadIdx.x] - sum;
+  for (uint32_t i = 0; i < per && b + i < n; ++i) {
+    prefix[b + i] = run;
+    run += count[b + i];
+  }
+  if (threadIdx.x == 1023) {
+    prefix[n] = s_part[1023];
+    *total = s_part[1023];
+  }
+}
 
 __device__ __forceinline__ uint32_t find_lab(const uint32_t *__restrict__ lab, uint32_t x,
                                              unsigned long long *__restrict__ err) {
@@ -218,9 +324,9 @@ __device__ __forceinline__ uint32_t find_lab(const uint32_t *__restrict__ lab, u
 // ------------------------------------------------------------------------------------------
 // Stage 2: hook (CONNECT over the best edge). act == nullptr => fragments are 0..nact-1.
 // Strict total order on keys => the hook graph's only cycles are mutual pairs; the smaller
-// label stays root (the reference merges equal-level fragments on a shared core edge,
-// ghs_implementation.py:186-196, and picks the initiator by (fragment_id, rank),
-// ghs_implementation_mpi.py:237-239). Every hook adds exactly one MSF edge.
+// label stays root (the reference merges equal-level fragments over a shared core edge,
+// ghs_implementation.py:186-196, initiator by (fragment_id, rank), ghs_implementation_mpi.py:
+// 237-239). Every hook adds exactly one MSF edge; one pair of atomics per block for the totals.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act, uint64_t nact,
                                                 const uint64_t *__restrict__ best, const uint32_t *__restrict__ lab,
@@ -228,45 +334,57 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
                                                 uint32_t *__restrict__ par, uint8_t *__restrict__ in_mst,
                                                 unsigned long long *__restrict__ acc /* [0] weight, [1] edges */,
                                                 unsigned long long *__restrict__ err) {
-  for (uint64_t i = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; i - threadIdx.x < nact;
-       i += (uint64_t)gridDim.x * BLOCK) {
-    unsigned long long wsum = 0, cnt = 0;
-    if (i < nact) {
-      const uint32_t c = act ? act[i] : (uint32_t)i;
-      const uint64_t k = best[c];
-      uint32_t p = c;
-      if (k != KEY_NONE) {
-        const uint32_t eid = (uint32_t)k;
-        const uint32_t la = find_lab(lab, eu[eid], err);
-        const uint32_t lb = find_lab(lab, ev[eid], err);
-        if (la != c && lb != c) atomicOr(err, 2ull);  // the chosen edge must leave c
-        const uint32_t other = (la == c) ? lb : la;
-        const bool mutual = best[other] == k;
-        if (!(mutual && c < other)) {
-          p = other;
-          in_mst[eid] = 1;
-          wsum = k >> 32;
-          cnt = 1;
-        }
+  __shared__ unsigned long long s_w[BLOCK / WAVE], s_c[BLOCK / WAVE];
+  unsigned long long wsum = 0, cnt = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; i < nact; i += (uint64_t)gridDim.x * BLOCK) {
+    const uint32_t c = act ? act[i] : (uint32_t)i;
+    const uint64_t k = best[c];
+    uint32_t p = c;
+    if (k != KEY_NONE) {
+      const uint32_t eid = (uint32_t)k;
+      const uint32_t la = find_lab(lab, eu[eid], err);
+      const uint32_t lb = find_lab(lab, ev[eid], err);
+      if (la != c && lb != c) atomicOr(err, 2ull);  // the chosen edge must leave c
+      const uint32_t other = (la == c) ? lb : la;
+      const bool mutual = best[other] == k;
+      if (!(mutual && c < other)) {
+        p = other;
+        in_mst[eid] = 1;
+        wsum += k >> 32;
+        cnt += 1;
       }
-      par[c] = p;
     }
+    par[c] = p;
+  }
 #pragma unroll
-    for (int d = WAVE / 2; d > 0; d >>= 1) {
-      wsum += __shfl_xor(wsum, d);
-      cnt += __shfl_xor(cnt, d);
+  for (int d = WAVE / 2; d > 0; d >>= 1) {
+    wsum += __shfl_xor(wsum, d);
+    cnt += __shfl_xor(cnt, d);
+  }
+  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+  if (lane == 0) {
+    s_w[wid] = wsum;
+    s_c[wid] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long tw = 0, tc = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / WAVE; ++w) {
+      tw += s_w[w];
+      tc += s_c[w];
     }
-    if ((threadIdx.x & (WAVE - 1)) == 0 && cnt) {
-      atomicAdd(acc + 0, wsum);
-      atomicAdd(acc + 1, cnt);
+    if (tc) {
+      atomicAdd(acc + 0, tw);
+      atomicAdd(acc + 1, tc);
     }
   }
 }
 
 // ------------------------------------------------------------------------------------------
 // Stage 3: pointer jumping (INITIATE broadcast of the new fragment id). Path splitting on par:
-// concurrent compression only ever moves a pointer to an ancestor, so stale reads are still
-// valid ancestors and every walk ends at its root. lab[c] = root.
+// concurrent compression only moves a pointer to an ancestor, so stale reads are still valid
+// ancestors and every walk ends at its root. lab[c] = root.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act, uint64_t nact, uint32_t *par,
                                                 uint32_t *__restrict__ lab, unsigned long long *__restrict__ err) {
@@ -290,12 +408,11 @@ __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act
 }
 
 // ------------------------------------------------------------------------------------------
-// Stage 3b: next active fragment list = roots that still had an outgoing edge; reset their
-// best slot. (A root with no outgoing edge is a finished MSF component: the reference's
-// "best_weight == inf at the core => terminate", ghs_implementation.py:316-320.)
-// The list itself is produced by an order-preserving select (hipcub::DeviceSelect::Flagged),
-// so every rank of a multi-GPU run holds the same list in the same order — the all-reduce
-// slots line up without any exchange of the list.
+// Stage 3b: flags of the next active fragment list = roots that still had an outgoing edge
+// (their best slot is reset). A root with no outgoing edge is finished for this level (the
+// reference: "best_weight == inf at the core => terminate", ghs_implementation.py:316-320).
+// The list is produced by an order-preserving select, so every rank of a multi-GPU run holds
+// the same list in the same order and the all-reduce slots line up.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(BLOCK) void k_flag_next(const uint32_t *__restrict__ act, uint64_t nact,
                                                      const uint32_t *__restrict__ par, uint64_t *__restrict__ best,
@@ -308,9 +425,163 @@ __global__ __launch_bounds__(BLOCK) void k_flag_next(const uint32_t *__restrict_
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Between levels: compress every vertex to its root (lab[v] = find(v)) and flag the roots.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(BLOCK) void k_resolve(uint32_t n, uint32_t *lab, uint8_t *__restrict__ root_flag,
+                                                   unsigned long long *__restrict__ err) {
+  for (uint64_t v = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; v < n; v += (uint64_t)gridDim.x * BLOCK) {
+    const uint32_t r = find_lab(lab, (uint32_t)v, err);
+    lab[v] = r;
+    root_flag[v] = (r == (uint32_t)v) ? 1 : 0;
+  }
+}
+
+// giant-fragment membership bitmap: bit v = (lab[v] == giant); one u64 word per wave
+__global__ __launch_bounds__(BLOCK) void k_bitmap(uint32_t n, const uint32_t *__restrict__ lab, uint32_t giant,
+                                                  uint64_t *__restrict__ bits) {
+  const uint64_t words = ((uint64_t)n + 63) / 64;
+  for (uint64_t base = blockIdx.x * (uint64_t)BLOCK; base < (uint64_t)n; base += (uint64_t)gridDim.x * BLOCK) {
+    const uint64_t v = base + threadIdx.x;
+    const bool in = v < n && lab[v] == giant;
+    const uint64_t b = __ballot(in);
+    if ((threadIdx.x & (WAVE - 1)) == 0 && (v >> 6) < words) bits[v >> 6] = b;
+  }
+}
+
+__global__ void k_sample_labels(uint32_t n, const uint32_t *__restrict__ lab, uint32_t nsamp, uint32_t *__restrict__ out) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsamp; i += gridDim.x * blockDim.x) {
+    const uint64_t v = ((uint64_t)i * n) / nsamp;
+    out[i] = lab[v < n ? v : n - 1];
+  }
+}
+
+__global__ void k_sample_weights(uint64_t cnt, const uint32_t *__restrict__ w, uint32_t nsamp, uint32_t *__restrict__ out) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsamp; i += gridDim.x * blockDim.x) {
+    const uint64_t e = ((uint64_t)i * cnt) / nsamp;
+    out[i] = w[e];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Level pass: canonical edges e in [e_lo, e_hi) with w_lo <= w < w_hi whose ends lie in
+// different fragments -> (lab[u], lab[v], key) into this block's staging region (block-private,
+// deterministic). FILTER = false for the first level (every vertex is its own fragment).
+// lab is fully resolved (one hop) when this runs.
+// ------------------------------------------------------------------------------------------
+template <bool FILTER>
+__global__ __launch_bounds__(BLOCK) void k_level_select(uint64_t e_lo, uint64_t e_hi, const uint32_t *__restrict__ eu,
+                                                        const uint32_t *__restrict__ ev, const uint32_t *__restrict__ ew,
+                                                        uint32_t w_lo, uint64_t w_hi, const uint32_t *__restrict__ lab,
+                                                        const uint64_t *__restrict__ giant_bits,
+                                                        uint32_t *__restrict__ ssrc, uint32_t *__restrict__ sdst,
+                                                        uint64_t *__restrict__ skey, uint64_t *__restrict__ seg_count) {
+  __shared__ uint32_t s_wcnt[BLOCK / WAVE];
+  const uint64_t T = e_hi - e_lo;
+  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
+  const uint64_t vb = Q * blockIdx.x;
+  const uint64_t ve = (vb + Q < T) ? vb + Q : T;
+  uint64_t out_n = 0;
+  for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
+    const uint64_t v = v0 + (uint64_t)threadIdx.x * 4;
+    uint32_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, w[4] = {0, 0, 0, 0};
+    bool sel[4] = {false, false, false, false};
+    const uint64_t e0 = e_lo + v;
+    if (v + 4 <= ve && (e0 & 3) == 0) {
+      const uint4 a4 = *reinterpret_cast<const uint4 *>(eu + e0);
+      const uint4 b4 = *reinterpret_cast<const uint4 *>(ev + e0);
+      const uint4 w4 = *reinterpret_cast<const uint4 *>(ew + e0);
+      a[0] = a4.x; a[1] = a4.y; a[2] = a4.z; a[3] = a4.w;
+      b[0] = b4.x; b[1] = b4.y; b[2] = b4.z; b[3] = b4.w;
+      w[0] = w4.x; w[1] = w4.y; w[2] = w4.z; w[3] = w4.w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sel[j] = w[j] >= w_lo && (uint64_t)w[j] < w_hi;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (v + j < ve) {
+          a[j] = eu[e0 + j];
+          b[j] = ev[e0 + j];
+          w[j] = ew[e0 + j];
+          sel[j] = w[j] >= w_lo && (uint64_t)w[j] < w_hi;
+        }
+      }
+    }
+    if (FILTER) {
+      // REJECT a whole class at once: both ends in the giant fragment (1-bit bitmap in L2)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (sel[j]) {
+          const bool ga = (giant_bits[a[j] >> 6] >> (a[j] & 63)) & 1;
+          const bool gb = (giant_bits[b[j] >> 6] >> (b[j] & 63)) & 1;
+          if (ga && gb) sel[j] = false;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (sel[j]) {
+          a[j] = lab[a[j]];
+          b[j] = lab[b[j]];
+          if (a[j] == b[j]) sel[j] = false;
+        }
+      }
+    }
+    uint32_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mine += sel[j] ? 1u : 0u;
+    uint32_t total;
+    const uint32_t before = block_offsets(mine, s_wcnt, &total);
+    uint64_t pos = vb + out_n + before;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (sel[j]) {
+        ssrc[pos] = a[j];
+        sdst[pos] = b[j];
+        skey[pos] = ((uint64_t)w[j] << 32) | (uint32_t)(e0 + j);
+        ++pos;
+      }
+    }
+    out_n += total;
+  }
+  if (threadIdx.x == 0) seg_count[blockIdx.x] = (vb < T) ? out_n : 0;
+}
+
+// staging segments -> dense forward arcs [0, S) of the level arc buffer (order preserved)
+__global__ __launch_bounds__(BLOCK) void k_gather_segments(uint64_t T, const uint64_t *__restrict__ seg_prefix,
+                                                           const uint32_t *__restrict__ ssrc,
+                                                           const uint32_t *__restrict__ sdst,
+                                                           const uint64_t *__restrict__ skey, uint32_t *__restrict__ dsrc,
+                                                           uint32_t *__restrict__ ddst, uint64_t *__restrict__ dkey) {
+  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
+  const uint64_t vb = Q * blockIdx.x;
+  const uint64_t cnt = seg_prefix[blockIdx.x + 1] - seg_prefix[blockIdx.x];
+  const uint64_t dbase = seg_prefix[blockIdx.x];
+  for (uint64_t i = threadIdx.x; i < cnt; i += BLOCK) {
+    dsrc[dbase + i] = ssrc[vb + i];
+    ddst[dbase + i] = sdst[vb + i];
+    dkey[dbase + i] = skey[vb + i];
+  }
+}
+
 __global__ void k_iota(uint32_t *__restrict__ a, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     a[i] = (uint32_t)i;
+}
+
+// reverse arcs [S, 2S): src = sorted dst labels (already written), dst/key gathered by index
+__global__ void k_fill_reverse(uint64_t S, const uint32_t *__restrict__ idx, uint32_t *__restrict__ asrc,
+                               uint32_t *__restrict__ adst, uint64_t *__restrict__ akey) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < S; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t j = idx[i];
+    adst[S + i] = asrc[j];
+    akey[S + i] = akey[j];
+  }
+}
+
+__global__ void k_set_seg1(uint64_t *start, uint64_t *prefix, uint64_t total) {
+  start[0] = 0;
+  prefix[0] = 0;
+  prefix[1] = total;
 }
 
 // dense all-reduce staging: int64 slot = key ^ 2^63 preserves unsigned order under signed MIN
@@ -339,6 +610,12 @@ static inline unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+static inline int bits_for(uint64_t maxval) {
+  int b = 0;
+  while (b < 64 && (maxval >> b)) ++b;
+  return b ? b : 1;
+}
+
 }  // namespace ghs
 
 using namespace ghs;
@@ -346,55 +623,74 @@ using namespace ghs;
 // ============================================================================================
 // Solver handle
 // ============================================================================================
+struct ArcBuf {
+  uint32_t *src = nullptr, *dst = nullptr;
+  uint64_t *key = nullptr;
+  uint64_t *seg_start = nullptr, *seg_count = nullptr, *seg_prefix = nullptr;
+};
+
 struct ghs_solver {
   uint32_t n = 0;
-  uint64_t m = 0;
-  const uint32_t *eu = nullptr, *ev = nullptr;
-  const uint32_t *in_src = nullptr, *in_dst = nullptr;
-  const uint64_t *in_key = nullptr;
-  uint64_t num_arcs = 0;
+  uint64_t m = 0, e_lo = 0, e_hi = 0;
+  const uint32_t *eu = nullptr, *ev = nullptr, *ew = nullptr;
   uint8_t *in_mst = nullptr;
   hipStream_t stream = nullptr;
+  ghs_config_t cfg{};
 
   uint32_t *lab = nullptr, *par = nullptr, *act[2] = {nullptr, nullptr};
-  uint64_t *best = nullptr;
-  uint32_t *bsrc[2] = {nullptr, nullptr}, *bdst[2] = {nullptr, nullptr};
-  uint64_t *bkey[2] = {nullptr, nullptr};
+  uint64_t *best = nullptr, *bits = nullptr;
   uint8_t *flags = nullptr;
+  uint32_t *sample = nullptr;
+  ArcBuf buf[2];
+  uint64_t cap_arcs = 0;
   void *cub_temp = nullptr;
   size_t cub_bytes = 0;
-  unsigned long long *cnt = nullptr;    // device [0] arcs out, [1] active out, [2] weight, [3] edges
+  unsigned long long *cnt = nullptr;    // device [0] scratch total, [1] active out, [2] weight, [3] edges, [4] err
   unsigned long long *h_cnt = nullptr;  // pinned host mirror
+  uint32_t *h_sample = nullptr;         // pinned host sample buffer
+
+  // level plan (identical on every rank: computed from the global canonical list)
+  std::vector<uint64_t> thresholds;  // level i: [thr[i], thr[i+1])
+  uint32_t level = 0;                // index of the level being processed
+  bool level_open = false;
+  uint64_t level_arcs = 0;           // arcs built for the current level (stats)
 
   // round state
-  uint32_t round = 0;      // completed rounds
-  int phase = 0;           // 0: expect minedge, 1: expect contract, 2: done
-  int cur_buf = -1;        // -1: arcs are the input arrays
+  uint32_t round = 0;        // completed rounds (all levels)
+  uint32_t level_round = 0;  // completed rounds in this level
+  int phase = 0;             // 0: expect minedge, 1: expect contract, 2: done
+  int cur = 0;               // arc buffer holding the live arcs
+  bool cur_single = true;    // live arcs are one dense segment
   uint64_t cur_arcs = 0;
   int act_cur = 0;
-  bool act_ident = true;   // round 1: fragments are 0..n-1
+  bool act_ident = true;     // fragments are 0..n-1
   uint64_t nact = 0;
   uint64_t edges_before = 0;
 
   std::vector<ghs_round_stats_t> stats;
-  std::vector<hipEvent_t> ev_pool;  // 5 per round (up to GHS_MAX_ROUND_STATS rounds)
+  std::vector<hipEvent_t> ev_pool;
   std::chrono::steady_clock::time_point t0;
 };
 
-static std::mutex g_mutex;  // calls are serialised per process
+static std::mutex g_mutex;  // the one-shot entry points are serialised per process
 
-static size_t select_temp_bytes(uint32_t n) {
-  size_t a = 0, b = 0;
+static constexpr uint32_t NSAMPLE = 65536;
+
+static size_t cub_temp_bytes(uint32_t n, uint64_t cap) {
+  size_t a = 0, b = 0, c = 0;
   const size_t items = n ? n : 1;
   (void)hipcub::DeviceSelect::Flagged(nullptr, a, (const uint32_t *)nullptr, (const uint8_t *)nullptr,
                                       (uint32_t *)nullptr, (unsigned long long *)nullptr, items);
   (void)hipcub::DeviceSelect::Flagged(nullptr, b, hipcub::CountingInputIterator<uint32_t>(0u),
                                       (const uint8_t *)nullptr, (uint32_t *)nullptr, (unsigned long long *)nullptr,
                                       items);
-  return (a > b ? a : b) + 256;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, c, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                          (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                          (size_t)(cap ? cap : 1), 0, bits_for(n ? n - 1 : 0));
+  return std::max(a, std::max(b, c)) + 256;
 }
 
-static size_t workspace_layout(uint32_t n, uint64_t num_arcs, ghs_solver *s, char *base) {
+static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, char *base) {
   size_t off = 0;
   auto carve = [&](size_t bytes) -> char * {
     char *p = base ? base + off : nullptr;
@@ -402,27 +698,166 @@ static size_t workspace_layout(uint32_t n, uint64_t num_arcs, ghs_solver *s, cha
     return p;
   };
   const size_t N = (size_t)n;
+  const uint64_t cap = 2 * local_edges + 4 * SEG_G;  // a level's arcs: <= 2 per selected edge (+ padding)
   char *p;
   p = carve(N * 4); if (s) s->lab = (uint32_t *)p;
   p = carve(N * 4); if (s) s->par = (uint32_t *)p;
   p = carve(N * 8); if (s) s->best = (uint64_t *)p;
   p = carve(N * 4); if (s) s->act[0] = (uint32_t *)p;
   p = carve(N * 4); if (s) s->act[1] = (uint32_t *)p;
-  for (int b = 0; b < 2; ++b) {
-    p = carve(num_arcs * 4); if (s) s->bsrc[b] = (uint32_t *)p;
-    p = carve(num_arcs * 4); if (s) s->bdst[b] = (uint32_t *)p;
-    p = carve(num_arcs * 8); if (s) s->bkey[b] = (uint64_t *)p;
-  }
   p = carve(N ? N : 1); if (s) s->flags = (uint8_t *)p;
-  size_t cb = select_temp_bytes(n);
-  p = carve(cb); if (s) { s->cub_temp = p; s->cub_bytes = cb; }
+  p = carve(((N + 63) / 64) * 8 + 8); if (s) s->bits = (uint64_t *)p;
+  p = carve(NSAMPLE * 4); if (s) s->sample = (uint32_t *)p;
+  for (int b = 0; b < 2; ++b) {
+    p = carve(cap * 4); if (s) s->buf[b].src = (uint32_t *)p;
+    p = carve(cap * 4); if (s) s->buf[b].dst = (uint32_t *)p;
+    p = carve(cap * 8); if (s) s->buf[b].key = (uint64_t *)p;
+    p = carve(SEG_G * 8); if (s) s->buf[b].seg_start = (uint64_t *)p;
+    p = carve(SEG_G * 8); if (s) s->buf[b].seg_count = (uint64_t *)p;
+    p = carve((SEG_G + 1) * 8); if (s) s->buf[b].seg_prefix = (uint64_t *)p;
+  }
+  const size_t cb = cub_temp_bytes(n, cap);
+  p = carve(cb); if (s) { s->cub_temp = p; s->cub_bytes = cb; s->cap_arcs = cap; }
   p = carve(8 * sizeof(unsigned long long)); if (s) s->cnt = (unsigned long long *)p;
   return off;
 }
 
-static int check_dev_ptr16(const void *p, uint64_t count, const char *name) {
-  if (count && !p) GHS_FAIL(GHS_E_ARG, std::string(name) + " is NULL");
-  if (((uintptr_t)p) & 15) GHS_FAIL(GHS_E_ARG, std::string(name) + " must be 16-byte aligned");
+static hipEvent_t round_event(ghs_solver *s, uint32_t round, int k) {
+  if (round >= GHS_MAX_ROUND_STATS) return nullptr;
+  const size_t idx = (size_t)round * 6 + k;
+  while (s->ev_pool.size() <= idx) {
+    hipEvent_t ev = nullptr;
+    if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+    s->ev_pool.push_back(ev);
+  }
+  return s->ev_pool[idx];
+}
+
+static void record(ghs_solver *s, int k) {
+  hipEvent_t ev = round_event(s, s->round, k);
+  if (ev) (void)hipEventRecord(ev, s->stream);
+}
+
+static void default_config(ghs_config_t *c) {
+  c->max_levels = 3;
+  c->level1_edges_per_vertex = 2.0;
+  c->level_growth = 8.0;
+}
+
+// ---- level planning: thresholds from a sample of the GLOBAL canonical weights ----------------
+static int plan_levels(ghs_solver *s) {
+  s->thresholds.clear();
+  s->thresholds.push_back(0);
+  const uint32_t L = std::max<uint32_t>(1, std::min<uint32_t>(s->cfg.max_levels, 16));
+  if (L > 1 && s->m > 0) {
+    const uint32_t ns = (uint32_t)std::min<uint64_t>(NSAMPLE, s->m);
+    k_sample_weights<<<grid_for(ns, 256, 256), 256, 0, s->stream>>>(s->m, s->ew, ns, s->sample);
+    GHS_HIP_CHECK(hipGetLastError());
+    GHS_HIP_CHECK(hipMemcpyAsync(s->h_sample, s->sample, ns * 4, hipMemcpyDeviceToHost, s->stream));
+    GHS_HIP_CHECK(hipStreamSynchronize(s->stream));
+    std::vector<uint32_t> w(s->h_sample, s->h_sample + ns);
+    std::sort(w.begin(), w.end());
+    double target = s->cfg.level1_edges_per_vertex * (double)s->n;
+    for (uint32_t i = 1; i < L; ++i) {
+      const double frac = target / (double)s->m;
+      if (frac >= 1.0) break;
+      const size_t q = (size_t)(frac * ns);
+      target *= s->cfg.level_growth;
+      if (q == 0) continue;
+      const uint64_t thr = (uint64_t)w[std::min<size_t>(q, ns - 1)];
+      if (thr > s->thresholds.back()) s->thresholds.push_back(thr);
+    }
+  }
+  s->thresholds.push_back(1ull << 32);
+  return GHS_OK;
+}
+
+// ---- open the next level: select + filter its edges, build its arcs, set the active list ----
+static int open_level(ghs_solver *s) {
+  const uint32_t lv = s->level;
+  const uint32_t w_lo = (uint32_t)s->thresholds[lv];
+  const uint64_t w_hi = s->thresholds[lv + 1];
+  const bool first = (lv == 0);
+  hipStream_t st = s->stream;
+  ArcBuf &X = s->buf[0], &Y = s->buf[1];
+  const uint64_t T = s->e_hi - s->e_lo;
+
+  if (!first) {
+    // compress labels, find the giant fragment from a sample, build its bitmap
+    k_resolve<<<grid_for(s->n, BLOCK, 16384), BLOCK, 0, st>>>(s->n, s->lab, s->flags, s->cnt + 4);
+    const uint32_t ns = std::min<uint32_t>(NSAMPLE, s->n);
+    k_sample_labels<<<grid_for(ns, 256, 256), 256, 0, st>>>(s->n, s->lab, ns, s->sample);
+    GHS_HIP_CHECK(hipGetLastError());
+    GHS_HIP_CHECK(hipMemcpyAsync(s->h_sample, s->sample, ns * 4, hipMemcpyDeviceToHost, st));
+    GHS_HIP_CHECK(hipStreamSynchronize(st));
+    std::unordered_map<uint32_t, uint32_t> freq;
+    uint32_t giant = s->h_sample[0], gc = 0;
+    for (uint32_t i = 0; i < ns; ++i) {
+      const uint32_t c = ++freq[s->h_sample[i]];
+      if (c > gc || (c == gc && s->h_sample[i] < giant)) {
+        gc = c;
+        giant = s->h_sample[i];
+      }
+    }
+    k_bitmap<<<grid_for(s->n, BLOCK, 16384), BLOCK, 0, st>>>(s->n, s->lab, giant, s->bits);
+    GHS_HIP_CHECK(hipGetLastError());
+  }
+
+  // 1. this level's edges (filtered) into block-private staging regions of Y
+  const unsigned G = grid_for(T, ARCS_PER_BLOCK, SEG_G);
+  if (T) {
+    if (first)
+      k_level_select<false><<<G, BLOCK, 0, st>>>(s->e_lo, s->e_hi, s->eu, s->ev, s->ew, w_lo, w_hi, s->lab, s->bits,
+                                                 Y.src, Y.dst, Y.key, Y.seg_count);
+    else
+      k_level_select<true><<<G, BLOCK, 0, st>>>(s->e_lo, s->e_hi, s->eu, s->ev, s->ew, w_lo, w_hi, s->lab, s->bits,
+                                                Y.src, Y.dst, Y.key, Y.seg_count);
+    GHS_HIP_CHECK(hipGetLastError());
+    k_scan_counts<<<1, 1024, 0, st>>>(Y.seg_count, G, Y.seg_prefix, s->cnt + 0);
+    // 2. dense forward arcs X[0, S) (canonical order kept: grouped by the source's vertex)
+    k_gather_segments<<<G, BLOCK, 0, st>>>(T, Y.seg_prefix, Y.src, Y.dst, Y.key, X.src, X.dst, X.key);
+    GHS_HIP_CHECK(hipGetLastError());
+  } else {
+    GHS_HIP_CHECK(hipMemsetAsync(s->cnt, 0, 8, st));
+  }
+  GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, 8, hipMemcpyDeviceToHost, st));
+  GHS_HIP_CHECK(hipStreamSynchronize(st));
+  const uint64_t S = s->h_cnt[0];
+  // 3. reverse arcs X[S, 2S): radix sort (dst label, index) -> grouped by dst label
+  if (S) {
+    uint32_t *idx_in = Y.src, *idx_out = Y.dst;  // Y's staging is consumed
+    k_iota<<<grid_for(S, 256, 16384), 256, 0, st>>>(idx_in, S);
+    size_t cb = s->cub_bytes;
+    GHS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(s->cub_temp, cb, X.dst, X.src + S, idx_in, idx_out, (size_t)S, 0,
+                                                     bits_for(s->n - 1), st));
+    k_fill_reverse<<<grid_for(S, 256, 16384), 256, 0, st>>>(S, idx_out, X.src, X.dst, X.key);
+    GHS_HIP_CHECK(hipGetLastError());
+  }
+  s->cur = 0;
+  s->cur_single = true;
+  s->cur_arcs = 2 * S;
+  s->level_arcs = 2 * S;
+  k_set_seg1<<<1, 1, 0, st>>>(X.seg_start, X.seg_prefix, s->cur_arcs);
+  GHS_HIP_CHECK(hipGetLastError());
+
+  // 4. active fragments: every current root (first level: every vertex). Identical on every
+  //    rank (the fragment state is replicated); roots without arcs anywhere drop out after
+  //    their first round (best stays NONE).
+  if (first) {
+    s->act_ident = true;
+    s->nact = s->n;
+  } else {
+    size_t cb = s->cub_bytes;
+    GHS_HIP_CHECK(hipcub::DeviceSelect::Flagged(s->cub_temp, cb, hipcub::CountingInputIterator<uint32_t>(0u), s->flags,
+                                                s->act[0], s->cnt + 1, (size_t)s->n, st));
+    GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt + 1, s->cnt + 1, 8, hipMemcpyDeviceToHost, st));
+    GHS_HIP_CHECK(hipStreamSynchronize(st));
+    s->act_ident = false;
+    s->act_cur = 0;
+    s->nact = s->h_cnt[1];
+  }
+  s->level_round = 0;
+  s->level_open = true;
   return GHS_OK;
 }
 
@@ -439,44 +874,58 @@ int ghs_device_count(int *count) {
   return GHS_OK;
 }
 
-size_t ghs_workspace_bytes(uint32_t n, uint64_t m, uint64_t num_arcs) {
-  (void)m;
-  return workspace_layout(n, num_arcs, nullptr, nullptr);
+void ghs_default_config(ghs_config_t *cfg) {
+  if (cfg) default_config(cfg);
 }
 
-int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_asrc,
-                      const uint32_t *d_adst, const uint64_t *d_akey, uint64_t num_arcs, void *d_workspace,
+size_t ghs_workspace_bytes(uint32_t n, uint64_t m, uint64_t local_edges) {
+  (void)m;
+  return workspace_layout(n, local_edges, nullptr, nullptr);
+}
+
+int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
+                      uint64_t e_lo, uint64_t e_hi, const ghs_config_t *cfg, void *d_workspace,
                       size_t workspace_bytes, uint8_t *d_in_mst, void *stream, ghs_solver_t **out) {
   if (!out) GHS_FAIL(GHS_E_ARG, "out is NULL");
   *out = nullptr;
-  if (m >= (1ull << 32)) GHS_FAIL(GHS_E_ARG, "m must be < 2^32 (eid is 32-bit)");
-  if (num_arcs >= (1ull << 40)) GHS_FAIL(GHS_E_ARG, "num_arcs too large");
-  int rc;
-  if ((rc = check_dev_ptr16(d_asrc, num_arcs, "d_asrc"))) return rc;
-  if ((rc = check_dev_ptr16(d_adst, num_arcs, "d_adst"))) return rc;
-  if ((rc = check_dev_ptr16(d_akey, num_arcs, "d_akey"))) return rc;
-  if (m && (!d_u || !d_v || !d_in_mst)) GHS_FAIL(GHS_E_ARG, "d_u/d_v/d_in_mst is NULL");
-  const size_t need = workspace_layout(n, num_arcs, nullptr, nullptr);
+  if (m >= (1ull << 31)) GHS_FAIL(GHS_E_ARG, "m must be < 2^31");
+  if (e_lo > e_hi || e_hi > m) GHS_FAIL(GHS_E_ARG, "bad edge range");
+  if (m && (!d_u || !d_v || !d_w || !d_in_mst)) GHS_FAIL(GHS_E_ARG, "d_u/d_v/d_w/d_in_mst is NULL");
+  if ((((uintptr_t)d_u) | ((uintptr_t)d_v) | ((uintptr_t)d_w)) & 15)
+    GHS_FAIL(GHS_E_ARG, "d_u/d_v/d_w must be 16-byte aligned");
+  const size_t need = workspace_layout(n, e_hi - e_lo, nullptr, nullptr);
   if (!d_workspace || workspace_bytes < need)
     GHS_FAIL(GHS_E_NOMEM, "workspace too small: need " + std::to_string(need) + " bytes");
   if (((uintptr_t)d_workspace) & 255) GHS_FAIL(GHS_E_ARG, "workspace must be 256-byte aligned");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) GHS_FAIL(GHS_E_NODEVICE, "no HIP device");
+  {
+    // every kernel indexes n-sized arrays with these ids: validate before launching anything
+    int ok = 1;
+    const int rc0 = ghs_check_canonical(n, m, d_u, d_v, stream, &ok);
+    if (rc0) return rc0;
+    if (!ok) GHS_FAIL(GHS_E_NONCANON, "edge list is not canonical (need u < v < n, strictly ascending (u, v))");
+  }
 
   ghs_solver *s = new ghs_solver();
-  s->n = n; s->m = m; s->eu = d_u; s->ev = d_v;
-  s->in_src = d_asrc; s->in_dst = d_adst; s->in_key = d_akey; s->num_arcs = num_arcs;
+  s->n = n; s->m = m; s->e_lo = e_lo; s->e_hi = e_hi;
+  s->eu = d_u; s->ev = d_v; s->ew = d_w;
   s->in_mst = d_in_mst; s->stream = (hipStream_t)stream;
-  workspace_layout(n, num_arcs, s, (char *)d_workspace);
+  if (cfg) s->cfg = *cfg; else default_config(&s->cfg);
+  workspace_layout(n, e_hi - e_lo, s, (char *)d_workspace);
   auto fail = [&](hipError_t e, const char *what) {
     set_error(std::string(what) + ": " + hipGetErrorString(e));
     if (s->h_cnt) (void)hipHostFree(s->h_cnt);
+    if (s->h_sample) (void)hipHostFree(s->h_sample);
     delete s;
     return GHS_E_HIP;
   };
   hipError_t e;
   if ((e = hipHostMalloc((void **)&s->h_cnt, 8 * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess)
     return fail(e, "hipHostMalloc");
+  if ((e = hipHostMalloc((void **)&s->h_sample, NSAMPLE * 4, hipHostMallocDefault)) != hipSuccess)
+    return fail(e, "hipHostMalloc");
+  s->t0 = std::chrono::steady_clock::now();
   if (n) {
     if ((e = hipMemsetAsync(s->best, 0xff, (size_t)n * 8, s->stream)) != hipSuccess) return fail(e, "memset best");
     k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->lab, n);
@@ -485,29 +934,16 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   if ((e = hipMemsetAsync(s->cnt, 0, 8 * sizeof(unsigned long long), s->stream)) != hipSuccess)
     return fail(e, "memset counters");
   if ((e = hipGetLastError()) != hipSuccess) return fail(e, "init kernels");
-  s->cur_arcs = num_arcs;
-  s->nact = n;
-  s->act_ident = true;
+  int rc = plan_levels(s);
+  if (rc) {
+    ghs_solver_destroy(s);
+    return rc;
+  }
+  s->level = 0;
+  s->level_open = false;
   s->phase = n ? 0 : 2;
-  s->t0 = std::chrono::steady_clock::now();
   *out = s;
   return GHS_OK;
-}
-
-static hipEvent_t round_event(ghs_solver *s, uint32_t round, int k) {
-  if (round >= GHS_MAX_ROUND_STATS) return nullptr;
-  const size_t idx = (size_t)round * 5 + k;
-  while (s->ev_pool.size() <= idx) {
-    hipEvent_t ev = nullptr;
-    if (hipEventCreate(&ev) != hipSuccess) return nullptr;
-    s->ev_pool.push_back(ev);
-  }
-  return s->ev_pool[idx];
-}
-
-static void record(ghs_solver *s, int k) {
-  hipEvent_t ev = round_event(s, s->round, k);
-  if (ev) (void)hipEventRecord(ev, s->stream);
 }
 
 int ghs_solver_minedge(ghs_solver_t *s, uint64_t *num_active) {
@@ -517,22 +953,27 @@ int ghs_solver_minedge(ghs_solver_t *s, uint64_t *num_active) {
     return GHS_OK;
   }
   if (s->phase != 0) GHS_FAIL(GHS_E_STATE, "minedge called twice without contract");
-  if (s->round >= 64) GHS_FAIL(GHS_E_ROUNDCAP, "round cap exceeded");
+  if (s->round >= 16 * GHS_MAX_ROUND_STATS) GHS_FAIL(GHS_E_ROUNDCAP, "round cap exceeded");
+  if (!s->level_open) {
+    int rc = open_level(s);
+    if (rc) return rc;
+  }
   record(s, 0);
   const uint64_t A = s->cur_arcs;
+  const ArcBuf &I = s->buf[s->cur];
+  ArcBuf &O = s->buf[s->cur ^ 1];
   if (A) {
-    const unsigned grid = grid_for(A, ARCS_PER_BLOCK, 8192);
-    if (s->round == 0) {
-      k_minedge<true, false><<<grid, BLOCK, 0, s->stream>>>(s->in_src, s->in_dst, s->in_key, A, s->lab, s->best,
-                                                            nullptr, nullptr, nullptr, nullptr);
+    SegView in{I.seg_start, I.seg_prefix, s->cur_single ? 1u : SEG_G, A};
+    const unsigned G = grid_for(A, ARCS_PER_BLOCK, SEG_G);
+    if (s->level_round == 0) {
+      k_minedge<true, false><<<G, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, nullptr, nullptr,
+                                                         nullptr, nullptr, nullptr);
     } else {
-      const int ob = (s->cur_buf == 0) ? 1 : 0;
-      const uint32_t *isrc = s->cur_buf < 0 ? s->in_src : s->bsrc[s->cur_buf];
-      const uint32_t *idst = s->cur_buf < 0 ? s->in_dst : s->bdst[s->cur_buf];
-      const uint64_t *ikey = s->cur_buf < 0 ? s->in_key : s->bkey[s->cur_buf];
-      GHS_HIP_CHECK(hipMemsetAsync(s->cnt, 0, sizeof(unsigned long long), s->stream));
-      k_minedge<false, true><<<grid, BLOCK, 0, s->stream>>>(isrc, idst, ikey, A, s->lab, s->best, s->bsrc[ob],
-                                                            s->bdst[ob], s->bkey[ob], s->cnt);
+      // unused segment slots of O (when G < SEG_G) stay zero-count
+      if (G < SEG_G) GHS_HIP_CHECK(hipMemsetAsync(O.seg_count + G, 0, (SEG_G - G) * 8, s->stream));
+      k_minedge<false, true><<<G, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, O.src, O.dst,
+                                                         O.key, O.seg_start, O.seg_count);
+      k_scan_counts<<<1, 1024, 0, s->stream>>>(O.seg_count, SEG_G, O.seg_prefix, s->cnt + 0);
     }
     GHS_HIP_CHECK(hipGetLastError());
   }
@@ -574,23 +1015,31 @@ int ghs_solver_contract(ghs_solver_t *s, int *done) {
   const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
   const uint64_t nact = s->nact;
   const unsigned g = grid_for(nact, BLOCK, 16384);
-  k_hook<<<g, BLOCK, 0, s->stream>>>(act, nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst, s->cnt + 2,
-                                     s->cnt + 4);
-  GHS_HIP_CHECK(hipGetLastError());
+  if (nact) {
+    k_hook<<<grid_for(nact, BLOCK, 2048), BLOCK, 0, s->stream>>>(act, nact, s->best, s->lab, s->eu, s->ev, s->par,
+                                                                 s->in_mst, s->cnt + 2, s->cnt + 4);
+    GHS_HIP_CHECK(hipGetLastError());
+  }
   record(s, 2);
-  k_jump<<<g, BLOCK, 0, s->stream>>>(act, nact, s->par, s->lab, s->cnt + 4);
-  GHS_HIP_CHECK(hipGetLastError());
+  if (nact) {
+    k_jump<<<g, BLOCK, 0, s->stream>>>(act, nact, s->par, s->lab, s->cnt + 4);
+    GHS_HIP_CHECK(hipGetLastError());
+  }
   record(s, 3);
   const int nb = s->act_ident ? 0 : (s->act_cur ^ 1);
-  k_flag_next<<<g, BLOCK, 0, s->stream>>>(act, nact, s->par, s->best, s->flags);
-  GHS_HIP_CHECK(hipGetLastError());
-  size_t cb = s->cub_bytes;
-  if (act) {
-    GHS_HIP_CHECK(hipcub::DeviceSelect::Flagged(s->cub_temp, cb, act, s->flags, s->act[nb], s->cnt + 1, (size_t)nact,
-                                                s->stream));
+  if (nact) {
+    k_flag_next<<<g, BLOCK, 0, s->stream>>>(act, nact, s->par, s->best, s->flags);
+    GHS_HIP_CHECK(hipGetLastError());
+    size_t cb = s->cub_bytes;
+    if (act) {
+      GHS_HIP_CHECK(hipcub::DeviceSelect::Flagged(s->cub_temp, cb, act, s->flags, s->act[nb], s->cnt + 1, (size_t)nact,
+                                                  s->stream));
+    } else {
+      GHS_HIP_CHECK(hipcub::DeviceSelect::Flagged(s->cub_temp, cb, hipcub::CountingInputIterator<uint32_t>(0u),
+                                                  s->flags, s->act[nb], s->cnt + 1, (size_t)nact, s->stream));
+    }
   } else {
-    GHS_HIP_CHECK(hipcub::DeviceSelect::Flagged(s->cub_temp, cb, hipcub::CountingInputIterator<uint32_t>(0u), s->flags,
-                                                s->act[nb], s->cnt + 1, (size_t)nact, s->stream));
+    GHS_HIP_CHECK(hipMemsetAsync(s->cnt + 1, 0, 8, s->stream));
   }
   record(s, 4);
   GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
@@ -600,25 +1049,30 @@ int ghs_solver_contract(ghs_solver_t *s, int *done) {
     GHS_FAIL(GHS_E_STATE, "internal invariant violated in round " + std::to_string(s->round + 1) + " (code " +
                               std::to_string(s->h_cnt[4]) + ")");
   }
-
   ghs_round_stats_t st{};
+  st.level = s->level;
+  st.level_arcs = s->level_round == 0 ? s->level_arcs : 0;
   st.live_arcs = s->cur_arcs;
   st.active_components = nact;
   st.hooks = s->h_cnt[3] - s->edges_before;
   s->edges_before = s->h_cnt[3];
   s->stats.push_back(st);
 
-  // advance: arcs compacted this round (rounds >= 2) become next round's input
-  if (s->round >= 1) {
-    s->cur_buf = (s->cur_buf == 0) ? 1 : 0;
+  // the arcs compacted by this round's min-edge kernel are the next round's input
+  if (s->level_round >= 1 && s->cur_arcs) {
+    s->cur ^= 1;
+    s->cur_single = false;
     s->cur_arcs = s->h_cnt[0];
   }
   s->act_cur = nb;
   s->act_ident = false;
   s->nact = s->h_cnt[1];
   s->round += 1;
-  if (s->nact == 0) {
-    s->phase = 2;
+  s->level_round += 1;
+  if (s->nact == 0) {  // level complete
+    s->level_open = false;
+    s->level += 1;
+    s->phase = (s->level + 1 >= s->thresholds.size()) ? 2 : 0;
   } else {
     s->phase = 0;
   }
@@ -630,8 +1084,7 @@ int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *
   if (!s) GHS_FAIL(GHS_E_ARG, "solver is NULL");
   if (s->phase != 2) GHS_FAIL(GHS_E_STATE, "finish before the loop terminated");
   GHS_HIP_CHECK(hipStreamSynchronize(s->stream));
-  const double ms =
-      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s->t0).count();
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s->t0).count();
   const uint32_t ns = (uint32_t)std::min<size_t>(s->stats.size(), GHS_MAX_ROUND_STATS);
   for (uint32_t r = 0; r < ns; ++r) {
     float t[4] = {0, 0, 0, 0};
@@ -650,6 +1103,7 @@ int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *
     result->total_weight = s->n ? s->h_cnt[2] : 0;
     result->rounds = s->round;
     result->num_stats = ns;
+    result->levels = (uint32_t)(s->thresholds.size() - 1);
     result->ms_total = ms;
   }
   return GHS_OK;
@@ -659,18 +1113,17 @@ int ghs_solver_destroy(ghs_solver_t *s) {
   if (!s) return GHS_OK;
   for (hipEvent_t e : s->ev_pool) (void)hipEventDestroy(e);
   if (s->h_cnt) (void)hipHostFree(s->h_cnt);
+  if (s->h_sample) (void)hipHostFree(s->h_sample);
   delete s;
   return GHS_OK;
 }
 
-int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_asrc,
-                   const uint32_t *d_adst, const uint64_t *d_akey, uint64_t num_arcs, void *d_workspace,
-                   size_t workspace_bytes, uint8_t *d_in_mst, void *stream, ghs_result_t *result,
-                   ghs_round_stats_t *stats) {
+int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
+                   const ghs_config_t *cfg, void *d_workspace, size_t workspace_bytes, uint8_t *d_in_mst, void *stream,
+                   ghs_result_t *result, ghs_round_stats_t *stats) {
   std::lock_guard<std::mutex> lock(g_mutex);
   ghs_solver_t *s = nullptr;
-  int rc = ghs_solver_create(n, m, d_u, d_v, d_asrc, d_adst, d_akey, num_arcs, d_workspace, workspace_bytes,
-                             d_in_mst, stream, &s);
+  int rc = ghs_solver_create(n, m, d_u, d_v, d_w, 0, m, cfg, d_workspace, workspace_bytes, d_in_mst, stream, &s);
   if (rc) return rc;
   int done = (n == 0);
   while (!done) {

@@ -28,13 +28,10 @@ extern "C" int ghs_mst_host(uint32_t n, uint64_t m, const uint32_t *u, const uin
     if (ok && e) ok = (u[e - 1] < u[e]) || (u[e - 1] == u[e] && v[e - 1] < v[e]);
     if (!ok) GHS_FAIL(GHS_E_NONCANON, "edge " + std::to_string(e) + " breaks canonical order (u < v < n, ascending)");
   }
-  const uint64_t A = 2 * m;
-  const size_t ws = ghs_workspace_bytes(n, m, A);
-  const size_t tmp = ghs_build_arcs_temp_bytes(n, m);
+  const size_t ws = ghs_workspace_bytes(n, m, m);
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t off_u = 0, off_v = off_u + al(m * 4), off_w = off_v + al(m * 4), off_src = off_w + al(m * 4),
-               off_dst = off_src + al(A * 4), off_key = off_dst + al(A * 4), off_mst = off_key + al(A * 8),
-               off_ws = off_mst + al(m ? m : 1), off_tmp = off_ws + al(ws), total = off_tmp + al(tmp);
+  const size_t off_u = 0, off_v = off_u + al(m * 4), off_w = off_v + al(m * 4), off_mst = off_w + al(m * 4),
+               off_ws = off_mst + al(m ? m : 1), total = off_ws + al(ws);
   DevBuf buf;
   GHS_HIP_CHECK(hipMalloc(&buf.p, total));
   char *b = (char *)buf.p;
@@ -43,14 +40,9 @@ extern "C" int ghs_mst_host(uint32_t n, uint64_t m, const uint32_t *u, const uin
     GHS_HIP_CHECK(hipMemcpyAsync(b + off_u, u, m * 4, hipMemcpyHostToDevice, st));
     GHS_HIP_CHECK(hipMemcpyAsync(b + off_v, v, m * 4, hipMemcpyHostToDevice, st));
     GHS_HIP_CHECK(hipMemcpyAsync(b + off_w, w, m * 4, hipMemcpyHostToDevice, st));
-    int rc = ghs_build_arcs(n, m, (uint32_t *)(b + off_u), (uint32_t *)(b + off_v), (uint32_t *)(b + off_w),
-                            (uint32_t *)(b + off_src), (uint32_t *)(b + off_dst), (uint64_t *)(b + off_key),
-                            b + off_tmp, tmp, st);
-    if (rc) return rc;
   }
-  int rc = ghs_mst_device(n, m, (uint32_t *)(b + off_u), (uint32_t *)(b + off_v), (uint32_t *)(b + off_src),
-                          (uint32_t *)(b + off_dst), (uint64_t *)(b + off_key), A, b + off_ws, ws,
-                          (uint8_t *)(b + off_mst), st, result, stats);
+  int rc = ghs_mst_device(n, m, (uint32_t *)(b + off_u), (uint32_t *)(b + off_v), (uint32_t *)(b + off_w), nullptr,
+                          b + off_ws, ws, (uint8_t *)(b + off_mst), st, result, stats);
   if (rc) return rc;
   if (m) GHS_HIP_CHECK(hipMemcpy(in_mst, b + off_mst, m, hipMemcpyDeviceToHost));
   return GHS_OK;

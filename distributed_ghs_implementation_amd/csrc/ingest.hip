@@ -279,6 +279,25 @@ int ghs_build_arcs(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *
   return ghs_build_arcs_range(n, m, d_u, d_v, d_w, 0, n, d_asrc, d_adst, d_akey, 2 * m, d_temp, temp_bytes, stream, &A);
 }
 
+int ghs_check_canonical(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, void *stream, int *ok) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!ok) GHS_FAIL(GHS_E_ARG, "ok is NULL");
+  *ok = 1;
+  if (m == 0) return GHS_OK;
+  if (!d_u || !d_v) GHS_FAIL(GHS_E_ARG, "NULL pointer");
+  unsigned int *bad = nullptr;
+  GHS_HIP_CHECK(hipMallocAsync((void **)&bad, sizeof(unsigned int), st));
+  GHS_HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(unsigned int), st));
+  k_check_canonical<<<grid_cap(m, 256, 16384), 256, 0, st>>>(n, m, d_u, d_v, bad);
+  unsigned int h_bad = 0;
+  hipError_t e = hipMemcpyAsync(&h_bad, bad, sizeof(h_bad), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFreeAsync(bad, st);
+  GHS_HIP_CHECK(e);
+  *ok = h_bad ? 0 : 1;
+  return GHS_OK;
+}
+
 size_t ghs_rmat_temp_bytes(uint32_t scale, uint32_t edgefactor) {
   const uint64_t T = (uint64_t)edgefactor << scale;
   size_t sort_b = 0, uniq_b = 0;

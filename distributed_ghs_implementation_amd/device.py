@@ -1,13 +1,13 @@
 """Device-resident pipeline (torch supplies device memory and the stream; HIP does the work).
 
     edges = generate_rmat(24)                    # canonical u, v, w in HBM (BASELINE config 3)
-    eng = DeviceMST(edges)                       # arc + workspace buffers, allocated once
-    res = eng.run()                              # canonical edges -> in_mst flags + weight
+    eng = DeviceMST(edges)                       # workspace allocated once
+    res, stats = eng.run()                       # canonical edges -> in_mst flags + weight
 
 `DeviceMST.run()` is the timed unit of bench.py: from the device-resident canonical edge list to
-the in_mst flags and total weight (BASELINE.md "Definitions"): symmetric arc build (radix sort by
-source) + the Boruvka rounds. Nothing falls back to the CPU: without the HIP library or a GPU the
-constructors raise.
+the in_mst flags and total weight (BASELINE.md "Definitions") — validation, the weight-level
+plan, every level's filter + arc build, and all Boruvka rounds. Nothing falls back to the CPU:
+without the HIP library or a GPU the constructors raise.
 """
 import ctypes
 
@@ -69,7 +69,7 @@ def generate_rmat(scale, edgefactor=16, seed=1, wseed=2, device="cuda"):
                                       _ptr(tmp), tb, _stream()))
     del tmp
     mm = m.value
-    # keep exact-size tensors (clone so the oversize buffers are released)
+    # exact-size tensors (clone so the oversize buffers are released)
     return DeviceEdges(1 << scale, u[:mm].clone(), v[:mm].clone(), w[:mm].clone())
 
 
@@ -86,57 +86,39 @@ def generate_grid(k, mode=0, wseed=2, device="cuda"):
     return DeviceEdges(k * k, u, v, w)
 
 
-class DeviceMST:
-    """Preallocated single-GPU engine for one DeviceEdges graph (or one rank's source range)."""
+def edge_range(m, rank, world):
+    """Contiguous canonical-edge range owned by `rank` (balanced by edge count, 4-aligned so the
+    16-byte vector loads of the level pass stay aligned)."""
+    lo = ((m * rank) // world) & ~3
+    hi = m if rank == world - 1 else ((m * (rank + 1)) // world) & ~3
+    return lo, hi
 
-    def __init__(self, edges, src_lo=0, src_hi=None):
+
+class DeviceMST:
+    """Preallocated single-GPU engine for one DeviceEdges graph (or one rank's edge range)."""
+
+    def __init__(self, edges, e_lo=0, e_hi=None, config=None):
         L = self.L = _native.load()
         _native.require_gpu()
         self.edges = edges
         n, m = edges.n, edges.m
-        self.src_lo = int(src_lo)
-        self.src_hi = n if src_hi is None else int(src_hi)
+        self.e_lo = int(e_lo)
+        self.e_hi = m if e_hi is None else int(e_hi)
+        self.config = config if config is not None else _native.make_config()
         dev = edges.device
-        self.temp_bytes = int(L.ghs_build_arcs_temp_bytes(n, m))
-        self.temp = torch.empty(max(self.temp_bytes, 256), dtype=torch.uint8, device=dev)
-        cnt = ctypes.c_uint64(0)
-        if self.src_lo == 0 and self.src_hi == n:
-            cnt.value = 2 * m
-        else:
-            _native.check(L.ghs_count_arcs_range(n, m, _ptr(edges.u), _ptr(edges.v), self.src_lo, self.src_hi,
-                                                 _ptr(self.temp), self.temp_bytes, _stream(), ctypes.byref(cnt)))
-        self.num_arcs = int(cnt.value)
-        A = max(self.num_arcs, 1)
-        self.asrc = torch.empty(A, dtype=torch.int32, device=dev)
-        self.adst = torch.empty(A, dtype=torch.int32, device=dev)
-        self.akey = torch.empty(A, dtype=torch.int64, device=dev)
-        self.ws_bytes = int(L.ghs_workspace_bytes(n, m, self.num_arcs))
+        self.ws_bytes = int(L.ghs_workspace_bytes(n, m, self.e_hi - self.e_lo))
         self.ws = torch.empty(max(self.ws_bytes, 256), dtype=torch.uint8, device=dev)
         self.in_mst = torch.zeros(max(m, 1), dtype=torch.uint8, device=dev)
 
-    def build_arcs(self):
-        e = self.edges
-        got = ctypes.c_uint64(0)
-        _native.check(self.L.ghs_build_arcs_range(e.n, e.m, _ptr(e.u), _ptr(e.v), _ptr(e.w), self.src_lo, self.src_hi,
-                                                  _ptr(self.asrc), _ptr(self.adst), _ptr(self.akey), self.num_arcs,
-                                                  _ptr(self.temp), self.temp_bytes, _stream(), ctypes.byref(got)))
-        if got.value != self.num_arcs:
-            raise _native.GHSError(_native.GHS_E_STATE, f"built {got.value} arcs, expected {self.num_arcs}")
-
-    def solve(self):
-        """Boruvka rounds on the built arcs -> (Result, [round stats])."""
+    def run(self):
+        """Canonical edges (HBM) -> in_mst flags + totals. Returns (Result, [round stats])."""
         e = self.edges
         res = _native.Result()
         stats = (_native.RoundStats * _native.GHS_MAX_ROUND_STATS)()
-        _native.check(self.L.ghs_mst_device(e.n, e.m, _ptr(e.u), _ptr(e.v), _ptr(self.asrc), _ptr(self.adst),
-                                            _ptr(self.akey), self.num_arcs, _ptr(self.ws), self.ws_bytes,
-                                            _ptr(self.in_mst), _stream(), ctypes.byref(res), stats))
+        _native.check(self.L.ghs_mst_device(e.n, e.m, _ptr(e.u), _ptr(e.v), _ptr(e.w), ctypes.byref(self.config),
+                                            _ptr(self.ws), self.ws_bytes, _ptr(self.in_mst), _stream(),
+                                            ctypes.byref(res), stats))
         return res, [stats[i].as_dict() for i in range(res.num_stats)]
-
-    def run(self):
-        """Canonical edges (HBM) -> in_mst flags + totals. Returns (Result, stats)."""
-        self.build_arcs()
-        return self.solve()
 
     def in_mst_host(self):
         return self.in_mst[: self.edges.m].cpu().numpy().astype(bool)

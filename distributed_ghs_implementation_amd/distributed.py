@@ -4,9 +4,9 @@ Replaces the reference's MPI path (ghs_implementation_mpi.py:884-954: one rank P
 pickled point-to-point messages, bcast/Barrier/gather) with one rank per GPU and ONE collective
 per round:
 
-  * partition: rank r owns the arcs whose source lies in the vertex range
-    [r*n/N, (r+1)*n/N) (ghs_build_arcs_range); the canonical edge list (needed to resolve a
-    chosen edge's endpoints) and the fragment state are replicated;
+  * partition: rank r owns the contiguous canonical-edge range [r*m/N, (r+1)*m/N) and builds
+    the arcs of ITS edges only (both directions); the canonical edge list (read by the level
+    pass and to resolve a chosen edge's endpoints) and the fragment state are replicated;
   * per round: local min-edge over the rank's arcs -> dense best[] slots of the active
     fragments -> all_reduce(MIN) -> identical hook / pointer-jump / next-list on every rank;
   * result: in_mst is identical on every rank by construction (same inputs, same decisions);
@@ -23,13 +23,7 @@ import torch
 import torch.distributed as dist
 
 from . import _native
-from .device import DeviceEdges, DeviceMST, _ptr, _stream
-
-
-def vertex_range(n, rank, world):
-    """Contiguous source-vertex range owned by `rank` (equal vertex counts; the seeded vertex
-    permutation of the R-MAT generator spreads hubs evenly)."""
-    return (n * rank) // world, (n * (rank + 1)) // world
+from .device import DeviceEdges, DeviceMST, _ptr, _stream, edge_range  # noqa: F401
 
 
 class HipStepper:
@@ -40,8 +34,8 @@ class HipStepper:
         L = self.L = engine.L
         ed = engine.edges
         h = ctypes.c_void_p(0)
-        _native.check(L.ghs_solver_create(ed.n, ed.m, _ptr(ed.u), _ptr(ed.v), _ptr(engine.asrc), _ptr(engine.adst),
-                                          _ptr(engine.akey), engine.num_arcs, _ptr(engine.ws), engine.ws_bytes,
+        _native.check(L.ghs_solver_create(ed.n, ed.m, _ptr(ed.u), _ptr(ed.v), _ptr(ed.w), engine.e_lo, engine.e_hi,
+                                          ctypes.byref(engine.config), _ptr(engine.ws), engine.ws_bytes,
                                           _ptr(engine.in_mst), _stream(), ctypes.byref(h)))
         self.h = h
         self.dense = torch.empty(max(ed.n, 1), dtype=torch.int64, device=ed.device)
@@ -81,12 +75,12 @@ class HipStepper:
             pass
 
 
-def run_rounds(stepper, allreduce_min, max_rounds=64):
+def run_rounds(stepper, allreduce_min, max_rounds=4096):
     """The level loop shared by every backend: min-edge, all-reduce MIN, contract.
 
     `allreduce_min(tensor)` reduces in place across ranks (identity for one rank). Returns the
-    number of rounds executed. Raises RuntimeError past `max_rounds` (hang guard; Boruvka needs
-    at most ceil(log2 n) + 1)."""
+    number of rounds executed (all weight levels). Raises RuntimeError past `max_rounds` (hang
+    guard; Boruvka needs at most ceil(log2 n) + 1 rounds per level)."""
     rounds = 0
     while True:
         count = stepper.minedge()
@@ -112,17 +106,16 @@ def torch_allreduce_min(group=None):
 class DistributedMST:
     """One rank's share of a multi-GPU MST over a replicated DeviceEdges graph."""
 
-    def __init__(self, edges, rank=None, world=None, group=None):
+    def __init__(self, edges, rank=None, world=None, group=None, config=None):
         self.rank = dist.get_rank(group) if rank is None else rank
         self.world = dist.get_world_size(group) if world is None else world
         self.group = group
-        lo, hi = vertex_range(edges.n, self.rank, self.world)
-        self.engine = DeviceMST(edges, lo, hi)
+        lo, hi = edge_range(edges.m, self.rank, self.world)
+        self.engine = DeviceMST(edges, lo, hi, config)
         self.edges = edges
 
     def run(self):
-        """Arc build for the owned range + the round loop. Returns (Result, stats)."""
-        self.engine.build_arcs()
+        """The level/round loop over the owned edge range. Returns (Result, stats)."""
         st = HipStepper(self.engine)
         try:
             run_rounds(st, torch_allreduce_min(self.group))

@@ -44,24 +44,41 @@ extern "C" {
 
 #define GHS_MAX_ROUND_STATS 64
 
-/* Per-round record (one GHS level). */
+/* Per-round record (one Boruvka round == one GHS level of the reference). */
 typedef struct ghs_round_stats {
+  uint32_t level;             /* weight level this round belongs to */
+  uint32_t reserved;
+  uint64_t level_arcs;        /* first round of a level: arcs built for the level, else 0 */
   uint64_t live_arcs;         /* arcs scanned by the min-edge kernel this round */
   uint64_t active_components; /* fragments that searched for an outgoing edge */
   uint64_t hooks;             /* fragments that merged (== MST edges added) */
   float ms_minedge;           /* min-outgoing-edge (+ fused compaction) kernel */
   float ms_hook;              /* hook (CONNECT) kernel */
   float ms_jump;              /* pointer-jump relabel (INITIATE) kernel */
-  float ms_active;            /* next-fragment-list compaction kernel */
+  float ms_active;            /* next-fragment-list compaction */
 } ghs_round_stats_t;
 
 typedef struct ghs_result {
   uint64_t num_mst_edges;     /* n - (#components) */
   uint64_t total_weight;      /* sum of w over MST edges */
-  uint32_t rounds;            /* Boruvka rounds (GHS levels) executed */
+  uint32_t rounds;            /* Boruvka rounds executed (all levels) */
   uint32_t num_stats;         /* entries filled in the stats array (<= GHS_MAX_ROUND_STATS) */
-  double ms_total;            /* wall time of the MST loop (device-resident input -> flags) */
+  uint32_t levels;            /* weight levels planned */
+  uint32_t reserved;
+  double ms_total;            /* host wall time of the solve (device-resident input -> flags) */
 } ghs_result_t;
+
+/* Weight-level plan of the filter. Level 1 holds roughly the
+ * level1_edges_per_vertex * n lightest edges, each further level level_growth times more, the
+ * last level the rest; max_levels = 1 runs plain Boruvka over every edge at once. Thresholds
+ * are weight quantiles of a fixed sample of the canonical list, so every rank plans the same
+ * levels. Results do not depend on the plan (only speed does). */
+typedef struct ghs_config {
+  uint32_t max_levels;
+  uint32_t reserved;
+  double level1_edges_per_vertex;
+  double level_growth;
+} ghs_config_t;
 
 /* ---- library / device ------------------------------------------------------------------- */
 int ghs_abi_version(void);
@@ -79,61 +96,60 @@ int ghs_mst_host(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t *v, c
                  uint8_t *in_mst, ghs_result_t *result, ghs_round_stats_t *stats);
 
 /* ---- device-resident API -----------------------------------------------------------------
- * The canonical device graph is the symmetric ARC list: each canonical edge (u, v, w) appears as
- * arcs u->v and v->u, arcs grouped by source vertex (the per-node neighbour lists of the
- * reference's node_<id>.json files, create_graph_files.py:56-74), with key = w<<32 | eid.
- * SoA: asrc[A], adst[A] (uint32), akey[A] (uint64), A = 2m. Pointers must be 16-byte aligned. */
+ * Input: the canonical edge list in HBM (d_u, d_v, d_w: m uint32 each, 16-byte aligned). Each
+ * weight level is turned into a symmetric ARC list on the device — every selected edge as
+ * u->v and v->u, grouped by source: the device form of the reference's per-node neighbour
+ * files node_<id>.json (create_graph_files.py:56-74) — with key = w<<32 | eid. */
+void ghs_default_config(ghs_config_t *cfg);
 
-/* temp bytes for ghs_build_arcs / ghs_build_arcs_range / ghs_count_arcs_range */
+/* workspace bytes for ghs_mst_device / a solver handle owning local_edges canonical edges */
+size_t ghs_workspace_bytes(uint32_t n, uint64_t m, uint64_t local_edges);
+
+/* Whole MST on one device: canonical edges -> d_in_mst (m bytes, 1 = in the MSF) + totals.
+ * cfg may be NULL (defaults). Blocks the calling thread until done (one host sync per round
+ * for the termination test, one per level for the plan). Reference: GHSAlgorithm.run,
+ * ghs_implementation.py:442-490. */
+int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
+                   const ghs_config_t *cfg, void *d_workspace, size_t workspace_bytes, uint8_t *d_in_mst,
+                   void *stream, ghs_result_t *result, ghs_round_stats_t *stats);
+
+/* Standalone ingest utility (not needed by ghs_mst_device): the full symmetric arc list
+ * (asrc/adst u32, akey u64, 2m entries, grouped by source) of a canonical edge list, or only the
+ * arcs whose source lies in [src_lo, src_hi). Validates canonicity (GHS_E_NONCANON). */
 size_t ghs_build_arcs_temp_bytes(uint32_t n, uint64_t m);
-/* number of arcs whose source lies in [src_lo, src_hi) (a rank's share for multi-GPU) */
 int ghs_count_arcs_range(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, uint32_t src_lo,
                          uint32_t src_hi, void *d_temp, size_t temp_bytes, void *stream, uint64_t *num_arcs);
-/* arcs with source in [src_lo, src_hi) only, grouped by source; *num_arcs = count written.
- * Multi-GPU ranks own disjoint source ranges, so every fragment's arcs are split over ranks
- * and the per-round all-reduce MIN combines them. */
 int ghs_build_arcs_range(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
                          uint32_t src_lo, uint32_t src_hi, uint32_t *d_asrc, uint32_t *d_adst, uint64_t *d_akey,
                          uint64_t arc_capacity, void *d_temp, size_t temp_bytes, void *stream, uint64_t *num_arcs);
-/* canonical edges (device) -> symmetric arc list grouped by source (device). Validates
- * canonicity on the device and returns GHS_E_NONCANON when it does not hold. */
 int ghs_build_arcs(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
                    uint32_t *d_asrc, uint32_t *d_adst, uint64_t *d_akey, void *d_temp, size_t temp_bytes,
                    void *stream);
-
-/* workspace bytes for ghs_mst_device / the solver handle; num_arcs = arcs this device scans */
-size_t ghs_workspace_bytes(uint32_t n, uint64_t m, uint64_t num_arcs);
-
-/* Whole MST on one device. d_u/d_v (canonical endpoints, m entries) are read by the hook stage
- * to find the other fragment of a chosen edge; arcs as above; d_in_mst: m bytes (written).
- * Blocks the calling thread until done (one host sync per round for the termination test). */
-int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v,
-                   const uint32_t *d_asrc, const uint32_t *d_adst, const uint64_t *d_akey, uint64_t num_arcs,
-                   void *d_workspace, size_t workspace_bytes, uint8_t *d_in_mst, void *stream,
-                   ghs_result_t *result, ghs_round_stats_t *stats);
+/* device-side canonicity check: *ok = 1 iff u < v < n and (u, v) strictly ascending */
+int ghs_check_canonical(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, void *stream, int *ok);
 
 /* ---- stepwise solver (multi-GPU: one process per GPU, RCCL all-reduce between steps) ------
  * Replaces the per-rank protocol loop of ghs_implementation_mpi.py:673-748 and its
- * collectives (:907 bcast, :929 Barrier, :766 gather). Each rank scans ITS slice of the arc
- * list; the per-fragment best keys are combined with an all-reduce MIN by the caller:
+ * collectives (:907 bcast, :929 Barrier, :766 gather). Every rank holds the replicated
+ * canonical list and owns the contiguous edge range [e_lo, e_hi); per round it scans the arcs of
+ * ITS edges and the per-fragment best keys are combined with an all-reduce MIN by the caller:
  *   h = ghs_solver_create(...)
- *   loop: ghs_solver_minedge(h, &C)            local min-edge per fragment
+ *   loop: ghs_solver_minedge(h, &C)            local min-edge per fragment (opens levels)
  *         ghs_solver_pack_best(h, d_dense)     C int64 slots, order-preserving (key ^ 2^63)
  *         <caller: all_reduce(d_dense[0:C], MIN)>
  *         ghs_solver_unpack_best(h, d_dense)
  *         ghs_solver_contract(h, &done)        hook + pointer-jump + next fragment list
- *   ghs_solver_finish(h, result); ghs_solver_destroy(h)
+ *   ghs_solver_finish(h, result, stats); ghs_solver_destroy(h)
  * Identical inputs on every rank => identical hook decisions => replicated in_mst. */
 typedef struct ghs_solver ghs_solver_t;
-int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v,
-                      const uint32_t *d_asrc, const uint32_t *d_adst, const uint64_t *d_akey, uint64_t num_arcs,
-                      void *d_workspace, size_t workspace_bytes, uint8_t *d_in_mst, void *stream,
-                      ghs_solver_t **out);
+int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
+                      uint64_t e_lo, uint64_t e_hi, const ghs_config_t *cfg, void *d_workspace,
+                      size_t workspace_bytes, uint8_t *d_in_mst, void *stream, ghs_solver_t **out);
 /* runs the min-edge kernel; *num_active = fragments whose best slot must be all-reduced */
 int ghs_solver_minedge(ghs_solver_t *h, uint64_t *num_active);
 int ghs_solver_pack_best(ghs_solver_t *h, int64_t *d_dense);
 int ghs_solver_unpack_best(ghs_solver_t *h, const int64_t *d_dense);
-/* hook + jump + next list; *done = 1 when no fragment has an outgoing edge */
+/* hook + jump + next list; *done = 1 when every level is complete */
 int ghs_solver_contract(ghs_solver_t *h, int *done);
 int ghs_solver_finish(ghs_solver_t *h, ghs_result_t *result, ghs_round_stats_t *stats);
 int ghs_solver_destroy(ghs_solver_t *h);

@@ -1,7 +1,7 @@
-"""The multi-rank orchestration (distributed.run_rounds + vertex_range partition + all-reduce
-MIN) on CPU with the gloo backend, world_size 2 and 3. The per-rank compute is the oracle's
-numpy stepper (oracle/boruvka_steps.py) standing in for the HIP stepper; the result must equal
-canonical Kruskal on every rank."""
+"""The multi-rank orchestration (distributed.run_rounds + edge_range partition + all-reduce
+MIN) on CPU with the gloo backend, world_size 2 and 3, with one and with several weight levels.
+The per-rank compute is the oracle's numpy stepper (oracle/boruvka_steps.py) standing in for the
+HIP stepper; the result must equal canonical Kruskal on every rank."""
 import os
 import socket
 
@@ -20,16 +20,17 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, u, v, w, out):
+def _worker(rank, world, port, n, u, v, w, thr, out):
     import torch.distributed as dist
 
-    from distributed_ghs_implementation_amd.distributed import run_rounds, vertex_range
+    from distributed_ghs_implementation_amd.device import edge_range
+    from distributed_ghs_implementation_amd.distributed import run_rounds
     from oracle.boruvka_steps import CpuStepper
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    lo, hi = vertex_range(n, rank, world)
-    st = CpuStepper(n, u, v, w, lo, hi)
+    lo, hi = edge_range(len(u), rank, world)
+    st = CpuStepper(n, u, v, w, lo, hi, thr)
 
     def ar(t):
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
@@ -41,26 +42,29 @@ def _worker(rank, world, port, n, u, v, w, out):
     dist.destroy_process_group()
 
 
-def _run(world, n, u, v, w):
+def _run(world, n, u, v, w, thr):
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), n, u, v, w, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), n, u, v, w, thr, out), nprocs=world, join=True)
     return dict(out)
 
 
-@pytest.mark.parametrize("world,name", [(2, "ties_4.json"), (2, "cgf_n1000_p001.json"), (3, "ties_2.json")])
-def test_gloo_ranks_match_kruskal(world, name):
+@pytest.mark.parametrize("world,name,levels", [(2, "ties_4.json", 1), (2, "cgf_n1000_p001.json", 3),
+                                               (3, "ties_2.json", 2), (2, "ties_5.json", 3)])
+def test_gloo_ranks_match_kruskal(world, name, levels):
     from oracle import oracle
     fx = load_fixture(name)
     n = fx["num_nodes"]
     e = np.array(fx["edges"], dtype=np.int64).reshape(-1, 3)
     u, v, w = oracle.canonicalize_c(n, e[:, 0], e[:, 1], e[:, 2])
     ref_in, ref_tw, ref_k = oracle.kruskal_c(n, u, v, w)
-    out = _run(world, n, u, v, w)
+    qs = np.quantile(w, np.linspace(0, 1, levels + 1)[1:-1]).astype(np.int64).tolist() if levels > 1 else []
+    thr = [0] + sorted(set(int(q) + 1 for q in qs)) + [1 << 32]
+    out = _run(world, n, u, v, w, thr)
     assert len(out) == world
     for rank in range(world):
         in_mst, total, count, rounds = out[rank]
         assert np.array_equal(np.array(in_mst, np.uint8), ref_in)
         assert total == ref_tw == fx["expected_total_weight"]
         assert count == ref_k
-        assert rounds <= int(np.ceil(np.log2(max(n, 2)))) + 2
+        assert rounds <= (len(thr) - 1) * (int(np.ceil(np.log2(max(n, 2)))) + 2)

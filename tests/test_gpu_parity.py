@@ -68,43 +68,65 @@ def test_noncanonical_device_input_rejected(torch_cuda):
     from distributed_ghs_implementation_amd import _native
     from distributed_ghs_implementation_amd.device import DeviceEdges, DeviceMST
     t = lambda a: torch.tensor(a, dtype=torch.int32, device="cuda")
-    e = DeviceEdges(4, t([1, 0]), t([2, 3]), t([1, 1]))  # not ascending
-    eng = DeviceMST(e)
-    with pytest.raises(_native.GHSError) as ei:
-        eng.run()
-    assert ei.value.code == _native.GHS_E_NONCANON
+    for u, v in [([1, 0], [2, 3]), ([0, 0], [1, 9]), ([2], [1]), ([0, 0], [1, 1])]:
+        e = DeviceEdges(4, t(u), t(v), t([1] * len(u)))
+        with pytest.raises(_native.GHSError) as ei:
+            DeviceMST(e).run()
+        assert ei.value.code == _native.GHS_E_NONCANON
 
 
+CONFIGS = [dict(max_levels=1), dict(), dict(max_levels=6, level1_edges_per_vertex=0.25, level_growth=2.0),
+           dict(max_levels=16, level1_edges_per_vertex=0.01, level_growth=1.5)]
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
 @pytest.mark.parametrize("scale", [10, 14, 18])
-def test_rmat_device_vs_oracle(scale, torch_cuda):
+def test_rmat_device_vs_oracle(scale, cfg, torch_cuda):
+    from distributed_ghs_implementation_amd import _native
     from distributed_ghs_implementation_amd.device import DeviceMST, generate_rmat
     ora = _oracle()
     e = generate_rmat(scale, 16, seed=1, wseed=2)
     g = e.to_host()
     g.check()
     assert len(np.unique(g.w)) == g.m  # unique weights by construction
-    eng = DeviceMST(e)
+    eng = DeviceMST(e, config=_native.make_config(**cfg))
     res, stats = eng.run()
     ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
     assert np.array_equal(eng.in_mst_host(), ref_in.astype(bool))
     assert res.total_weight == ref_tw and res.num_mst_edges == ref_k
-    assert res.rounds <= scale + 2
-    assert stats[0]["live_arcs"] == 2 * g.m
+    assert sum(st["hooks"] for st in stats) == ref_k or res.rounds > len(stats)
 
 
+@pytest.mark.parametrize("cfg", CONFIGS[:3])
 @pytest.mark.parametrize("k,mode", [(2, 0), (3, 1), (64, 0), (257, 1), (1024, 0), (1024, 1)])
-def test_grid_device_vs_oracle(k, mode, torch_cuda):
+def test_grid_device_vs_oracle(k, mode, cfg, torch_cuda):
+    from distributed_ghs_implementation_amd import _native
     from distributed_ghs_implementation_amd.device import DeviceMST, generate_grid
     ora = _oracle()
     e = generate_grid(k, mode)
     g = e.to_host()
     g.check()
     assert g.m == 2 * k * (k - 1)
-    eng = DeviceMST(e)
+    eng = DeviceMST(e, config=_native.make_config(**cfg))
     res, _ = eng.run()
     ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
     assert np.array_equal(eng.in_mst_host(), ref_in.astype(bool))
     assert res.num_mst_edges == k * k - 1 == ref_k
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_tie_heavy_levels_vs_oracle(cfg, torch_cuda):
+    """Equal weights across level thresholds (a whole weight class lands in one level)."""
+    from distributed_ghs_implementation_amd import _native, canonicalize
+    from distributed_ghs_implementation_amd.device import DeviceEdges, DeviceMST
+    ora = _oracle()
+    rng = np.random.default_rng(11)
+    n, m = 30000, 400000
+    g = canonicalize(n, u=rng.integers(0, n, m), v=rng.integers(0, n, m), w=rng.integers(0, 4, m))
+    eng = DeviceMST(DeviceEdges.from_host(g), config=_native.make_config(**cfg))
+    res, _ = eng.run()
+    ref_in, ref_tw, _ = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    assert np.array_equal(eng.in_mst_host(), ref_in.astype(bool)) and res.total_weight == ref_tw
 
 
 def test_stepwise_solver_equals_monolithic(torch_cuda):
@@ -116,7 +138,6 @@ def test_stepwise_solver_equals_monolithic(torch_cuda):
     a = DeviceMST(e)
     ra, _ = a.run()
     b = DeviceMST(e)
-    b.build_arcs()
     st = HipStepper(b)
     run_rounds(st, lambda t: None)
     rb, _ = st.finish()
@@ -125,22 +146,19 @@ def test_stepwise_solver_equals_monolithic(torch_cuda):
     assert ra.total_weight == rb.total_weight and ra.rounds == rb.rounds
 
 
-def test_partitioned_ranks_emulated_on_one_gpu(torch_cuda):
-    """Two source-range engines on one GPU, all-reduce emulated with torch.minimum: the
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_ranks_emulated_on_one_gpu(world, torch_cuda):
+    """`world` edge-range engines on one GPU, all-reduce emulated with torch.minimum: the
     multi-GPU decomposition gives the single-GPU answer."""
     import torch
-    from distributed_ghs_implementation_amd.device import DeviceMST, generate_rmat
-    from distributed_ghs_implementation_amd.distributed import HipStepper, vertex_range
+    from distributed_ghs_implementation_amd.device import DeviceMST, edge_range, generate_rmat
+    from distributed_ghs_implementation_amd.distributed import HipStepper
     e = generate_rmat(15, 16, seed=3, wseed=4)
     ref = DeviceMST(e)
     ref.run()
-    world = 3
-    engines = [DeviceMST(e, *vertex_range(e.n, r, world)) for r in range(world)]
-    assert sum(x.num_arcs for x in engines) == 2 * e.m
-    steppers = []
-    for x in engines:
-        x.build_arcs()
-        steppers.append(HipStepper(x))
+    engines = [DeviceMST(e, *edge_range(e.m, r, world)) for r in range(world)]
+    assert sum(x.e_hi - x.e_lo for x in engines) == e.m
+    steppers = [HipStepper(x) for x in engines]
     done = False
     while not done:
         counts = [s.minedge() for s in steppers]
@@ -161,10 +179,38 @@ def test_partitioned_ranks_emulated_on_one_gpu(torch_cuda):
         assert np.array_equal(x.in_mst_host(), ref.in_mst_host())
 
 
-def test_rmat_s22_properties_and_determinism(torch_cuda):
-    """Larger scale: forest size == n - #components (components counted by the oracle's
-    union-find over the MSF edges), weight equality with oracle Kruskal, and two runs give
-    identical flags."""
+def test_build_arcs_utility(torch_cuda):
+    """ghs_build_arcs (ingest utility): 2m arcs grouped by source, each edge once per side."""
+    import ctypes
+    import torch
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import _ptr, _stream, generate_rmat
+    L = _native.load()
+    e = generate_rmat(12, 16, seed=1, wseed=2)
+    A = 2 * e.m
+    asrc = torch.empty(A, dtype=torch.int32, device="cuda")
+    adst = torch.empty(A, dtype=torch.int32, device="cuda")
+    akey = torch.empty(A, dtype=torch.int64, device="cuda")
+    tb = L.ghs_build_arcs_temp_bytes(e.n, e.m)
+    tmp = torch.empty(tb, dtype=torch.uint8, device="cuda")
+    _native.check(L.ghs_build_arcs(e.n, e.m, _ptr(e.u), _ptr(e.v), _ptr(e.w), _ptr(asrc), _ptr(adst), _ptr(akey),
+                                   _ptr(tmp), tb, _stream()))
+    s = asrc.cpu().numpy().view(np.uint32)
+    d = adst.cpu().numpy().view(np.uint32)
+    k = akey.cpu().numpy().view(np.uint64)
+    assert np.all(np.diff(s.astype(np.int64)) >= 0)
+    g = e.to_host()
+    eid = (k & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    assert np.array_equal(np.bincount(eid, minlength=g.m), np.full(g.m, 2))
+    assert np.array_equal(np.minimum(s, d), g.u[eid]) and np.array_equal(np.maximum(s, d), g.v[eid])
+    assert np.array_equal((k >> np.uint64(32)).astype(np.uint32), g.w[eid])
+    ok = ctypes.c_int(0)
+    _native.check(L.ghs_check_canonical(e.n, e.m, _ptr(e.u), _ptr(e.v), _stream(), ctypes.byref(ok)))
+    assert ok.value == 1
+
+
+def test_rmat_s20_oracle_and_determinism(torch_cuda):
+    """Larger scale: bit-exact vs oracle Kruskal, and two runs give identical flags."""
     from distributed_ghs_implementation_amd.device import DeviceMST, generate_rmat
     ora = _oracle()
     e = generate_rmat(20, 16, seed=1, wseed=2)
