@@ -82,15 +82,17 @@ class Config(ctypes.Structure):
     """ghs_config_t: the weight-level plan of the filter (speed only; results never change)."""
     _fields_ = [
         ("max_levels", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("num_ranks", ctypes.c_uint32),
         ("level1_edges_per_vertex", ctypes.c_double),
         ("level_growth", ctypes.c_double),
     ]
 
 
-def make_config(max_levels=None, level1_edges_per_vertex=None, level_growth=None):
+def make_config(max_levels=None, level1_edges_per_vertex=None, level_growth=None, num_ranks=None):
     c = Config()
     load().ghs_default_config(ctypes.byref(c))
+    if num_ranks is not None:
+        c.num_ranks = int(num_ranks)
     if max_levels is not None:
         c.max_levels = int(max_levels)
     if level1_edges_per_vertex is not None:

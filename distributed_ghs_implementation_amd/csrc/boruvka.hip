@@ -464,86 +464,191 @@ __global__ void k_sample_weights(uint64_t cnt, const uint32_t *__restrict__ w, u
 }
 
 // ------------------------------------------------------------------------------------------
-// Level pass: canonical edges e in [e_lo, e_hi) with w_lo <= w < w_hi whose ends lie in
-// different fragments -> (lab[u], lab[v], key) into this block's staging region (block-private,
-// deterministic). FILTER = false for the first level (every vertex is its own fragment).
-// lab is fully resolved (one hop) when this runs.
+// Level pass. Splits the edges still pending into (a) this level's edges whose ends lie in
+// different fragments -> (lab[u], lab[v], key) into this block's level staging region, and
+// (b) heavier edges that also survive the fragment test -> (u, v, key) into this block's
+// REMAINING region, the next level's input. Edges whose ends share a fragment are dropped for
+// good (cycle property). Both outputs are block-private regions (deterministic, no atomics).
+// FIRST: the input is the canonical list itself [e_lo, e_hi) (u, v, w; key built here),
+// every vertex is its own fragment, and the pass also validates canonicity (u < v < n,
+// strictly ascending) into err bit 8 — before any kernel indexes an array with these ids.
+// Otherwise the input is the previous level's remaining regions (segmented view) and lab is
+// fully resolved (one hop); the giant-fragment bitmap rejects most heavy edges without a
+// label gather.
 // ------------------------------------------------------------------------------------------
-template <bool FILTER>
-__global__ __launch_bounds__(BLOCK) void k_level_select(uint64_t e_lo, uint64_t e_hi, const uint32_t *__restrict__ eu,
-                                                        const uint32_t *__restrict__ ev, const uint32_t *__restrict__ ew,
-                                                        uint32_t w_lo, uint64_t w_hi, const uint32_t *__restrict__ lab,
-                                                        const uint64_t *__restrict__ giant_bits,
-                                                        uint32_t *__restrict__ ssrc, uint32_t *__restrict__ sdst,
-                                                        uint64_t *__restrict__ skey, uint64_t *__restrict__ seg_count) {
+template <bool FIRST>
+__global__ __launch_bounds__(BLOCK) void k_level_pass(uint32_t n, uint64_t e_lo, const uint32_t *__restrict__ eu,
+                                                      const uint32_t *__restrict__ ev, const uint32_t *__restrict__ ew,
+                                                      const uint32_t *__restrict__ ru, const uint32_t *__restrict__ rv,
+                                                      const uint64_t *__restrict__ rkey, SegView in, uint64_t w_hi,
+                                                      const uint32_t *__restrict__ lab,
+                                                      const uint64_t *__restrict__ giant_bits,
+                                                      uint32_t *__restrict__ lsrc, uint32_t *__restrict__ ldst,
+                                                      uint64_t *__restrict__ lkey, uint64_t *__restrict__ lcount,
+                                                      uint32_t *__restrict__ ou, uint32_t *__restrict__ ov,
+                                                      uint64_t *__restrict__ okey, uint64_t *__restrict__ ostart,
+                                                      uint64_t *__restrict__ ocount,
+                                                      unsigned long long *__restrict__ err) {
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
-  const uint64_t T = e_hi - e_lo;
+  __shared__ uint32_t s_seg[2];
+  const uint64_t T = in.total;
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
   const uint64_t vb = Q * blockIdx.x;
   const uint64_t ve = (vb + Q < T) ? vb + Q : T;
-  uint64_t out_n = 0;
+  if (!FIRST) {
+    if (threadIdx.x == 0) {
+      s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
+      s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
+    }
+    __syncthreads();
+  }
+  uint64_t nlev = 0, nrem = 0;
+  bool bad = false;
   for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
     const uint64_t v = v0 + (uint64_t)threadIdx.x * 4;
-    uint32_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, w[4] = {0, 0, 0, 0};
-    bool sel[4] = {false, false, false, false};
-    const uint64_t e0 = e_lo + v;
-    if (v + 4 <= ve && (e0 & 3) == 0) {
-      const uint4 a4 = *reinterpret_cast<const uint4 *>(eu + e0);
-      const uint4 b4 = *reinterpret_cast<const uint4 *>(ev + e0);
-      const uint4 w4 = *reinterpret_cast<const uint4 *>(ew + e0);
-      a[0] = a4.x; a[1] = a4.y; a[2] = a4.z; a[3] = a4.w;
-      b[0] = b4.x; b[1] = b4.y; b[2] = b4.z; b[3] = b4.w;
-      w[0] = w4.x; w[1] = w4.y; w[2] = w4.z; w[3] = w4.w;
+    uint32_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+    uint64_t k[4] = {KEY_NONE, KEY_NONE, KEY_NONE, KEY_NONE};
+    bool live[4] = {false, false, false, false};
+    if (FIRST) {
+      const uint64_t e0 = e_lo + v;
+      uint32_t w[4] = {0, 0, 0, 0};
+      if (v + 4 <= ve && (e0 & 3) == 0) {
+        const uint4 a4 = *reinterpret_cast<const uint4 *>(eu + e0);
+        const uint4 b4 = *reinterpret_cast<const uint4 *>(ev + e0);
+        const uint4 w4 = *reinterpret_cast<const uint4 *>(ew + e0);
+        a[0] = a4.x; a[1] = a4.y; a[2] = a4.z; a[3] = a4.w;
+        b[0] = b4.x; b[1] = b4.y; b[2] = b4.z; b[3] = b4.w;
+        w[0] = w4.x; w[1] = w4.y; w[2] = w4.z; w[3] = w4.w;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) sel[j] = w[j] >= w_lo && (uint64_t)w[j] < w_hi;
-    } else {
+        for (int j = 0; j < 4; ++j) live[j] = true;
+      } else if (v < ve) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (v + j < ve) {
+            a[j] = eu[e0 + j];
+            b[j] = ev[e0 + j];
+            w[j] = ew[e0 + j];
+            live[j] = true;
+          }
+        }
+      }
+      if (v < ve) {  // canonical order: u < v < n, (u, v) strictly ascending
+        uint32_t pa = 0, pb = 0;
+        const bool has_prev = e0 > 0;
+        if (has_prev) {
+          pa = eu[e0 - 1];
+          pb = ev[e0 - 1];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (live[j]) {
+            bool ok = a[j] < b[j] && b[j] < n;
+            if (j > 0 || has_prev) ok = ok && (pa < a[j] || (pa == a[j] && pb < b[j]));
+            bad |= !ok;
+            pa = a[j];
+            pb = b[j];
+            k[j] = ((uint64_t)w[j] << 32) | (uint32_t)(e0 + j);
+            if (!ok) live[j] = false;  // never index with an unchecked id
+          }
+        }
+      }
+    } else if (v < ve) {
+      const uint32_t sidx = (s_seg[0] == s_seg[1]) ? s_seg[0] : seg_find(in.prefix, s_seg[0], s_seg[1], v);
+      const uint64_t seg_end = in.prefix[sidx + 1];
+      const uint64_t i0 = in.start[sidx] + (v - in.prefix[sidx]);
+      if (v + 4 <= seg_end && v + 4 <= ve && (i0 & 3) == 0) {
+        const uint4 a4 = *reinterpret_cast<const uint4 *>(ru + i0);
+        const uint4 b4 = *reinterpret_cast<const uint4 *>(rv + i0);
+        const ulonglong2 k01 = *reinterpret_cast<const ulonglong2 *>(rkey + i0);
+        const ulonglong2 k23 = *reinterpret_cast<const ulonglong2 *>(rkey + i0 + 2);
+        a[0] = a4.x; a[1] = a4.y; a[2] = a4.z; a[3] = a4.w;
+        b[0] = b4.x; b[1] = b4.y; b[2] = b4.z; b[3] = b4.w;
+        k[0] = k01.x; k[1] = k01.y; k[2] = k23.x; k[3] = k23.y;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool in_range = v + j < ve && v + j < seg_end;
+          a[j] = in_range ? ru[i0 + j] : LABEL_NONE;
+          b[j] = in_range ? rv[i0 + j] : 0u;
+          k[j] = in_range ? rkey[i0 + j] : KEY_NONE;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) live[j] = a[j] != LABEL_NONE;
+      // REJECT a whole class at once: both ends in the giant fragment (1-bit bitmap in L2;
+      // a is sorted within a region, so one word load usually serves a lane's 4 edges)
+      uint32_t wa_idx = 0xffffffffu;
+      uint64_t wa = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        if (v + j < ve) {
-          a[j] = eu[e0 + j];
-          b[j] = ev[e0 + j];
-          w[j] = ew[e0 + j];
-          sel[j] = w[j] >= w_lo && (uint64_t)w[j] < w_hi;
+        if (live[j]) {
+          if ((a[j] >> 6) != wa_idx) {
+            wa_idx = a[j] >> 6;
+            wa = giant_bits[wa_idx];
+          }
+          const bool ga = (wa >> (a[j] & 63)) & 1;
+          if (ga && ((giant_bits[b[j] >> 6] >> (b[j] & 63)) & 1)) live[j] = false;
         }
       }
     }
-    if (FILTER) {
-      // REJECT a whole class at once: both ends in the giant fragment (1-bit bitmap in L2)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (sel[j]) {
-          const bool ga = (giant_bits[a[j] >> 6] >> (a[j] & 63)) & 1;
-          const bool gb = (giant_bits[b[j] >> 6] >> (b[j] & 63)) & 1;
-          if (ga && gb) sel[j] = false;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (sel[j]) {
-          a[j] = lab[a[j]];
-          b[j] = lab[b[j]];
-          if (a[j] == b[j]) sel[j] = false;
-        }
-      }
-    }
-    uint32_t mine = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) mine += sel[j] ? 1u : 0u;
-    uint32_t total;
-    const uint32_t before = block_offsets(mine, s_wcnt, &total);
-    uint64_t pos = vb + out_n + before;
+    // fragment test + level/remaining split
+    uint32_t la[4], lb[4];
+    bool lev[4], rem[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if (sel[j]) {
-        ssrc[pos] = a[j];
-        sdst[pos] = b[j];
-        skey[pos] = ((uint64_t)w[j] << 32) | (uint32_t)(e0 + j);
-        ++pos;
+      la[j] = a[j];
+      lb[j] = b[j];
+      if (!FIRST && live[j]) {
+        la[j] = lab[a[j]];
+        lb[j] = lab[b[j]];
+        if (la[j] == lb[j]) live[j] = false;
+      }
+      const bool in_level = (k[j] >> 32) < w_hi;
+      lev[j] = live[j] && in_level;
+      rem[j] = live[j] && !in_level;
+    }
+    uint32_t mlev = 0, mrem = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mlev += lev[j] ? 1u : 0u;
+      mrem += rem[j] ? 1u : 0u;
+    }
+    uint32_t tlev, trem;
+    const uint32_t blev = block_offsets(mlev, s_wcnt, &tlev);
+    const uint32_t brem = block_offsets(mrem, s_wcnt, &trem);
+    uint64_t pl = vb + nlev + blev, pr = vb + nrem + brem;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (lev[j]) {
+        lsrc[pl] = la[j];
+        ldst[pl] = lb[j];
+        lkey[pl] = k[j];
+        ++pl;
+      }
+      if (rem[j]) {
+        ou[pr] = a[j];
+        ov[pr] = b[j];
+        okey[pr] = k[j];
+        ++pr;
       }
     }
-    out_n += total;
+    nlev += tlev;
+    nrem += trem;
   }
-  if (threadIdx.x == 0) seg_count[blockIdx.x] = (vb < T) ? out_n : 0;
+  if (FIRST && bad) atomicOr(err, 8ull);
+  // remaining regions padded to a multiple of 4 with dead entries (u = LABEL_NONE)
+  const uint64_t padded = (nrem + 3) & ~3ull;
+  if (threadIdx.x < padded - nrem) {
+    const uint64_t pos = vb + nrem + threadIdx.x;
+    ou[pos] = LABEL_NONE;
+    ov[pos] = 0;
+    okey[pos] = KEY_NONE;
+  }
+  if (threadIdx.x == 0) {
+    lcount[blockIdx.x] = (vb < T) ? nlev : 0;
+    ostart[blockIdx.x] = vb;
+    ocount[blockIdx.x] = (vb < T) ? padded : 0;
+  }
 }
 
 // staging segments -> dense forward arcs [0, S) of the level arc buffer (order preserved)
@@ -575,6 +680,14 @@ __global__ void k_fill_reverse(uint64_t S, const uint32_t *__restrict__ idx, uin
     const uint32_t j = idx[i];
     adst[S + i] = asrc[j];
     akey[S + i] = akey[j];
+  }
+}
+
+// flag every fragment that has an arc in the level: run heads of the (grouped) source labels
+__global__ void k_mark_sources(uint64_t A, const uint32_t *__restrict__ src, uint8_t *__restrict__ flags) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < A; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = src[i];
+    if (i == 0 || src[i - 1] != c) flags[c] = 1;
   }
 }
 
@@ -642,6 +755,10 @@ struct ghs_solver {
   uint8_t *flags = nullptr;
   uint32_t *sample = nullptr;
   ArcBuf buf[2];
+  ArcBuf rem[2];             // remaining (not yet levelled) edges: u, v, key as block regions
+  int rcur = 0;              // rem buffer holding the pending edges (level >= 1)
+  uint64_t rem_total = 0;    // pending edges (incl. padding) after the last level pass
+  uint32_t rem_nseg = 1;     // regions of the pending edges
   uint64_t cap_arcs = 0;
   void *cub_temp = nullptr;
   size_t cub_bytes = 0;
@@ -674,7 +791,8 @@ struct ghs_solver {
 
 static std::mutex g_mutex;  // the one-shot entry points are serialised per process
 
-static constexpr uint32_t NSAMPLE = 65536;
+static constexpr uint32_t NSAMPLE = 8192;    // labels sampled to find the giant fragment
+static constexpr uint32_t NSAMPLE_W = 16384; // weights sampled for the level plan
 
 static size_t cub_temp_bytes(uint32_t n, uint64_t cap) {
   size_t a = 0, b = 0, c = 0;
@@ -716,6 +834,15 @@ static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, 
     p = carve(SEG_G * 8); if (s) s->buf[b].seg_count = (uint64_t *)p;
     p = carve((SEG_G + 1) * 8); if (s) s->buf[b].seg_prefix = (uint64_t *)p;
   }
+  const uint64_t rcap = local_edges + 4 * SEG_G;
+  for (int b = 0; b < 2; ++b) {
+    p = carve(rcap * 4); if (s) s->rem[b].src = (uint32_t *)p;
+    p = carve(rcap * 4); if (s) s->rem[b].dst = (uint32_t *)p;
+    p = carve(rcap * 8); if (s) s->rem[b].key = (uint64_t *)p;
+    p = carve(SEG_G * 8); if (s) s->rem[b].seg_start = (uint64_t *)p;
+    p = carve(SEG_G * 8); if (s) s->rem[b].seg_count = (uint64_t *)p;
+    p = carve((SEG_G + 1) * 8); if (s) s->rem[b].seg_prefix = (uint64_t *)p;
+  }
   const size_t cb = cub_temp_bytes(n, cap);
   p = carve(cb); if (s) { s->cub_temp = p; s->cub_bytes = cb; s->cap_arcs = cap; }
   p = carve(8 * sizeof(unsigned long long)); if (s) s->cnt = (unsigned long long *)p;
@@ -739,32 +866,33 @@ static void record(ghs_solver *s, int k) {
 }
 
 static void default_config(ghs_config_t *c) {
-  c->max_levels = 3;
-  c->level1_edges_per_vertex = 2.0;
-  c->level_growth = 8.0;
+  c->max_levels = 8;
+  c->num_ranks = 1;
+  c->level1_edges_per_vertex = 0.5;
+  c->level_growth = 4.0;
 }
 
 // ---- level planning: thresholds from a sample of the GLOBAL canonical weights ----------------
 static int plan_levels(ghs_solver *s) {
   s->thresholds.clear();
   s->thresholds.push_back(0);
-  const uint32_t L = std::max<uint32_t>(1, std::min<uint32_t>(s->cfg.max_levels, 16));
+  const uint32_t L = std::max<uint32_t>(1, std::min<uint32_t>(s->cfg.max_levels, 32));
   if (L > 1 && s->m > 0) {
-    const uint32_t ns = (uint32_t)std::min<uint64_t>(NSAMPLE, s->m);
+    const uint32_t ns = (uint32_t)std::min<uint64_t>(NSAMPLE_W, s->m);
     k_sample_weights<<<grid_for(ns, 256, 256), 256, 0, s->stream>>>(s->m, s->ew, ns, s->sample);
     GHS_HIP_CHECK(hipGetLastError());
     GHS_HIP_CHECK(hipMemcpyAsync(s->h_sample, s->sample, ns * 4, hipMemcpyDeviceToHost, s->stream));
     GHS_HIP_CHECK(hipStreamSynchronize(s->stream));
     std::vector<uint32_t> w(s->h_sample, s->h_sample + ns);
-    std::sort(w.begin(), w.end());
     double target = s->cfg.level1_edges_per_vertex * (double)s->n;
     for (uint32_t i = 1; i < L; ++i) {
       const double frac = target / (double)s->m;
       if (frac >= 1.0) break;
       const size_t q = (size_t)(frac * ns);
-      target *= s->cfg.level_growth;
+      target *= std::max(1.01, s->cfg.level_growth);
       if (q == 0) continue;
-      const uint64_t thr = (uint64_t)w[std::min<size_t>(q, ns - 1)];
+      std::nth_element(w.begin(), w.begin() + q, w.end());
+      const uint64_t thr = (uint64_t)w[q];
       if (thr > s->thresholds.back()) s->thresholds.push_back(thr);
     }
   }
@@ -772,15 +900,16 @@ static int plan_levels(ghs_solver *s) {
   return GHS_OK;
 }
 
-// ---- open the next level: select + filter its edges, build its arcs, set the active list ----
+// ---- open the next level: split pending edges, build the level's arcs, set the active list ---
+// Returns GHS_OK with s->level_open set, or with the level skipped (single rank, no arcs).
 static int open_level(ghs_solver *s) {
   const uint32_t lv = s->level;
-  const uint32_t w_lo = (uint32_t)s->thresholds[lv];
   const uint64_t w_hi = s->thresholds[lv + 1];
   const bool first = (lv == 0);
   hipStream_t st = s->stream;
   ArcBuf &X = s->buf[0], &Y = s->buf[1];
-  const uint64_t T = s->e_hi - s->e_lo;
+  const int rin = s->rcur, rout = first ? 0 : (s->rcur ^ 1);
+  ArcBuf &RI = s->rem[rin], &RO = s->rem[rout];
 
   if (!first) {
     // compress labels, find the giant fragment from a sample, build its bitmap
@@ -790,39 +919,65 @@ static int open_level(ghs_solver *s) {
     GHS_HIP_CHECK(hipGetLastError());
     GHS_HIP_CHECK(hipMemcpyAsync(s->h_sample, s->sample, ns * 4, hipMemcpyDeviceToHost, st));
     GHS_HIP_CHECK(hipStreamSynchronize(st));
-    std::unordered_map<uint32_t, uint32_t> freq;
-    uint32_t giant = s->h_sample[0], gc = 0;
-    for (uint32_t i = 0; i < ns; ++i) {
-      const uint32_t c = ++freq[s->h_sample[i]];
-      if (c > gc || (c == gc && s->h_sample[i] < giant)) {
-        gc = c;
-        giant = s->h_sample[i];
+    std::vector<uint32_t> smp(s->h_sample, s->h_sample + ns);
+    std::sort(smp.begin(), smp.end());
+    uint32_t giant = smp[0];
+    size_t best_run = 0;
+    for (size_t i = 0; i < smp.size();) {
+      size_t j = i;
+      while (j < smp.size() && smp[j] == smp[i]) ++j;
+      if (j - i > best_run) {
+        best_run = j - i;
+        giant = smp[i];
       }
+      i = j;
     }
     k_bitmap<<<grid_for(s->n, BLOCK, 16384), BLOCK, 0, st>>>(s->n, s->lab, giant, s->bits);
     GHS_HIP_CHECK(hipGetLastError());
   }
 
-  // 1. this level's edges (filtered) into block-private staging regions of Y
+  // 1. split: this level's surviving edges -> Y staging; heavier survivors -> RO regions
+  const uint64_t T = first ? (s->e_hi - s->e_lo) : s->rem_total;
   const unsigned G = grid_for(T, ARCS_PER_BLOCK, SEG_G);
+  SegView in{RI.seg_start, RI.seg_prefix, s->rem_nseg, T};
   if (T) {
     if (first)
-      k_level_select<false><<<G, BLOCK, 0, st>>>(s->e_lo, s->e_hi, s->eu, s->ev, s->ew, w_lo, w_hi, s->lab, s->bits,
-                                                 Y.src, Y.dst, Y.key, Y.seg_count);
+      k_level_pass<true><<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->eu, s->ev, s->ew, nullptr, nullptr, nullptr, in, w_hi,
+                                              s->lab, s->bits, Y.src, Y.dst, Y.key, Y.seg_count, RO.src, RO.dst,
+                                              RO.key, RO.seg_start, RO.seg_count, s->cnt + 4);
     else
-      k_level_select<true><<<G, BLOCK, 0, st>>>(s->e_lo, s->e_hi, s->eu, s->ev, s->ew, w_lo, w_hi, s->lab, s->bits,
-                                                Y.src, Y.dst, Y.key, Y.seg_count);
+      k_level_pass<false><<<G, BLOCK, 0, st>>>(s->n, 0, nullptr, nullptr, nullptr, RI.src, RI.dst, RI.key, in, w_hi,
+                                               s->lab, s->bits, Y.src, Y.dst, Y.key, Y.seg_count, RO.src, RO.dst,
+                                               RO.key, RO.seg_start, RO.seg_count, s->cnt + 4);
     GHS_HIP_CHECK(hipGetLastError());
     k_scan_counts<<<1, 1024, 0, st>>>(Y.seg_count, G, Y.seg_prefix, s->cnt + 0);
-    // 2. dense forward arcs X[0, S) (canonical order kept: grouped by the source's vertex)
+    k_scan_counts<<<1, 1024, 0, st>>>(RO.seg_count, G, RO.seg_prefix, s->cnt + 5);
+    // 2. dense forward arcs X[0, S) (order kept: grouped by the source's vertex)
     k_gather_segments<<<G, BLOCK, 0, st>>>(T, Y.seg_prefix, Y.src, Y.dst, Y.key, X.src, X.dst, X.key);
     GHS_HIP_CHECK(hipGetLastError());
   } else {
     GHS_HIP_CHECK(hipMemsetAsync(s->cnt, 0, 8, st));
+    GHS_HIP_CHECK(hipMemsetAsync(s->cnt + 5, 0, 8, st));
   }
-  GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, 8, hipMemcpyDeviceToHost, st));
+  GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   GHS_HIP_CHECK(hipStreamSynchronize(st));
+  if (s->h_cnt[4] & 8) {
+    s->phase = 2;
+    GHS_FAIL(GHS_E_NONCANON, "edge list is not canonical (need u < v < n, strictly ascending (u, v))");
+  }
+  if (s->h_cnt[4]) {
+    s->phase = 2;
+    GHS_FAIL(GHS_E_STATE, "internal invariant violated (code " + std::to_string(s->h_cnt[4]) + ")");
+  }
   const uint64_t S = s->h_cnt[0];
+  s->rem_total = s->h_cnt[5];
+  s->rem_nseg = G;
+  s->rcur = rout;
+  s->level_arcs = 2 * S;
+  if (S == 0 && s->cfg.num_ranks <= 1) {  // nothing to merge at this level (single rank only:
+    s->level_open = false;                // ranks must run the same rounds)
+    return GHS_OK;
+  }
   // 3. reverse arcs X[S, 2S): radix sort (dst label, index) -> grouped by dst label
   if (S) {
     uint32_t *idx_in = Y.src, *idx_out = Y.dst;  // Y's staging is consumed
@@ -836,18 +991,28 @@ static int open_level(ghs_solver *s) {
   s->cur = 0;
   s->cur_single = true;
   s->cur_arcs = 2 * S;
-  s->level_arcs = 2 * S;
   k_set_seg1<<<1, 1, 0, st>>>(X.seg_start, X.seg_prefix, s->cur_arcs);
   GHS_HIP_CHECK(hipGetLastError());
 
-  // 4. active fragments: every current root (first level: every vertex). Identical on every
-  //    rank (the fragment state is replicated); roots without arcs anywhere drop out after
-  //    their first round (best stays NONE).
-  if (first) {
+  // 4. active fragments. Single rank: the fragments that have an arc in this level.
+  //    Several ranks: every current root (first level: every vertex) — identical on every
+  //    rank without an exchange; roots without arcs anywhere drop out after one round.
+  size_t cb = s->cub_bytes;
+  if (s->cfg.num_ranks <= 1) {
+    GHS_HIP_CHECK(hipMemsetAsync(s->flags, 0, s->n, st));
+    k_mark_sources<<<grid_for(2 * S, 256, 16384), 256, 0, st>>>(2 * S, X.src, s->flags);
+    GHS_HIP_CHECK(hipGetLastError());
+    GHS_HIP_CHECK(hipcub::DeviceSelect::Flagged(s->cub_temp, cb, hipcub::CountingInputIterator<uint32_t>(0u), s->flags,
+                                                s->act[0], s->cnt + 1, (size_t)s->n, st));
+    GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt + 1, s->cnt + 1, 8, hipMemcpyDeviceToHost, st));
+    GHS_HIP_CHECK(hipStreamSynchronize(st));
+    s->act_ident = false;
+    s->act_cur = 0;
+    s->nact = s->h_cnt[1];
+  } else if (first) {
     s->act_ident = true;
     s->nact = s->n;
   } else {
-    size_t cb = s->cub_bytes;
     GHS_HIP_CHECK(hipcub::DeviceSelect::Flagged(s->cub_temp, cb, hipcub::CountingInputIterator<uint32_t>(0u), s->flags,
                                                 s->act[0], s->cnt + 1, (size_t)s->n, st));
     GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt + 1, s->cnt + 1, 8, hipMemcpyDeviceToHost, st));
@@ -899,13 +1064,6 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   if (((uintptr_t)d_workspace) & 255) GHS_FAIL(GHS_E_ARG, "workspace must be 256-byte aligned");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) GHS_FAIL(GHS_E_NODEVICE, "no HIP device");
-  {
-    // every kernel indexes n-sized arrays with these ids: validate before launching anything
-    int ok = 1;
-    const int rc0 = ghs_check_canonical(n, m, d_u, d_v, stream, &ok);
-    if (rc0) return rc0;
-    if (!ok) GHS_FAIL(GHS_E_NONCANON, "edge list is not canonical (need u < v < n, strictly ascending (u, v))");
-  }
 
   ghs_solver *s = new ghs_solver();
   s->n = n; s->m = m; s->e_lo = e_lo; s->e_hi = e_hi;
@@ -954,9 +1112,15 @@ int ghs_solver_minedge(ghs_solver_t *s, uint64_t *num_active) {
   }
   if (s->phase != 0) GHS_FAIL(GHS_E_STATE, "minedge called twice without contract");
   if (s->round >= 16 * GHS_MAX_ROUND_STATS) GHS_FAIL(GHS_E_ROUNDCAP, "round cap exceeded");
-  if (!s->level_open) {
+  while (!s->level_open) {
+    if (s->level + 1 >= s->thresholds.size()) {  // every level done
+      s->phase = 2;
+      if (num_active) *num_active = 0;
+      return GHS_OK;
+    }
     int rc = open_level(s);
     if (rc) return rc;
+    if (!s->level_open) s->level += 1;  // skipped (no arcs)
   }
   record(s, 0);
   const uint64_t A = s->cur_arcs;
@@ -1072,7 +1236,8 @@ int ghs_solver_contract(ghs_solver_t *s, int *done) {
   if (s->nact == 0) {  // level complete
     s->level_open = false;
     s->level += 1;
-    s->phase = (s->level + 1 >= s->thresholds.size()) ? 2 : 0;
+    const bool no_more = (s->level + 1 >= s->thresholds.size()) || (s->cfg.num_ranks <= 1 && s->rem_total == 0);
+    s->phase = no_more ? 2 : 0;
   } else {
     s->phase = 0;
   }

@@ -111,6 +111,9 @@ class DistributedMST:
         self.world = dist.get_world_size(group) if world is None else world
         self.group = group
         lo, hi = edge_range(edges.m, self.rank, self.world)
+        if config is None:
+            config = _native.make_config(num_ranks=self.world)
+        config.num_ranks = self.world
         self.engine = DeviceMST(edges, lo, hi, config)
         self.edges = edges
 

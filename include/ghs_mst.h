@@ -75,7 +75,8 @@ typedef struct ghs_result {
  * levels. Results do not depend on the plan (only speed does). */
 typedef struct ghs_config {
   uint32_t max_levels;
-  uint32_t reserved;
+  uint32_t num_ranks;         /* ranks sharing the solve (1 = single GPU; >1: identical rounds on
+                                 every rank, so empty levels are not skipped) */
   double level1_edges_per_vertex;
   double level_growth;
 } ghs_config_t;

@@ -1,0 +1,50 @@
+"""Sweep the weight-level plan (speed only; results must not change) on one GPU."""
+import argparse
+import itertools
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=int, default=24)
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    import torch
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import DeviceMST, generate_rmat
+    e = generate_rmat(args.scale, 16, seed=1, wseed=2)
+    torch.cuda.synchronize()
+    ref = None
+    for L, l1, gr in itertools.product([1, 2, 3, 4, 8, 16], [0.125, 0.25, 0.5, 1.0], [2.0, 4.0, 8.0]):
+        if L == 1 and (l1 != 0.25 or gr != 2.0):
+            continue
+        if L == 2 and gr != 2.0:
+            continue
+        cfg = _native.make_config(max_levels=L, level1_edges_per_vertex=l1, level_growth=gr)
+        eng = DeviceMST(e, config=cfg)
+        eng.run()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            res, stats = eng.run()
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        if ref is None:
+            ref = res.total_weight
+        assert res.total_weight == ref
+        kern = sum(s["ms_minedge"] + s["ms_hook"] + s["ms_jump"] + s["ms_active"] for s in stats)
+        print(json.dumps({"levels": L, "l1": l1, "growth": gr, "ms": round(min(ts), 3), "rounds": res.rounds,
+                          "planned_levels": res.levels, "round_kernels_ms": round(kern, 3),
+                          "arcs_per_level": [s["level_arcs"] for s in stats if s["level_arcs"]]}), flush=True)
+        del eng
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
