@@ -793,6 +793,7 @@ static std::mutex g_mutex;  // the one-shot entry points are serialised per proc
 
 static constexpr uint32_t NSAMPLE = 8192;    // labels sampled to find the giant fragment
 static constexpr uint32_t NSAMPLE_W = 16384; // weights sampled for the level plan
+static constexpr uint32_t NSAMPLE_MAX = NSAMPLE_W > NSAMPLE ? NSAMPLE_W : NSAMPLE;
 
 static size_t cub_temp_bytes(uint32_t n, uint64_t cap) {
   size_t a = 0, b = 0, c = 0;
@@ -825,7 +826,7 @@ static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, 
   p = carve(N * 4); if (s) s->act[1] = (uint32_t *)p;
   p = carve(N ? N : 1); if (s) s->flags = (uint8_t *)p;
   p = carve(((N + 63) / 64) * 8 + 8); if (s) s->bits = (uint64_t *)p;
-  p = carve(NSAMPLE * 4); if (s) s->sample = (uint32_t *)p;
+  p = carve(NSAMPLE_MAX * 4); if (s) s->sample = (uint32_t *)p;
   for (int b = 0; b < 2; ++b) {
     p = carve(cap * 4); if (s) s->buf[b].src = (uint32_t *)p;
     p = carve(cap * 4); if (s) s->buf[b].dst = (uint32_t *)p;
@@ -1081,7 +1082,7 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   hipError_t e;
   if ((e = hipHostMalloc((void **)&s->h_cnt, 8 * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess)
     return fail(e, "hipHostMalloc");
-  if ((e = hipHostMalloc((void **)&s->h_sample, NSAMPLE * 4, hipHostMallocDefault)) != hipSuccess)
+  if ((e = hipHostMalloc((void **)&s->h_sample, NSAMPLE_MAX * 4, hipHostMallocDefault)) != hipSuccess)
     return fail(e, "hipHostMalloc");
   s->t0 = std::chrono::steady_clock::now();
   if (n) {
