@@ -73,6 +73,13 @@ constexpr uint32_t JUMP_MAX_STEPS = 1u << 26;
 
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
+// best[c] = min(best[c], k). A plain read first: best only ever decreases, so a stale read is
+// never below the true value and skipping on best <= k is always safe.
+__device__ __forceinline__ void flush_min(uint64_t *__restrict__ best, uint32_t c, uint64_t k) {
+  uint64_t *p = best + c;
+  if (*p > k) atomicMin(reinterpret_cast<unsigned long long *>(p), (unsigned long long)k);
+}
+
 // Block-wide exclusive offsets for a compaction step: each lane contributes `mine` items and
 // gets the count of items of lower lanes of the whole block; *total = block total.
 // Every thread of the block must call it (two barriers).
@@ -150,6 +157,8 @@ __global__ __launch_bounds__(BLOCK) void k_minedge(const uint32_t *__restrict__ 
   __syncthreads();
   const uint32_t slo = s_seg[0], shi = s_seg[1];
   uint64_t out_n = 0;  // survivors written so far by this block
+  uint32_t carry_l = LABEL_NONE;  // wave-uniform deferred run (label, min key)
+  uint64_t carry_v = KEY_NONE;
 
   for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
     const uint64_t v = v0 + (uint64_t)threadIdx.x * ARCS_PER_THREAD;
@@ -207,6 +216,22 @@ __global__ __launch_bounds__(BLOCK) void k_minedge(const uint32_t *__restrict__ 
       }
     }
 
+    uint32_t smask = 0;  // survivors (inter-fragment arcs), taken before the carry merge
+#pragma unroll
+    for (int j = 0; j < 4; ++j) smask |= (V[j] != KEY_NONE) ? (1u << j) : 0u;
+    // Deferred run of the previous iteration (wave-uniform carry): a run that reaches the
+    // wave's end is not flushed but carried, and merged into the next run of the same label
+    // (min is associative, contiguity is not needed). A giant fragment's run of millions of
+    // arcs then costs one atomic per wave instead of one per 256 arcs (same-address atomics
+    // serialise at the memory side).
+    if (lane == 0 && L[0] == carry_l && carry_l != LABEL_NONE) {
+      V[0] = umin64(V[0], carry_v);
+      carry_l = LABEL_NONE;  // merged
+    }
+    carry_l = __shfl(carry_l, 0);
+    if (carry_l != LABEL_NONE && lane == 0) flush_min(best, carry_l, carry_v);  // not merged
+    carry_l = LABEL_NONE;
+
     // ---- wave-wide segmented min over 256 arcs, segments = runs of equal source label
     const uint32_t prevL3 = __shfl_up(L[3], 1);
     bool H[4];
@@ -236,23 +261,25 @@ __global__ __launch_bounds__(BLOCK) void k_minedge(const uint32_t *__restrict__ 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       run = H[j] ? V[j] : umin64(run, V[j]);
+      const bool wave_end = (j == 3) && (lane == WAVE - 1);
       const bool tail = (j < 3) ? H[j + 1] : (lane == WAVE - 1 || nextH0);
-      if (tail && run != KEY_NONE) {
-        uint64_t *p = best + L[j];
-        if (*p > run) atomicMin(reinterpret_cast<unsigned long long *>(p), (unsigned long long)run);
+      if (tail && !wave_end && run != KEY_NONE) flush_min(best, L[j], run);
+      if (wave_end) {
+        carry_l = (run != KEY_NONE) ? L[3] : LABEL_NONE;
+        carry_v = run;
       }
     }
+    carry_l = __shfl(carry_l, WAVE - 1);
+    carry_v = __shfl(carry_v, WAVE - 1);
 
     if (COMPACT) {
-      uint32_t mine = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) mine += (V[j] != KEY_NONE) ? 1u : 0u;
+      const uint32_t mine = (uint32_t)__popc(smask);
       uint32_t total;
       const uint32_t before = block_offsets(mine, s_wcnt, &total);
       uint64_t pos = vb + out_n + before;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        if (V[j] != KEY_NONE) {
+        if (smask & (1u << j)) {
           osrc[pos] = L[j];
           odst[pos] = D[j];
           okey[pos] = K[j];
@@ -262,6 +289,7 @@ __global__ __launch_bounds__(BLOCK) void k_minedge(const uint32_t *__restrict__ 
       out_n += total;
     }
   }
+  if (lane == 0 && carry_l != LABEL_NONE) flush_min(best, carry_l, carry_v);
   if (COMPACT) {
     // pad to a multiple of 4 with dead arcs; stays inside [vb, vb + Q) and below the capacity
     // (the workspace reserves 4 * SEG_G spare arcs)
