@@ -48,7 +48,6 @@
 // is refreshed every round by k_jump. A vertex's fragment is found by following lab[] to a
 // fixpoint (find_lab); k_resolve compresses every vertex to its root between levels.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -78,6 +77,44 @@ __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < 
 __device__ __forceinline__ void flush_min(uint64_t *__restrict__ best, uint32_t c, uint64_t k) {
   uint64_t *p = best + c;
   if (*p > k) atomicMin(reinterpret_cast<unsigned long long *>(p), (unsigned long long)k);
+}
+
+// Per-block LDS cache of fragment minima. A run tail (label L, min key k) lands in a
+// direct-mapped slot: if the slot holds L (or is claimed for L now) the min is taken in LDS
+// (native ds_min_u64), else it goes to best[] directly. The block flushes its slots once at the
+// end. A fragment with arcs all over the stream (the giant) then costs one global update per
+// block instead of one per run — same-address global operations serialise at the memory side
+// (~12 ns each, MI355X_MICROARCH.md "fanin") and atomics drop the line from L2, so every later
+// plain read of that slot misses too.
+constexpr int HOT_BITS = 9;
+constexpr int HOT_SLOTS = 1 << HOT_BITS;
+
+__device__ __forceinline__ void hot_init(uint32_t *s_hl, unsigned long long *s_hk) {
+  for (int i = threadIdx.x; i < HOT_SLOTS; i += BLOCK) {
+    s_hl[i] = LABEL_NONE;
+    s_hk[i] = KEY_NONE;
+  }
+}
+
+__device__ __forceinline__ void hot_min(uint32_t *s_hl, unsigned long long *s_hk, uint64_t *__restrict__ best,
+                                        uint32_t L, uint64_t k) {
+  const uint32_t slot = (L * 0x9E3779B1u) >> (32 - HOT_BITS);
+  uint32_t cur = s_hl[slot];
+  if (cur == LABEL_NONE) {
+    cur = atomicCAS(&s_hl[slot], LABEL_NONE, L);
+    if (cur == LABEL_NONE) cur = L;
+  }
+  if (cur == L)
+    atomicMin(&s_hk[slot], (unsigned long long)k);
+  else
+    flush_min(best, L, k);
+}
+
+__device__ __forceinline__ void hot_flush(const uint32_t *s_hl, const unsigned long long *s_hk, uint64_t *__restrict__ best) {
+  for (int i = threadIdx.x; i < HOT_SLOTS; i += BLOCK) {
+    const uint32_t L = s_hl[i];
+    if (L != LABEL_NONE && s_hk[i] != KEY_NONE) flush_min(best, L, s_hk[i]);
+  }
 }
 
 // Block-wide exclusive offsets for a compaction step: each lane contributes `mine` items and
@@ -125,28 +162,57 @@ __device__ __forceinline__ uint32_t seg_find(const uint64_t *__restrict__ prefix
 }
 
 // ------------------------------------------------------------------------------------------
-// Stage 1: minimum outgoing edge per fragment (+ fused REJECT filter / stream compaction).
-//
-// Each lane owns 4 consecutive arcs (16-B loads of src/dst, 2x16-B of key). Arcs are grouped by
-// source, so equal source labels form runs; a wave-wide segmented min-scan over its 256 arcs
-// (in-lane serial + 6-step cross-lane scan) leaves one candidate per run, and only run tails
-// touch best[] — after a plain read, since best only ever decreases (a stale read is never
-// smaller than the true value, so skipping on `best <= cand` is always safe).
-// IDENT: labels are already current roots (a level's first round): no gathers, dst not read.
-// COMPACT: survivors (inter-fragment arcs) are written relabelled to this block's output segment.
-// Dead arcs (src == LABEL_NONE) pad segments and are skipped.
+// Segmented edge input: every region holds a multiple of 4 entries and starts at a multiple of
+// 4 (dead entries, a == LABEL_NONE, pad the regions), so a lane's 4-entry tile at a virtual
+// index v (a multiple of 4) lies wholly inside one region. Tiles past the block's range read
+// the tile at index 0 (always allocated) and are masked, so every load is unconditional.
+// ------------------------------------------------------------------------------------------
+struct EdgeTile {
+  uint4 a, b;
+  ulonglong2 k01, k23;
+};
+
+__device__ __forceinline__ uint64_t tile_phys(const SegView &in, uint32_t slo, uint32_t shi, uint64_t v, uint64_t ve) {
+  if (v >= ve) return 0;
+  const uint32_t sidx = (slo == shi) ? slo : seg_find(in.prefix, slo, shi, v);
+  return in.start[sidx] + (v - in.prefix[sidx]);
+}
+
+__device__ __forceinline__ void tile_load(EdgeTile &t, const uint32_t *__restrict__ ea, const uint32_t *__restrict__ eb,
+                                          const uint64_t *__restrict__ ek, uint64_t i0) {
+  t.a = *reinterpret_cast<const uint4 *>(ea + i0);
+  t.b = *reinterpret_cast<const uint4 *>(eb + i0);
+  t.k01 = *reinterpret_cast<const ulonglong2 *>(ek + i0);
+  t.k23 = *reinterpret_cast<const ulonglong2 *>(ek + i0 + 2);
+}
+
+// ------------------------------------------------------------------------------------------
+// Stage 1: minimum outgoing edge per fragment (+ fused REJECT filter / stream compaction),
+// edge-centric: every live edge (a, b, key) of the level is a candidate for BOTH fragments.
+//  a-side: the edges keep the canonical order (grouped by the a vertex), so equal a labels form
+//    runs; a wave-wide segmented min-scan over its 256 edges (in-lane serial + 6-step cross-lane
+//    scan) leaves one candidate per run, and only run tails touch the fragment minima.
+//  b-side: one candidate per edge.
+// Candidates go through the block's LDS cache (hot_min) and then best[] — after a plain read,
+// since best only ever decreases (a stale read is never smaller than the true value, so skipping
+// on `best <= cand` is always safe).
+// IDENT: labels are already current roots (a level's first round): no label gathers.
+// COMPACT: survivors (inter-fragment edges) are written relabelled to this block's output
+// region (padded to a multiple of 4 with dead entries).
 // ------------------------------------------------------------------------------------------
 template <bool IDENT, bool COMPACT>
-__global__ __launch_bounds__(BLOCK) void k_minedge(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
-                                                   const uint64_t *__restrict__ key, SegView in,
-                                                   const uint32_t *__restrict__ lab, uint64_t *__restrict__ best,
-                                                   uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
-                                                   uint64_t *__restrict__ okey, uint64_t *__restrict__ oseg_start,
-                                                   uint64_t *__restrict__ oseg_count) {
+GHS_STREAM_KERNEL void k_minedge(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
+                                 const uint64_t *__restrict__ key, SegView in, const uint32_t *__restrict__ lab,
+                                 uint64_t *__restrict__ best, uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
+                                 uint64_t *__restrict__ okey, uint64_t *__restrict__ oseg_start,
+                                 uint64_t *__restrict__ oseg_count) {
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
   __shared__ uint32_t s_seg[2];
+  __shared__ uint32_t s_hl[HOT_SLOTS];
+  __shared__ unsigned long long s_hk[HOT_SLOTS];
   const int lane = threadIdx.x & (WAVE - 1);
   const uint64_t T = in.total;
+  hot_init(s_hl, s_hk);
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;  // multiple of 4
   const uint64_t vb = Q * blockIdx.x;
   const uint64_t ve = (vb + Q < T) ? vb + Q : T;
@@ -157,82 +223,62 @@ __global__ __launch_bounds__(BLOCK) void k_minedge(const uint32_t *__restrict__ 
   __syncthreads();
   const uint32_t slo = s_seg[0], shi = s_seg[1];
   uint64_t out_n = 0;  // survivors written so far by this block
-  uint32_t carry_l = LABEL_NONE;  // wave-uniform deferred run (label, min key)
+  uint32_t carry_l = LABEL_NONE;  // wave-uniform deferred a-side run (label, min key)
   uint64_t carry_v = KEY_NONE;
+  EdgeTile cur, nxt;
+  tile_load(cur, src, dst, key, tile_phys(in, slo, shi, vb + (uint64_t)threadIdx.x * ARCS_PER_THREAD, ve));
 
   for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
     const uint64_t v = v0 + (uint64_t)threadIdx.x * ARCS_PER_THREAD;
-    uint32_t L[4], D[4];
-    uint64_t K[4];
+    const bool in_range = v < ve;
+    uint32_t L[4] = {cur.a.x, cur.a.y, cur.a.z, cur.a.w};
+    uint32_t D[4] = {cur.b.x, cur.b.y, cur.b.z, cur.b.w};
+    const uint64_t K[4] = {cur.k01.x, cur.k01.y, cur.k23.x, cur.k23.y};
     bool valid[4];
-    if (v < ve) {
-      const uint32_t s = (slo == shi) ? slo : seg_find(in.prefix, slo, shi, v);
-      const uint64_t seg_end = in.prefix[s + 1];
-      const uint64_t i0 = in.start[s] + (v - in.prefix[s]);
-      if (v + 4 <= seg_end && v + 4 <= ve && (i0 & 3) == 0) {
-        const uint4 s4 = *reinterpret_cast<const uint4 *>(src + i0);
-        L[0] = s4.x; L[1] = s4.y; L[2] = s4.z; L[3] = s4.w;
-        if (!IDENT) {
-          const uint4 d4 = *reinterpret_cast<const uint4 *>(dst + i0);
-          D[0] = d4.x; D[1] = d4.y; D[2] = d4.z; D[3] = d4.w;
-        }
-        const ulonglong2 k01 = *reinterpret_cast<const ulonglong2 *>(key + i0);
-        const ulonglong2 k23 = *reinterpret_cast<const ulonglong2 *>(key + i0 + 2);
-        K[0] = k01.x; K[1] = k01.y; K[2] = k23.x; K[3] = k23.y;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) valid[j] = L[j] != LABEL_NONE;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const bool in_range = v + j < ve && v + j < seg_end;
-          L[j] = in_range ? src[i0 + j] : LABEL_NONE;
-          D[j] = (!IDENT && in_range) ? dst[i0 + j] : 0u;
-          K[j] = in_range ? key[i0 + j] : KEY_NONE;
-          valid[j] = L[j] != LABEL_NONE;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        L[j] = LABEL_NONE; D[j] = 0; K[j] = KEY_NONE; valid[j] = false;
-      }
-    }
-    uint64_t V[4];
-    if (IDENT) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) V[j] = valid[j] ? K[j] : KEY_NONE;  // level arcs: src != dst
-    } else {
-      uint32_t cs[4], cd[4];
+    for (int j = 0; j < 4; ++j) valid[j] = in_range & (L[j] != LABEL_NONE);
+    uint32_t cs[4], cd[4];
+    if (!IDENT) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {  // 8 independent gathers in flight per lane
         cs[j] = lab[valid[j] ? L[j] : 0u];
         cd[j] = lab[valid[j] ? D[j] : 0u];
       }
+    }
+    tile_load(nxt, src, dst, key, tile_phys(in, slo, shi, v + ARCS_PER_BLOCK, ve));
+    uint64_t V[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < 4; ++j) {
+      if (!IDENT) {
         L[j] = valid[j] ? cs[j] : LABEL_NONE;
         D[j] = cd[j];
-        V[j] = (valid[j] && cs[j] != cd[j]) ? K[j] : KEY_NONE;
+        V[j] = (valid[j] & (cs[j] != cd[j])) ? K[j] : KEY_NONE;
+      } else {
+        if (!valid[j]) L[j] = LABEL_NONE;
+        V[j] = valid[j] ? K[j] : KEY_NONE;  // level edges: a != b
       }
     }
 
-    uint32_t smask = 0;  // survivors (inter-fragment arcs), taken before the carry merge
+    uint32_t smask = 0;  // survivors (inter-fragment edges), taken before the carry merge
 #pragma unroll
     for (int j = 0; j < 4; ++j) smask |= (V[j] != KEY_NONE) ? (1u << j) : 0u;
-    // Deferred run of the previous iteration (wave-uniform carry): a run that reaches the
-    // wave's end is not flushed but carried, and merged into the next run of the same label
-    // (min is associative, contiguity is not needed). A giant fragment's run of millions of
-    // arcs then costs one atomic per wave instead of one per 256 arcs (same-address atomics
-    // serialise at the memory side).
+    // b-side: one candidate per live edge
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (smask & (1u << j)) hot_min(s_hl, s_hk, best, D[j], V[j]);
+    // a-side. Deferred run of the previous iteration (wave-uniform carry): a run that reaches
+    // the wave's end is not flushed but carried, and merged into the next run of the same label
+    // (min is associative, contiguity is not needed).
+    uint64_t X[4] = {V[0], V[1], V[2], V[3]};
     if (lane == 0 && L[0] == carry_l && carry_l != LABEL_NONE) {
-      V[0] = umin64(V[0], carry_v);
+      X[0] = umin64(X[0], carry_v);
       carry_l = LABEL_NONE;  // merged
     }
     carry_l = __shfl(carry_l, 0);
-    if (carry_l != LABEL_NONE && lane == 0) flush_min(best, carry_l, carry_v);  // not merged
+    if (carry_l != LABEL_NONE && lane == 0) hot_min(s_hl, s_hk, best, carry_l, carry_v);  // not merged
     carry_l = LABEL_NONE;
 
-    // ---- wave-wide segmented min over 256 arcs, segments = runs of equal source label
+    // ---- wave-wide segmented min over 256 edges, segments = runs of equal a label
     const uint32_t prevL3 = __shfl_up(L[3], 1);
     bool H[4];
     H[0] = (lane == 0) || (L[0] != prevL3);
@@ -243,7 +289,7 @@ __global__ __launch_bounds__(BLOCK) void k_minedge(const uint32_t *__restrict__ 
     int f = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      x = H[j] ? V[j] : umin64(x, V[j]);
+      x = H[j] ? X[j] : umin64(x, X[j]);
       f |= H[j] ? 1 : 0;
     }
 #pragma unroll
@@ -260,10 +306,10 @@ __global__ __launch_bounds__(BLOCK) void k_minedge(const uint32_t *__restrict__ 
     const int nextH0 = __shfl_down(H[0] ? 1 : 0, 1);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      run = H[j] ? V[j] : umin64(run, V[j]);
+      run = H[j] ? X[j] : umin64(run, X[j]);
       const bool wave_end = (j == 3) && (lane == WAVE - 1);
       const bool tail = (j < 3) ? H[j + 1] : (lane == WAVE - 1 || nextH0);
-      if (tail && !wave_end && run != KEY_NONE) flush_min(best, L[j], run);
+      if (tail && !wave_end && run != KEY_NONE) hot_min(s_hl, s_hk, best, L[j], run);
       if (wave_end) {
         carry_l = (run != KEY_NONE) ? L[3] : LABEL_NONE;
         carry_v = run;
@@ -288,11 +334,14 @@ __global__ __launch_bounds__(BLOCK) void k_minedge(const uint32_t *__restrict__ 
       }
       out_n += total;
     }
+    cur = nxt;
   }
-  if (lane == 0 && carry_l != LABEL_NONE) flush_min(best, carry_l, carry_v);
+  if (lane == 0 && carry_l != LABEL_NONE) hot_min(s_hl, s_hk, best, carry_l, carry_v);
+  __syncthreads();
+  hot_flush(s_hl, s_hk, best);
   if (COMPACT) {
-    // pad to a multiple of 4 with dead arcs; stays inside [vb, vb + Q) and below the capacity
-    // (the workspace reserves 4 * SEG_G spare arcs)
+    // pad to a multiple of 4 with dead entries; stays inside [vb, vb + Q) and below the capacity
+    // (the workspace reserves 4 * SEG_G spare entries)
     const uint64_t padded = (out_n + 3) & ~3ull;
     if (threadIdx.x < padded - out_n) {
       const uint64_t pos = vb + out_n + threadIdx.x;
@@ -303,6 +352,35 @@ __global__ __launch_bounds__(BLOCK) void k_minedge(const uint32_t *__restrict__ 
     if (threadIdx.x == 0) {
       oseg_start[blockIdx.x] = vb;
       oseg_count[blockIdx.x] = (vb < T) ? padded : 0;
+    }
+  }
+}
+
+// flag every fragment that has a live edge in the level (both ends)
+GHS_STREAM_KERNEL void k_mark_edges(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst, SegView in,
+                                    uint8_t *__restrict__ flags) {
+  __shared__ uint32_t s_seg[2];
+  const uint64_t T = in.total;
+  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
+  const uint64_t vb = Q * blockIdx.x;
+  const uint64_t ve = (vb + Q < T) ? vb + Q : T;
+  if (threadIdx.x == 0) {
+    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
+    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
+  }
+  __syncthreads();
+  for (uint64_t v = vb + (uint64_t)threadIdx.x * 4; v < ve; v += ARCS_PER_BLOCK) {
+    const uint64_t i0 = tile_phys(in, s_seg[0], s_seg[1], v, ve);
+    const uint4 a = *reinterpret_cast<const uint4 *>(src + i0);
+    const uint4 b = *reinterpret_cast<const uint4 *>(dst + i0);
+    const uint32_t A[4] = {a.x, a.y, a.z, a.w}, B[4] = {b.x, b.y, b.z, b.w};
+    uint32_t prev = LABEL_NONE;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (A[j] == LABEL_NONE) continue;
+      if (A[j] != prev) flags[A[j]] = 1;  // a is grouped: skip repeated stores
+      prev = A[j];
+      flags[B[j]] = 1;
     }
   }
 }
@@ -492,149 +570,290 @@ __global__ void k_sample_weights(uint64_t cnt, const uint32_t *__restrict__ w, u
 }
 
 // ------------------------------------------------------------------------------------------
-// Level pass. Splits the edges still pending into (a) this level's edges whose ends lie in
-// different fragments -> (lab[u], lab[v], key) into this block's level staging region, and
-// (b) heavier edges that also survive the fragment test -> (u, v, key) into this block's
-// REMAINING region, the next level's input. Edges whose ends share a fragment are dropped for
-// good (cycle property). Both outputs are block-private regions (deterministic, no atomics).
-// FIRST: the input is the canonical list itself [e_lo, e_hi) (u, v, w; key built here),
-// every vertex is its own fragment, and the pass also validates canonicity (u < v < n,
-// strictly ascending) into err bit 8 — before any kernel indexes an array with these ids.
-// Otherwise the input is the previous level's remaining regions (segmented view) and lab is
-// fully resolved (one hop); the giant-fragment bitmap rejects most heavy edges without a
-// label gather.
+// Canonical passes: the two full streams over the caller's canonical list [e_lo, e_hi)
+// (u, v, w: 12 B per edge; key = w << 32 | eid built here).
+//  SELECT (opens level 0): validates canonicity (u < v < n, (u, v) strictly ascending) into err
+//    bit 8 — before any kernel indexes an array with these ids — and emits the edges with
+//    w < w_hi into this block's level staging region (every vertex is its own fragment, so the
+//    labels are the endpoints). Nothing else is written: the heavier edges stay where they are.
+//  FILTER (opens level 1): re-streams the list once level 0 is complete and drops, for good,
+//    every edge with w < w_lo (level 0: already decided) and every heavier edge whose ends both
+//    lie in the giant fragment (cycle property: the reference's REJECT for a whole weight class),
+//    tested on a 1-bit membership bitmap (n/8 bytes, resident in each XCD's L2) — no label
+//    gathers. The survivors (u, v, key) go to this block's PENDING region; the later level passes
+//    resolve them against the labels.
+// Block-private output regions: deterministic, no atomics.
 // ------------------------------------------------------------------------------------------
-template <bool FIRST>
-__global__ __launch_bounds__(BLOCK) void k_level_pass(uint32_t n, uint64_t e_lo, const uint32_t *__restrict__ eu,
-                                                      const uint32_t *__restrict__ ev, const uint32_t *__restrict__ ew,
-                                                      const uint32_t *__restrict__ ru, const uint32_t *__restrict__ rv,
-                                                      const uint64_t *__restrict__ rkey, SegView in, uint64_t w_hi,
-                                                      const uint32_t *__restrict__ lab,
-                                                      const uint64_t *__restrict__ giant_bits,
-                                                      uint32_t *__restrict__ lsrc, uint32_t *__restrict__ ldst,
-                                                      uint64_t *__restrict__ lkey, uint64_t *__restrict__ lcount,
-                                                      uint32_t *__restrict__ ou, uint32_t *__restrict__ ov,
-                                                      uint64_t *__restrict__ okey, uint64_t *__restrict__ ostart,
-                                                      uint64_t *__restrict__ ocount,
-                                                      unsigned long long *__restrict__ err) {
+// Buffer resource over [p, p + bytes) (bytes clipped to 2^31 - 1). Loads past the end return 0
+// instead of faulting, so the streaming loops issue every load unconditionally: no branch around
+// a load, hence no path-dependent outstanding-load count, and hipcc's waits stay counted
+// (vmcnt(N)) instead of draining the prefetched tile (cdna_hip_programming.md T8/T20). Built
+// from block-uniform values only.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint64_t bytes) {
+  const int nb = (int)(bytes > 0x7fffffffull ? 0x7fffffffull : bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, nb, 0x00020000);
+}
+
+__device__ __forceinline__ uint4 ld_b128(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 0);
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
+
+__device__ __forceinline__ uint32_t ld_b32(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, 0, 0);
+}
+
+// ------------------------------------------------------------------------------------------
+// Canonical passes: the two full streams over the caller's canonical list [e_lo, e_hi)
+// (u, v, w: 12 B per edge; key = w << 32 | eid built here). The stream runs over the aligned
+// range [E0, e_hi), E0 = e_lo & ~3 (edges below e_lo are masked), so every lane's 4-edge tile
+// is one 16-B load per array.
+//  SELECT (opens level 0): validates canonicity (u < v < n, (u, v) strictly ascending) into err
+//    bit 8 — before any kernel indexes an array with these ids — and emits the edges with
+//    w < w_hi into this block's level staging region (every vertex is its own fragment, so the
+//    labels are the endpoints). Nothing else is written: the heavier edges stay where they are.
+//  FILTER (opens level 1): re-streams the list once level 0 is complete and drops, for good,
+//    every edge with w < w_lo (level 0: already decided) and every heavier edge whose ends both
+//    lie in the giant fragment (cycle property: the reference's REJECT for a whole weight class),
+//    tested on a 1-bit membership bitmap (n/8 bytes, resident in each XCD's L2) — no label
+//    gathers. The survivors (u, v, key) go to this block's PENDING region; the later level passes
+//    resolve them against the labels.
+// Block-private output regions: deterministic, no atomics. Per iteration a lane issues its
+// bitmap probes for the tile in registers, then the next tile's loads, and only then waits for
+// the probes (loads complete in order), so one tile stays in flight across the compaction.
+// ------------------------------------------------------------------------------------------
+template <bool FILTER>
+GHS_STREAM_KERNEL void k_canon_pass(uint32_t n, uint64_t e_lo, uint64_t e_hi, const uint32_t *__restrict__ eu,
+                                    const uint32_t *__restrict__ ev, const uint32_t *__restrict__ ew, uint64_t w_lo,
+                                    uint64_t w_hi, const uint64_t *__restrict__ giant_bits,
+                                    uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
+                                    uint64_t *__restrict__ okey, uint64_t *__restrict__ ostart,
+                                    uint64_t *__restrict__ ocount, unsigned long long *__restrict__ err) {
+  __shared__ uint32_t s_wcnt[BLOCK / WAVE];
+  const uint64_t E0 = e_lo & ~3ull;
+  const uint64_t T = e_hi - E0;
+  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
+  const uint64_t vb = Q * blockIdx.x;
+  const uint64_t ve = (vb + Q < T) ? vb + Q : T;
+  const uint64_t eb = E0 + vb;  // first edge of this block
+  const uint64_t nbytes = ve > vb ? (ve - vb) * 4 : 0;
+  const __amdgpu_buffer_rsrc_t ru = make_rsrc(eu + eb, nbytes);
+  const __amdgpu_buffer_rsrc_t rv = make_rsrc(ev + eb, nbytes);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(ew + eb, nbytes);
+  // validation: the edge before each lane's tile; offset -4 (the block's first tile) is out of
+  // range of the descriptor and is replaced by the block's predecessor edge, loaded once
+  uint32_t bpa = 0, bpb = 0;
+  if (!FILTER && eb > 0 && ve > vb) {
+    bpa = eu[eb - 1];
+    bpb = ev[eb - 1];
+  }
+  const uint32_t lane_off = threadIdx.x * 16u;  // byte offset of the lane's tile in an iteration
+  uint64_t nout = 0;
+  bool bad = false;
+  uint4 ca = ld_b128(ru, lane_off), cb = ld_b128(rv, lane_off), cw = ld_b128(rw, lane_off);
+  uint32_t cpa = 0, cpb = 0;
+  if (!FILTER) {
+    cpa = ld_b32(ru, lane_off - 4);
+    cpb = ld_b32(rv, lane_off - 4);
+  }
+  for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
+    const uint64_t v = v0 + (uint64_t)threadIdx.x * 4;
+    const uint64_t e0 = E0 + v;
+    const uint32_t a[4] = {ca.x, ca.y, ca.z, ca.w}, b[4] = {cb.x, cb.y, cb.z, cb.w}, w[4] = {cw.x, cw.y, cw.z, cw.w};
+    // lane mask of the tile: edges in [e_lo, ve) (32-bit arithmetic, no branches)
+    const uint32_t nv = v < ve ? (uint32_t)((ve - v) < 4 ? (ve - v) : 4) : 0u;
+    const uint32_t nskip = e0 < e_lo ? (uint32_t)(e_lo - e0) : 0u;
+    bool live[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) live[j] = ((uint32_t)j < nv) & ((uint32_t)j >= nskip);
+    bool out[4];
+    uint32_t gbw[4];
+    uint4 q0, q3;
+    uint32_t A0 = 0, A3 = 0;
+    if (FILTER) {
+      // probes, all issued before any is used. a is sorted: two 16-B probes cover the
+      // 128-vertex blocks of a[0] and a[3]; an a[j] outside both (a tile spanning > 2 blocks) is
+      // treated as outside the giant, so its edge is kept — always safe, the later level passes
+      // test it again. b is random: one 32-bit word per edge. Lanes that need no probe read
+      // word 0 (one request per wave instruction).
+      const uint4 *bits4 = reinterpret_cast<const uint4 *>(giant_bits);
+      const uint32_t *bits32 = reinterpret_cast<const uint32_t *>(giant_bits);
+      A0 = a[0] >> 7;
+      A3 = a[3] >> 7;
+      q0 = bits4[live[0] ? A0 : 0u];
+      q3 = bits4[live[3] ? A3 : 0u];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        out[j] = live[j] & ((uint64_t)w[j] >= w_lo);
+        gbw[j] = bits32[out[j] ? (b[j] >> 5) : 0u];
+      }
+    }
+    // next tile (out-of-range offsets read 0)
+    const uint32_t noff = (uint32_t)(v0 + ARCS_PER_BLOCK - vb) * 4u + lane_off;
+    ca = ld_b128(ru, noff);
+    cb = ld_b128(rv, noff);
+    cw = ld_b128(rw, noff);
+    uint32_t npa = 0, npb = 0;
+    if (!FILTER) {
+      npa = ld_b32(ru, noff - 4);
+      npb = ld_b32(rv, noff - 4);
+    }
+    if (FILTER) {
+      uint32_t ga[4], gb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t blk = a[j] >> 7, wsel = (a[j] >> 5) & 3;
+        const uint4 q = (blk == A0) ? q0 : q3;
+        const bool odd = wsel & 1;  // two-level select (an == chain becomes a branch tree)
+        const uint32_t lo = odd ? q.y : q.x, hi = odd ? q.w : q.z;
+        const uint32_t word = (wsel & 2) ? hi : lo;
+        ga[j] = ((blk == A0) | (blk == A3)) ? (word >> (a[j] & 31)) & 1u : 0u;
+        gb[j] = (gbw[j] >> (b[j] & 31)) & 1u;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        out[j] = out[j] & ((ga[j] & gb[j]) == 0u);  // bitwise (no && : keeps the probes unsunk)
+    } else {
+      // u < v < n and (u, v) strictly above the previous edge; bitwise (no short-circuit
+      // branches: hipcc turns && / || chains into exec-mask control flow here)
+      uint32_t pa = (v == vb) ? bpa : cpa, pb = (v == vb) ? bpb : cpb;
+      const uint32_t first = (e0 == 0) ? 1u : 0u;  // edge 0 has no predecessor
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t ordered = (j == 0 ? first : 0u) | (uint32_t)(pa < a[j]) | ((uint32_t)(pa == a[j]) & (uint32_t)(pb < b[j]));
+        const uint32_t ok = (uint32_t)(a[j] < b[j]) & (uint32_t)(b[j] < n) & ordered;
+        bad |= live[j] & (ok == 0u);
+        live[j] = live[j] & (ok != 0u);  // never index with an unchecked id
+        pa = a[j];
+        pb = b[j];
+        out[j] = live[j] & ((uint64_t)w[j] < w_hi);
+      }
+      cpa = npa;
+      cpb = npb;
+    }
+    uint32_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mine += out[j] ? 1u : 0u;
+    uint32_t tot;
+    const uint32_t before = block_offsets(mine, s_wcnt, &tot);
+    uint64_t pos = vb + nout + before;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (out[j]) {
+        osrc[pos] = a[j];
+        odst[pos] = b[j];
+        okey[pos] = ((uint64_t)w[j] << 32) | (uint32_t)(e0 + j);
+        ++pos;
+      }
+    }
+    nout += tot;
+  }
+  if (!FILTER && bad) atomicOr(err, 8ull);
+  // output regions are padded to a multiple of 4 with dead entries (a = LABEL_NONE)
+  const uint64_t padded = (nout + 3) & ~3ull;
+  if (threadIdx.x < padded - nout) {
+    const uint64_t pos = vb + nout + threadIdx.x;
+    osrc[pos] = LABEL_NONE;
+    odst[pos] = 0;
+    okey[pos] = KEY_NONE;
+  }
+  if (threadIdx.x == 0) {
+    ostart[blockIdx.x] = vb;
+    ocount[blockIdx.x] = (vb < T) ? padded : 0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Level pass over the PENDING edges (levels >= 1). Splits them into (a) this level's edges whose
+// ends lie in different fragments -> (lab[u], lab[v], key) into this block's level staging
+// region, and (b) heavier edges that also survive the fragment test -> (u, v, key) into this
+// block's REMAINING region, the next level's input. Edges whose ends share a fragment are
+// dropped for good (cycle property). lab is fully resolved (one hop); the giant-fragment bitmap
+// rejects most heavy edges without a label gather. Block-private regions, no atomics.
+// ------------------------------------------------------------------------------------------
+GHS_STREAM_KERNEL void k_level_pass(const uint32_t *__restrict__ ru, const uint32_t *__restrict__ rv,
+                                    const uint64_t *__restrict__ rkey, SegView in, uint64_t w_hi,
+                                    const uint32_t *__restrict__ lab, const uint64_t *__restrict__ giant_bits,
+                                    uint32_t *__restrict__ lsrc, uint32_t *__restrict__ ldst,
+                                    uint64_t *__restrict__ lkey, uint64_t *__restrict__ lstart,
+                                    uint64_t *__restrict__ lcount, uint32_t *__restrict__ ou, uint32_t *__restrict__ ov, uint64_t *__restrict__ okey,
+                                    uint64_t *__restrict__ ostart, uint64_t *__restrict__ ocount) {
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
   __shared__ uint32_t s_seg[2];
   const uint64_t T = in.total;
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
   const uint64_t vb = Q * blockIdx.x;
   const uint64_t ve = (vb + Q < T) ? vb + Q : T;
-  if (!FIRST) {
-    if (threadIdx.x == 0) {
-      s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
-      s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
-    }
-    __syncthreads();
+  if (threadIdx.x == 0) {
+    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
+    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
   }
+  __syncthreads();
+  const uint32_t slo = s_seg[0], shi = s_seg[1];
+  // regions hold multiples of 4 entries and start at multiples of 4, so a lane's 4-entry tile
+  // is either wholly inside one region or past ve; past-ve tiles read a valid tile (index 0)
+  // and are masked, so every load is unconditional
+  auto tile_index = [&](uint64_t v) -> uint64_t {
+    if (v >= ve) return 0;
+    const uint32_t sidx = (slo == shi) ? slo : seg_find(in.prefix, slo, shi, v);
+    return in.start[sidx] + (v - in.prefix[sidx]);
+  };
+  const uint4 *bits4 = reinterpret_cast<const uint4 *>(giant_bits);
+  const uint32_t *bits32 = reinterpret_cast<const uint32_t *>(giant_bits);
   uint64_t nlev = 0, nrem = 0;
-  bool bad = false;
+  uint64_t i0 = tile_index(vb + (uint64_t)threadIdx.x * 4);
+  uint4 ca = *reinterpret_cast<const uint4 *>(ru + i0), cb = *reinterpret_cast<const uint4 *>(rv + i0);
+  ulonglong2 ck01 = *reinterpret_cast<const ulonglong2 *>(rkey + i0);
+  ulonglong2 ck23 = *reinterpret_cast<const ulonglong2 *>(rkey + i0 + 2);
   for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
     const uint64_t v = v0 + (uint64_t)threadIdx.x * 4;
-    uint32_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
-    uint64_t k[4] = {KEY_NONE, KEY_NONE, KEY_NONE, KEY_NONE};
-    bool live[4] = {false, false, false, false};
-    if (FIRST) {
-      const uint64_t e0 = e_lo + v;
-      uint32_t w[4] = {0, 0, 0, 0};
-      if (v + 4 <= ve && (e0 & 3) == 0) {
-        const uint4 a4 = *reinterpret_cast<const uint4 *>(eu + e0);
-        const uint4 b4 = *reinterpret_cast<const uint4 *>(ev + e0);
-        const uint4 w4 = *reinterpret_cast<const uint4 *>(ew + e0);
-        a[0] = a4.x; a[1] = a4.y; a[2] = a4.z; a[3] = a4.w;
-        b[0] = b4.x; b[1] = b4.y; b[2] = b4.z; b[3] = b4.w;
-        w[0] = w4.x; w[1] = w4.y; w[2] = w4.z; w[3] = w4.w;
+    const bool valid = v < ve;
+    const uint32_t a[4] = {ca.x, ca.y, ca.z, ca.w}, b[4] = {cb.x, cb.y, cb.z, cb.w};
+    const uint64_t k[4] = {ck01.x, ck01.y, ck23.x, ck23.y};
+    bool live[4], lev[4], rem[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) live[j] = true;
-      } else if (v < ve) {
+    for (int j = 0; j < 4; ++j) live[j] = valid & (a[j] != LABEL_NONE);
+    // giant-bitmap probes (a sorted within a region: two 16-B probes cover a[0]'s and a[3]'s
+    // 128-vertex blocks; an a[j] outside both counts as outside the giant — safe), issued
+    // before the next tile's loads
+    const uint32_t A0 = a[0] >> 7, A3 = a[3] >> 7;
+    const uint4 q0 = bits4[live[0] ? A0 : 0u];
+    const uint4 q3 = bits4[live[3] ? A3 : 0u];
+    uint32_t gbw[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (v + j < ve) {
-            a[j] = eu[e0 + j];
-            b[j] = ev[e0 + j];
-            w[j] = ew[e0 + j];
-            live[j] = true;
-          }
-        }
-      }
-      if (v < ve) {  // canonical order: u < v < n, (u, v) strictly ascending
-        uint32_t pa = 0, pb = 0;
-        const bool has_prev = e0 > 0;
-        if (has_prev) {
-          pa = eu[e0 - 1];
-          pb = ev[e0 - 1];
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (live[j]) {
-            bool ok = a[j] < b[j] && b[j] < n;
-            if (j > 0 || has_prev) ok = ok && (pa < a[j] || (pa == a[j] && pb < b[j]));
-            bad |= !ok;
-            pa = a[j];
-            pb = b[j];
-            k[j] = ((uint64_t)w[j] << 32) | (uint32_t)(e0 + j);
-            if (!ok) live[j] = false;  // never index with an unchecked id
-          }
-        }
-      }
-    } else if (v < ve) {
-      const uint32_t sidx = (s_seg[0] == s_seg[1]) ? s_seg[0] : seg_find(in.prefix, s_seg[0], s_seg[1], v);
-      const uint64_t seg_end = in.prefix[sidx + 1];
-      const uint64_t i0 = in.start[sidx] + (v - in.prefix[sidx]);
-      if (v + 4 <= seg_end && v + 4 <= ve && (i0 & 3) == 0) {
-        const uint4 a4 = *reinterpret_cast<const uint4 *>(ru + i0);
-        const uint4 b4 = *reinterpret_cast<const uint4 *>(rv + i0);
-        const ulonglong2 k01 = *reinterpret_cast<const ulonglong2 *>(rkey + i0);
-        const ulonglong2 k23 = *reinterpret_cast<const ulonglong2 *>(rkey + i0 + 2);
-        a[0] = a4.x; a[1] = a4.y; a[2] = a4.z; a[3] = a4.w;
-        b[0] = b4.x; b[1] = b4.y; b[2] = b4.z; b[3] = b4.w;
-        k[0] = k01.x; k[1] = k01.y; k[2] = k23.x; k[3] = k23.y;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const bool in_range = v + j < ve && v + j < seg_end;
-          a[j] = in_range ? ru[i0 + j] : LABEL_NONE;
-          b[j] = in_range ? rv[i0 + j] : 0u;
-          k[j] = in_range ? rkey[i0 + j] : KEY_NONE;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) live[j] = a[j] != LABEL_NONE;
-      // REJECT a whole class at once: both ends in the giant fragment (1-bit bitmap in L2;
-      // a is sorted within a region, so one word load usually serves a lane's 4 edges)
-      uint32_t wa_idx = 0xffffffffu;
-      uint64_t wa = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (live[j]) {
-          if ((a[j] >> 6) != wa_idx) {
-            wa_idx = a[j] >> 6;
-            wa = giant_bits[wa_idx];
-          }
-          const bool ga = (wa >> (a[j] & 63)) & 1;
-          if (ga && ((giant_bits[b[j] >> 6] >> (b[j] & 63)) & 1)) live[j] = false;
-        }
-      }
-    }
-    // fragment test + level/remaining split
-    uint32_t la[4], lb[4];
-    bool lev[4], rem[4];
+    for (int j = 0; j < 4; ++j) gbw[j] = bits32[live[j] ? (b[j] >> 5) : 0u];
+    // next tile
+    i0 = tile_index(v + ARCS_PER_BLOCK);
+    ca = *reinterpret_cast<const uint4 *>(ru + i0);
+    cb = *reinterpret_cast<const uint4 *>(rv + i0);
+    ck01 = *reinterpret_cast<const ulonglong2 *>(rkey + i0);
+    ck23 = *reinterpret_cast<const ulonglong2 *>(rkey + i0 + 2);
+    // REJECT a whole class at once: both ends in the giant fragment
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      la[j] = a[j];
-      lb[j] = b[j];
-      if (!FIRST && live[j]) {
-        la[j] = lab[a[j]];
-        lb[j] = lab[b[j]];
-        if (la[j] == lb[j]) live[j] = false;
-      }
-      const bool in_level = (k[j] >> 32) < w_hi;
-      lev[j] = live[j] && in_level;
-      rem[j] = live[j] && !in_level;
+      const uint32_t blk = a[j] >> 7, wsel = (a[j] >> 5) & 3;
+      const uint4 q = (blk == A0) ? q0 : q3;
+      const bool odd = wsel & 1;
+      const uint32_t lo = odd ? q.y : q.x, hi = odd ? q.w : q.z;
+      const uint32_t word = (wsel & 2) ? hi : lo;
+      const uint32_t ga = ((blk == A0) | (blk == A3)) ? (word >> (a[j] & 31)) & 1u : 0u;
+      const uint32_t gb = (gbw[j] >> (b[j] & 31)) & 1u;
+      live[j] = live[j] & ((ga & gb) == 0u);
     }
+    // level/remaining split; labels are gathered only for this level's edges (they become arcs
+    // and need the fragment test) — heavier edges are carried forward raw, the bitmap of the
+    // next level (a larger giant) rejects most of them without any gather
+    uint32_t la[4], lb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool in_level = (k[j] >> 32) < w_hi;
+      lev[j] = live[j] & in_level;
+      rem[j] = live[j] & !in_level;
+      la[j] = lab[lev[j] ? a[j] : 0u];
+      lb[j] = lab[lev[j] ? b[j] : 0u];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lev[j] = lev[j] & (la[j] != lb[j]);
     uint32_t mlev = 0, mrem = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -663,66 +882,31 @@ __global__ __launch_bounds__(BLOCK) void k_level_pass(uint32_t n, uint64_t e_lo,
     nlev += tlev;
     nrem += trem;
   }
-  if (FIRST && bad) atomicOr(err, 8ull);
-  // remaining regions padded to a multiple of 4 with dead entries (u = LABEL_NONE)
-  const uint64_t padded = (nrem + 3) & ~3ull;
+  // both outputs padded to a multiple of 4 with dead entries (a = LABEL_NONE)
+  const uint64_t padded = (nrem + 3) & ~3ull, lpadded = (nlev + 3) & ~3ull;
   if (threadIdx.x < padded - nrem) {
     const uint64_t pos = vb + nrem + threadIdx.x;
     ou[pos] = LABEL_NONE;
     ov[pos] = 0;
     okey[pos] = KEY_NONE;
   }
+  if (threadIdx.x < lpadded - nlev) {
+    const uint64_t pos = vb + nlev + threadIdx.x;
+    lsrc[pos] = LABEL_NONE;
+    ldst[pos] = 0;
+    lkey[pos] = KEY_NONE;
+  }
   if (threadIdx.x == 0) {
-    lcount[blockIdx.x] = (vb < T) ? nlev : 0;
+    lstart[blockIdx.x] = vb;
+    lcount[blockIdx.x] = (vb < T) ? lpadded : 0;
     ostart[blockIdx.x] = vb;
     ocount[blockIdx.x] = (vb < T) ? padded : 0;
-  }
-}
-
-// staging segments -> dense forward arcs [0, S) of the level arc buffer (order preserved)
-__global__ __launch_bounds__(BLOCK) void k_gather_segments(uint64_t T, const uint64_t *__restrict__ seg_prefix,
-                                                           const uint32_t *__restrict__ ssrc,
-                                                           const uint32_t *__restrict__ sdst,
-                                                           const uint64_t *__restrict__ skey, uint32_t *__restrict__ dsrc,
-                                                           uint32_t *__restrict__ ddst, uint64_t *__restrict__ dkey) {
-  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
-  const uint64_t vb = Q * blockIdx.x;
-  const uint64_t cnt = seg_prefix[blockIdx.x + 1] - seg_prefix[blockIdx.x];
-  const uint64_t dbase = seg_prefix[blockIdx.x];
-  for (uint64_t i = threadIdx.x; i < cnt; i += BLOCK) {
-    dsrc[dbase + i] = ssrc[vb + i];
-    ddst[dbase + i] = sdst[vb + i];
-    dkey[dbase + i] = skey[vb + i];
   }
 }
 
 __global__ void k_iota(uint32_t *__restrict__ a, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     a[i] = (uint32_t)i;
-}
-
-// reverse arcs [S, 2S): src = sorted dst labels (already written), dst/key gathered by index
-__global__ void k_fill_reverse(uint64_t S, const uint32_t *__restrict__ idx, uint32_t *__restrict__ asrc,
-                               uint32_t *__restrict__ adst, uint64_t *__restrict__ akey) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < S; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t j = idx[i];
-    adst[S + i] = asrc[j];
-    akey[S + i] = akey[j];
-  }
-}
-
-// flag every fragment that has an arc in the level: run heads of the (grouped) source labels
-__global__ void k_mark_sources(uint64_t A, const uint32_t *__restrict__ src, uint8_t *__restrict__ flags) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < A; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t c = src[i];
-    if (i == 0 || src[i - 1] != c) flags[c] = 1;
-  }
-}
-
-__global__ void k_set_seg1(uint64_t *start, uint64_t *prefix, uint64_t total) {
-  start[0] = 0;
-  prefix[0] = 0;
-  prefix[1] = total;
 }
 
 // dense all-reduce staging: int64 slot = key ^ 2^63 preserves unsigned order under signed MIN
@@ -742,6 +926,64 @@ __global__ void k_unpack_best(const uint32_t *__restrict__ act, uint64_t nact, u
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Order-preserving select of flagged items: out[k] = (in ? in[i] : i) for the k-th i with
+// flags[i] != 0. Two passes over the byte flags (16 per lane per load) around a scan of
+// per-block counts; every rank of a multi-GPU run produces the same list in the same order.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t SEL_PER_BLOCK = BLOCK * 16;
+
+__global__ __launch_bounds__(BLOCK) void k_sel_count(const uint8_t *__restrict__ flags, uint64_t count,
+                                                     uint64_t *__restrict__ bcount) {
+  __shared__ uint32_t s_w[BLOCK / WAVE];
+  const uint64_t i0 = (uint64_t)blockIdx.x * SEL_PER_BLOCK + threadIdx.x * 16ull;
+  uint32_t c = 0;
+  if (i0 + 16 <= count) {
+    const uint4 f = *reinterpret_cast<const uint4 *>(flags + i0);
+    const uint32_t x[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c += __popc((x[k] | (x[k] >> 1) | (x[k] >> 2) | (x[k] >> 3) | (x[k] >> 4) | (x[k] >> 5) | (x[k] >> 6) | (x[k] >> 7)) & 0x01010101u);
+  } else {
+    for (uint64_t i = i0; i < count && i < i0 + 16; ++i) c += flags[i] ? 1u : 0u;
+  }
+#pragma unroll
+  for (int d = WAVE / 2; d > 0; d >>= 1) c += __shfl_xor(c, d);
+  if ((threadIdx.x & (WAVE - 1)) == 0) s_w[threadIdx.x / WAVE] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / WAVE; ++w) t += s_w[w];
+    bcount[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_sel_write(const uint8_t *__restrict__ flags, const uint32_t *__restrict__ in,
+                                                     uint64_t count, const uint64_t *__restrict__ bprefix,
+                                                     uint32_t *__restrict__ out) {
+  __shared__ uint32_t s_wcnt[BLOCK / WAVE];
+  const uint64_t i0 = (uint64_t)blockIdx.x * SEL_PER_BLOCK + threadIdx.x * 16ull;
+  uint32_t bits = 0;  // bit k = flags[i0 + k]
+  if (i0 + 16 <= count) {
+    const uint4 f = *reinterpret_cast<const uint4 *>(flags + i0);
+    const uint32_t x[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) bits |= (((x[k >> 2] >> (8 * (k & 3))) & 0xffu) ? 1u : 0u) << k;
+  } else {
+    for (int k = 0; k < 16; ++k)
+      if (i0 + k < count && flags[i0 + k]) bits |= 1u << k;
+  }
+  uint32_t tot;
+  const uint32_t before = block_offsets((uint32_t)__popc(bits), s_wcnt, &tot);
+  uint64_t pos = bprefix[blockIdx.x] + before;
+  while (bits) {
+    const int k = __ffs(bits) - 1;
+    bits &= bits - 1;
+    const uint64_t i = i0 + k;
+    out[pos++] = in ? in[i] : (uint32_t)i;
+  }
+}
+
 static inline unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap) {
   uint64_t g = (items + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -751,11 +993,6 @@ static inline unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-static inline int bits_for(uint64_t maxval) {
-  int b = 0;
-  while (b < 64 && (maxval >> b)) ++b;
-  return b ? b : 1;
-}
 
 }  // namespace ghs
 
@@ -782,14 +1019,16 @@ struct ghs_solver {
   uint64_t *best = nullptr, *bits = nullptr;
   uint8_t *flags = nullptr;
   uint32_t *sample = nullptr;
+  uint64_t *sel_cnt = nullptr, *sel_pre = nullptr;  // select scratch (per-block counts / prefix)
   ArcBuf buf[2];
   ArcBuf rem[2];             // remaining (not yet levelled) edges: u, v, key as block regions
   int rcur = 0;              // rem buffer holding the pending edges (level >= 1)
   uint64_t rem_total = 0;    // pending edges (incl. padding) after the last level pass
+  bool debug = false;         // GHS_DEBUG=1: per-level sizes on stderr
+  bool pending_built = false; // the FILTER pass has run (levels >= 1 read the pending regions)
+  uint64_t stat_pending = 0; // pending edges (incl. padding) right after the FILTER pass
   uint32_t rem_nseg = 1;     // regions of the pending edges
   uint64_t cap_arcs = 0;
-  void *cub_temp = nullptr;
-  size_t cub_bytes = 0;
   unsigned long long *cnt = nullptr;    // device [0] scratch total, [1] active out, [2] weight, [3] edges, [4] err
   unsigned long long *h_cnt = nullptr;  // pinned host mirror
   uint32_t *h_sample = nullptr;         // pinned host sample buffer
@@ -805,8 +1044,8 @@ struct ghs_solver {
   uint32_t level_round = 0;  // completed rounds in this level
   int phase = 0;             // 0: expect minedge, 1: expect contract, 2: done
   int cur = 0;               // arc buffer holding the live arcs
-  bool cur_single = true;    // live arcs are one dense segment
-  uint64_t cur_arcs = 0;
+  uint32_t cur_nseg = 1;     // regions of the live edges
+  uint64_t cur_arcs = 0;     // live edges (virtual range incl. padding)
   int act_cur = 0;
   bool act_ident = true;     // fragments are 0..n-1
   uint64_t nact = 0;
@@ -823,20 +1062,6 @@ static constexpr uint32_t NSAMPLE = 8192;    // labels sampled to find the giant
 static constexpr uint32_t NSAMPLE_W = 16384; // weights sampled for the level plan
 static constexpr uint32_t NSAMPLE_MAX = NSAMPLE_W > NSAMPLE ? NSAMPLE_W : NSAMPLE;
 
-static size_t cub_temp_bytes(uint32_t n, uint64_t cap) {
-  size_t a = 0, b = 0, c = 0;
-  const size_t items = n ? n : 1;
-  (void)hipcub::DeviceSelect::Flagged(nullptr, a, (const uint32_t *)nullptr, (const uint8_t *)nullptr,
-                                      (uint32_t *)nullptr, (unsigned long long *)nullptr, items);
-  (void)hipcub::DeviceSelect::Flagged(nullptr, b, hipcub::CountingInputIterator<uint32_t>(0u),
-                                      (const uint8_t *)nullptr, (uint32_t *)nullptr, (unsigned long long *)nullptr,
-                                      items);
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, c, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                          (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                          (size_t)(cap ? cap : 1), 0, bits_for(n ? n - 1 : 0));
-  return std::max(a, std::max(b, c)) + 256;
-}
-
 static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, char *base) {
   size_t off = 0;
   auto carve = [&](size_t bytes) -> char * {
@@ -845,7 +1070,7 @@ static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, 
     return p;
   };
   const size_t N = (size_t)n;
-  const uint64_t cap = 2 * local_edges + 4 * SEG_G;  // a level's arcs: <= 2 per selected edge (+ padding)
+  const uint64_t cap = local_edges + 4 * SEG_G;  // a level's edges (+ padding of the regions)
   char *p;
   p = carve(N * 4); if (s) s->lab = (uint32_t *)p;
   p = carve(N * 4); if (s) s->par = (uint32_t *)p;
@@ -855,6 +1080,9 @@ static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, 
   p = carve(N ? N : 1); if (s) s->flags = (uint8_t *)p;
   p = carve(((N + 63) / 64) * 8 + 8); if (s) s->bits = (uint64_t *)p;
   p = carve(NSAMPLE_MAX * 4); if (s) s->sample = (uint32_t *)p;
+  const size_t nsel = (N + SEL_PER_BLOCK - 1) / SEL_PER_BLOCK + 1;
+  p = carve(nsel * 8); if (s) s->sel_cnt = (uint64_t *)p;
+  p = carve((nsel + 1) * 8); if (s) s->sel_pre = (uint64_t *)p;
   for (int b = 0; b < 2; ++b) {
     p = carve(cap * 4); if (s) s->buf[b].src = (uint32_t *)p;
     p = carve(cap * 4); if (s) s->buf[b].dst = (uint32_t *)p;
@@ -872,8 +1100,7 @@ static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, 
     p = carve(SEG_G * 8); if (s) s->rem[b].seg_count = (uint64_t *)p;
     p = carve((SEG_G + 1) * 8); if (s) s->rem[b].seg_prefix = (uint64_t *)p;
   }
-  const size_t cb = cub_temp_bytes(n, cap);
-  p = carve(cb); if (s) { s->cub_temp = p; s->cub_bytes = cb; s->cap_arcs = cap; }
+  if (s) s->cap_arcs = cap;
   p = carve(8 * sizeof(unsigned long long)); if (s) s->cnt = (unsigned long long *)p;
   return off;
 }
@@ -892,6 +1119,21 @@ static hipEvent_t round_event(ghs_solver *s, uint32_t round, int k) {
 static void record(ghs_solver *s, int k) {
   hipEvent_t ev = round_event(s, s->round, k);
   if (ev) (void)hipEventRecord(ev, s->stream);
+}
+
+// order-preserving select of the flagged items of [0, count) (or of in[0, count)); *d_total = k
+static int select_flagged(ghs_solver *s, const uint8_t *flags, const uint32_t *in, uint64_t count, uint32_t *out,
+                          unsigned long long *d_total) {
+  if (count == 0) {
+    GHS_HIP_CHECK(hipMemsetAsync(d_total, 0, 8, s->stream));
+    return GHS_OK;
+  }
+  const unsigned nb = (unsigned)((count + SEL_PER_BLOCK - 1) / SEL_PER_BLOCK);
+  k_sel_count<<<nb, BLOCK, 0, s->stream>>>(flags, count, s->sel_cnt);
+  k_scan_counts<<<1, 1024, 0, s->stream>>>(s->sel_cnt, nb, s->sel_pre, d_total);
+  k_sel_write<<<nb, BLOCK, 0, s->stream>>>(flags, in, count, s->sel_pre, out);
+  GHS_HIP_CHECK(hipGetLastError());
+  return GHS_OK;
 }
 
 static void default_config(ghs_config_t *c) {
@@ -936,8 +1178,8 @@ static int open_level(ghs_solver *s) {
   const uint64_t w_hi = s->thresholds[lv + 1];
   const bool first = (lv == 0);
   hipStream_t st = s->stream;
-  ArcBuf &X = s->buf[0], &Y = s->buf[1];
-  const int rin = s->rcur, rout = first ? 0 : (s->rcur ^ 1);
+  ArcBuf &Y = s->buf[1];
+  const int rin = s->rcur, rout = s->rcur ^ 1;
   ArcBuf &RI = s->rem[rin], &RO = s->rem[rout];
 
   if (!first) {
@@ -961,32 +1203,64 @@ static int open_level(ghs_solver *s) {
       }
       i = j;
     }
+    if (s->debug) fprintf(stderr, "[ghs] level %u: giant %u holds %zu/%zu sampled vertices\n", lv, giant, best_run, smp.size());
     k_bitmap<<<grid_for(s->n, BLOCK, 16384), BLOCK, 0, st>>>(s->n, s->lab, giant, s->bits);
     GHS_HIP_CHECK(hipGetLastError());
   }
 
-  // 1. split: this level's surviving edges -> Y staging; heavier survivors -> RO regions
-  const uint64_t T = first ? (s->e_hi - s->e_lo) : s->rem_total;
-  const unsigned G = grid_for(T, ARCS_PER_BLOCK, SEG_G);
-  SegView in{RI.seg_start, RI.seg_prefix, s->rem_nseg, T};
+  // 1. this level's edges -> regions of Y (level edges: a, b labels + key, canonical order)
+  unsigned G = 1;
+  uint64_t T = 0;
+  if (first) {
+    // SELECT over the canonical list: level-0 edges only (validates the list)
+    T = s->e_hi > s->e_lo ? s->e_hi - (s->e_lo & ~3ull) : 0;  // the canonical passes stream [e_lo & ~3, e_hi)
+    G = grid_for(T, ARCS_PER_BLOCK, SEG_G);
+    if (s->e_hi > s->e_lo) {
+      k_canon_pass<false><<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, 0, w_hi, nullptr, Y.src, Y.dst,
+                                               Y.key, Y.seg_start, Y.seg_count, s->cnt + 4);
+      GHS_HIP_CHECK(hipGetLastError());
+    }
+  } else {
+    if (!s->pending_built) {
+      // FILTER over the canonical list once level 0 is complete: every heavier edge not inside
+      // the giant fragment becomes pending (regions of rem[rin])
+      const uint64_t TC = s->e_hi > s->e_lo ? s->e_hi - (s->e_lo & ~3ull) : 0;
+      const unsigned GC = grid_for(TC, ARCS_PER_BLOCK, SEG_G);
+      if (s->e_hi > s->e_lo) {
+        k_canon_pass<true><<<GC, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, s->thresholds[lv], 0,
+                                                 s->bits, RI.src, RI.dst, RI.key, RI.seg_start, RI.seg_count,
+                                                 s->cnt + 4);
+        GHS_HIP_CHECK(hipGetLastError());
+        k_scan_counts<<<1, 1024, 0, st>>>(RI.seg_count, GC, RI.seg_prefix, s->cnt + 5);
+        GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt + 5, s->cnt + 5, 8, hipMemcpyDeviceToHost, st));
+        GHS_HIP_CHECK(hipStreamSynchronize(st));
+        s->rem_total = s->h_cnt[5];
+      } else {
+        s->rem_total = 0;
+      }
+      s->rem_nseg = GC;
+      s->pending_built = true;
+      s->stat_pending = s->rem_total;
+    }
+    // split the pending edges: this level's inter-fragment edges -> Y staging; heavier
+    // survivors -> RO regions
+    T = s->rem_total;
+    G = grid_for(T, ARCS_PER_BLOCK, SEG_G);
+    if (T) {
+      SegView in{RI.seg_start, RI.seg_prefix, s->rem_nseg, T};
+      k_level_pass<<<G, BLOCK, 0, st>>>(RI.src, RI.dst, RI.key, in, w_hi, s->lab, s->bits, Y.src, Y.dst, Y.key,
+                                        Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key, RO.seg_start, RO.seg_count);
+      GHS_HIP_CHECK(hipGetLastError());
+      k_scan_counts<<<1, 1024, 0, st>>>(RO.seg_count, G, RO.seg_prefix, s->cnt + 5);
+    } else {
+      GHS_HIP_CHECK(hipMemsetAsync(s->cnt + 5, 0, 8, st));
+    }
+  }
   if (T) {
-    if (first)
-      k_level_pass<true><<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->eu, s->ev, s->ew, nullptr, nullptr, nullptr, in, w_hi,
-                                              s->lab, s->bits, Y.src, Y.dst, Y.key, Y.seg_count, RO.src, RO.dst,
-                                              RO.key, RO.seg_start, RO.seg_count, s->cnt + 4);
-    else
-      k_level_pass<false><<<G, BLOCK, 0, st>>>(s->n, 0, nullptr, nullptr, nullptr, RI.src, RI.dst, RI.key, in, w_hi,
-                                               s->lab, s->bits, Y.src, Y.dst, Y.key, Y.seg_count, RO.src, RO.dst,
-                                               RO.key, RO.seg_start, RO.seg_count, s->cnt + 4);
-    GHS_HIP_CHECK(hipGetLastError());
     k_scan_counts<<<1, 1024, 0, st>>>(Y.seg_count, G, Y.seg_prefix, s->cnt + 0);
-    k_scan_counts<<<1, 1024, 0, st>>>(RO.seg_count, G, RO.seg_prefix, s->cnt + 5);
-    // 2. dense forward arcs X[0, S) (order kept: grouped by the source's vertex)
-    k_gather_segments<<<G, BLOCK, 0, st>>>(T, Y.seg_prefix, Y.src, Y.dst, Y.key, X.src, X.dst, X.key);
     GHS_HIP_CHECK(hipGetLastError());
   } else {
     GHS_HIP_CHECK(hipMemsetAsync(s->cnt, 0, 8, st));
-    GHS_HIP_CHECK(hipMemsetAsync(s->cnt + 5, 0, 8, st));
   }
   GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   GHS_HIP_CHECK(hipStreamSynchronize(st));
@@ -999,40 +1273,33 @@ static int open_level(ghs_solver *s) {
     GHS_FAIL(GHS_E_STATE, "internal invariant violated (code " + std::to_string(s->h_cnt[4]) + ")");
   }
   const uint64_t S = s->h_cnt[0];
-  s->rem_total = s->h_cnt[5];
-  s->rem_nseg = G;
-  s->rcur = rout;
-  s->level_arcs = 2 * S;
+  if (s->debug)
+    fprintf(stderr, "[ghs] level %u open: w_hi=%llu input=%llu level_edges=%llu pending_after=%llu (filter pass kept %llu)\n",
+            lv, (unsigned long long)w_hi, (unsigned long long)T, (unsigned long long)S,
+            (unsigned long long)(first ? 0 : s->h_cnt[5]), (unsigned long long)s->stat_pending);
+  if (!first) {
+    s->rem_total = s->h_cnt[5];
+    s->rem_nseg = G;
+    s->rcur = rout;
+  }
+  s->level_arcs = S;
   if (S == 0 && s->cfg.num_ranks <= 1) {  // nothing to merge at this level (single rank only:
     s->level_open = false;                // ranks must run the same rounds)
     return GHS_OK;
   }
-  // 3. reverse arcs X[S, 2S): radix sort (dst label, index) -> grouped by dst label
-  if (S) {
-    uint32_t *idx_in = Y.src, *idx_out = Y.dst;  // Y's staging is consumed
-    k_iota<<<grid_for(S, 256, 16384), 256, 0, st>>>(idx_in, S);
-    size_t cb = s->cub_bytes;
-    GHS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(s->cub_temp, cb, X.dst, X.src + S, idx_in, idx_out, (size_t)S, 0,
-                                                     bits_for(s->n - 1), st));
-    k_fill_reverse<<<grid_for(S, 256, 16384), 256, 0, st>>>(S, idx_out, X.src, X.dst, X.key);
-    GHS_HIP_CHECK(hipGetLastError());
-  }
-  s->cur = 0;
-  s->cur_single = true;
-  s->cur_arcs = 2 * S;
-  k_set_seg1<<<1, 1, 0, st>>>(X.seg_start, X.seg_prefix, s->cur_arcs);
-  GHS_HIP_CHECK(hipGetLastError());
+  s->cur = 1;  // the level's edges are Y's G regions (S entries incl. padding)
+  s->cur_nseg = G;
+  s->cur_arcs = S;
+  SegView lev{Y.seg_start, Y.seg_prefix, G, S};
 
-  // 4. active fragments. Single rank: the fragments that have an arc in this level.
+  // 2. active fragments. Single rank: the fragments that have an edge in this level.
   //    Several ranks: every current root (first level: every vertex) — identical on every
   //    rank without an exchange; roots without arcs anywhere drop out after one round.
-  size_t cb = s->cub_bytes;
   if (s->cfg.num_ranks <= 1) {
     GHS_HIP_CHECK(hipMemsetAsync(s->flags, 0, s->n, st));
-    k_mark_sources<<<grid_for(2 * S, 256, 16384), 256, 0, st>>>(2 * S, X.src, s->flags);
+    if (S) k_mark_edges<<<grid_for(S, ARCS_PER_BLOCK, SEG_G), BLOCK, 0, st>>>(Y.src, Y.dst, lev, s->flags);
     GHS_HIP_CHECK(hipGetLastError());
-    GHS_HIP_CHECK(hipcub::DeviceSelect::Flagged(s->cub_temp, cb, hipcub::CountingInputIterator<uint32_t>(0u), s->flags,
-                                                s->act[0], s->cnt + 1, (size_t)s->n, st));
+    if (int rc = select_flagged(s, s->flags, nullptr, s->n, s->act[0], s->cnt + 1)) return rc;
     GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt + 1, s->cnt + 1, 8, hipMemcpyDeviceToHost, st));
     GHS_HIP_CHECK(hipStreamSynchronize(st));
     s->act_ident = false;
@@ -1042,8 +1309,7 @@ static int open_level(ghs_solver *s) {
     s->act_ident = true;
     s->nact = s->n;
   } else {
-    GHS_HIP_CHECK(hipcub::DeviceSelect::Flagged(s->cub_temp, cb, hipcub::CountingInputIterator<uint32_t>(0u), s->flags,
-                                                s->act[0], s->cnt + 1, (size_t)s->n, st));
+    if (int rc = select_flagged(s, s->flags, nullptr, s->n, s->act[0], s->cnt + 1)) return rc;
     GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt + 1, s->cnt + 1, 8, hipMemcpyDeviceToHost, st));
     GHS_HIP_CHECK(hipStreamSynchronize(st));
     s->act_ident = false;
@@ -1098,6 +1364,8 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   s->n = n; s->m = m; s->e_lo = e_lo; s->e_hi = e_hi;
   s->eu = d_u; s->ev = d_v; s->ew = d_w;
   s->in_mst = d_in_mst; s->stream = (hipStream_t)stream;
+  { const char *dbg = getenv("GHS_DEBUG"); s->debug = dbg && dbg[0] == '1'; }
+
   if (cfg) s->cfg = *cfg; else default_config(&s->cfg);
   workspace_layout(n, e_hi - e_lo, s, (char *)d_workspace);
   auto fail = [&](hipError_t e, const char *what) {
@@ -1156,7 +1424,7 @@ int ghs_solver_minedge(ghs_solver_t *s, uint64_t *num_active) {
   const ArcBuf &I = s->buf[s->cur];
   ArcBuf &O = s->buf[s->cur ^ 1];
   if (A) {
-    SegView in{I.seg_start, I.seg_prefix, s->cur_single ? 1u : SEG_G, A};
+    SegView in{I.seg_start, I.seg_prefix, s->cur_nseg, A};
     const unsigned G = grid_for(A, ARCS_PER_BLOCK, SEG_G);
     if (s->level_round == 0) {
       k_minedge<true, false><<<G, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, nullptr, nullptr,
@@ -1207,9 +1475,9 @@ int ghs_solver_contract(ghs_solver_t *s, int *done) {
   if (s->phase != 1) GHS_FAIL(GHS_E_STATE, "contract must follow minedge");
   const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
   const uint64_t nact = s->nact;
-  const unsigned g = grid_for(nact, BLOCK, 16384);
+  const unsigned g = grid_for(nact, BLOCK, 65535);
   if (nact) {
-    k_hook<<<grid_for(nact, BLOCK, 2048), BLOCK, 0, s->stream>>>(act, nact, s->best, s->lab, s->eu, s->ev, s->par,
+    k_hook<<<grid_for(nact, BLOCK, 65535), BLOCK, 0, s->stream>>>(act, nact, s->best, s->lab, s->eu, s->ev, s->par,
                                                                  s->in_mst, s->cnt + 2, s->cnt + 4);
     GHS_HIP_CHECK(hipGetLastError());
   }
@@ -1223,14 +1491,7 @@ int ghs_solver_contract(ghs_solver_t *s, int *done) {
   if (nact) {
     k_flag_next<<<g, BLOCK, 0, s->stream>>>(act, nact, s->par, s->best, s->flags);
     GHS_HIP_CHECK(hipGetLastError());
-    size_t cb = s->cub_bytes;
-    if (act) {
-      GHS_HIP_CHECK(hipcub::DeviceSelect::Flagged(s->cub_temp, cb, act, s->flags, s->act[nb], s->cnt + 1, (size_t)nact,
-                                                  s->stream));
-    } else {
-      GHS_HIP_CHECK(hipcub::DeviceSelect::Flagged(s->cub_temp, cb, hipcub::CountingInputIterator<uint32_t>(0u),
-                                                  s->flags, s->act[nb], s->cnt + 1, (size_t)nact, s->stream));
-    }
+    if (int rc = select_flagged(s, s->flags, act, nact, s->act[nb], s->cnt + 1)) return rc;
   } else {
     GHS_HIP_CHECK(hipMemsetAsync(s->cnt + 1, 0, 8, s->stream));
   }
@@ -1254,7 +1515,7 @@ int ghs_solver_contract(ghs_solver_t *s, int *done) {
   // the arcs compacted by this round's min-edge kernel are the next round's input
   if (s->level_round >= 1 && s->cur_arcs) {
     s->cur ^= 1;
-    s->cur_single = false;
+    s->cur_nseg = SEG_G;
     s->cur_arcs = s->h_cnt[0];
   }
   s->act_cur = nb;
@@ -1265,7 +1526,7 @@ int ghs_solver_contract(ghs_solver_t *s, int *done) {
   if (s->nact == 0) {  // level complete
     s->level_open = false;
     s->level += 1;
-    const bool no_more = (s->level + 1 >= s->thresholds.size()) || (s->cfg.num_ranks <= 1 && s->rem_total == 0);
+    const bool no_more = (s->level + 1 >= s->thresholds.size()) || (s->cfg.num_ranks <= 1 && s->pending_built && s->rem_total == 0);
     s->phase = no_more ? 2 : 0;
   } else {
     s->phase = 0;
