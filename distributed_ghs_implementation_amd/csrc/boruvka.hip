@@ -86,7 +86,7 @@ __device__ __forceinline__ void flush_min(uint64_t *__restrict__ best, uint32_t 
 // block instead of one per run — same-address global operations serialise at the memory side
 // (~12 ns each, MI355X_MICROARCH.md "fanin") and atomics drop the line from L2, so every later
 // plain read of that slot misses too.
-constexpr int HOT_BITS = 9;
+constexpr int HOT_BITS = 8;
 constexpr int HOT_SLOTS = 1 << HOT_BITS;
 
 __device__ __forceinline__ void hot_init(uint32_t *s_hl, unsigned long long *s_hk) {
@@ -141,15 +141,81 @@ __device__ __forceinline__ uint32_t block_offsets(uint32_t mine, uint32_t *s_wcn
   return before;
 }
 
+// Wave-level offsets for a block-wide compaction step: *lane_excl = items of lower lanes of the
+// wave, *wave_before = items of lower waves of the block, *wave_cnt = the wave's items,
+// *total = the block's. Every thread of the block must call it (two barriers).
+__device__ __forceinline__ void block_offsets_w(uint32_t mine, uint32_t *s_wcnt, uint32_t *lane_excl,
+                                                uint32_t *wave_before, uint32_t *wave_cnt, uint32_t *total) {
+  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+  uint32_t incl = mine;
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const uint32_t o = __shfl_up(incl, d);
+    if (lane >= d) incl += o;
+  }
+  *lane_excl = incl - mine;
+  *wave_cnt = __shfl(incl, WAVE - 1);
+  if (lane == WAVE - 1) s_wcnt[wid] = incl;
+  __syncthreads();
+  uint32_t before = 0, t = 0;
+#pragma unroll
+  for (int w = 0; w < BLOCK / WAVE; ++w) {
+    if (w < wid) before += s_wcnt[w];
+    t += s_wcnt[w];
+  }
+  *wave_before = before;
+  *total = t;
+  __syncthreads();
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Staged compaction of a wave's survivors: each lane puts its (<= 4) flagged items at
+// lane_excl.. in the wave's private LDS region (256 entries), then the wave writes its
+// contiguous output range [out, out + wave_cnt) with coalesced stores (lane i: items i, i + 64,
+// ...) instead of 12 scattered per-lane stores.
+struct WaveStage {
+  uint32_t a[WAVE * 4];
+  uint32_t b[WAVE * 4];
+  uint64_t k[WAVE * 4];
+};
+
+__device__ __forceinline__ void stage_write(WaveStage &ws, const uint32_t a[4], const uint32_t b[4], const uint64_t k[4],
+                                            uint32_t mask, uint32_t lane_excl, uint32_t wave_cnt,
+                                            uint32_t *__restrict__ oa, uint32_t *__restrict__ ob,
+                                            uint64_t *__restrict__ ok, uint64_t out) {
+  uint32_t p = lane_excl;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (mask & (1u << j)) {
+      ws.a[p] = a[j];
+      ws.b[p] = b[j];
+      ws.k[p] = k[j];
+      ++p;
+    }
+  }
+  wave_sync_lds();
+  const int lane = threadIdx.x & (WAVE - 1);
+  for (uint32_t i = lane; i < wave_cnt; i += WAVE) {
+    oa[out + i] = ws.a[i];
+    ob[out + i] = ws.b[i];
+    ok[out + i] = ws.k[i];
+  }
+  wave_sync_lds();  // the region is rewritten next iteration
+}
+
 // ------------------------------------------------------------------------------------------
 // Segmented input: virtual index v in [0, total) lives in segment s with
 // prefix[s] <= v < prefix[s+1], physical index start[s] + (v - prefix[s]).
 // ------------------------------------------------------------------------------------------
 struct SegView {
   const uint64_t *start;
-  const uint64_t *prefix;  // nseg + 1 entries
+  const uint64_t *prefix;  // nseg + 1 entries; prefix[nseg] = the virtual total (device-side)
   uint32_t nseg;
-  uint64_t total;
 };
 
 __device__ __forceinline__ uint32_t seg_find(const uint64_t *__restrict__ prefix, uint32_t lo, uint32_t hi, uint64_t v) {
@@ -210,8 +276,9 @@ GHS_STREAM_KERNEL void k_minedge(const uint32_t *__restrict__ src, const uint32_
   __shared__ uint32_t s_seg[2];
   __shared__ uint32_t s_hl[HOT_SLOTS];
   __shared__ unsigned long long s_hk[HOT_SLOTS];
+  __shared__ WaveStage s_stage[COMPACT ? BLOCK / WAVE : 1];
   const int lane = threadIdx.x & (WAVE - 1);
-  const uint64_t T = in.total;
+  const uint64_t T = in.prefix[in.nseg];
   hot_init(s_hl, s_hk);
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;  // multiple of 4
   const uint64_t vb = Q * blockIdx.x;
@@ -319,19 +386,10 @@ GHS_STREAM_KERNEL void k_minedge(const uint32_t *__restrict__ src, const uint32_
     carry_v = __shfl(carry_v, WAVE - 1);
 
     if (COMPACT) {
-      const uint32_t mine = (uint32_t)__popc(smask);
-      uint32_t total;
-      const uint32_t before = block_offsets(mine, s_wcnt, &total);
-      uint64_t pos = vb + out_n + before;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (smask & (1u << j)) {
-          osrc[pos] = L[j];
-          odst[pos] = D[j];
-          okey[pos] = K[j];
-          ++pos;
-        }
-      }
+      uint32_t lane_excl, wave_before, wave_cnt, total;
+      block_offsets_w((uint32_t)__popc(smask), s_wcnt, &lane_excl, &wave_before, &wave_cnt, &total);
+      stage_write(s_stage[threadIdx.x / WAVE], L, D, K, smask, lane_excl, wave_cnt, osrc, odst, okey,
+                  vb + out_n + wave_before);
       out_n += total;
     }
     cur = nxt;
@@ -356,34 +414,6 @@ GHS_STREAM_KERNEL void k_minedge(const uint32_t *__restrict__ src, const uint32_
   }
 }
 
-// flag every fragment that has a live edge in the level (both ends)
-GHS_STREAM_KERNEL void k_mark_edges(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst, SegView in,
-                                    uint8_t *__restrict__ flags) {
-  __shared__ uint32_t s_seg[2];
-  const uint64_t T = in.total;
-  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
-  const uint64_t vb = Q * blockIdx.x;
-  const uint64_t ve = (vb + Q < T) ? vb + Q : T;
-  if (threadIdx.x == 0) {
-    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
-    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
-  }
-  __syncthreads();
-  for (uint64_t v = vb + (uint64_t)threadIdx.x * 4; v < ve; v += ARCS_PER_BLOCK) {
-    const uint64_t i0 = tile_phys(in, s_seg[0], s_seg[1], v, ve);
-    const uint4 a = *reinterpret_cast<const uint4 *>(src + i0);
-    const uint4 b = *reinterpret_cast<const uint4 *>(dst + i0);
-    const uint32_t A[4] = {a.x, a.y, a.z, a.w}, B[4] = {b.x, b.y, b.z, b.w};
-    uint32_t prev = LABEL_NONE;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (A[j] == LABEL_NONE) continue;
-      if (A[j] != prev) flags[A[j]] = 1;  // a is grouped: skip repeated stores
-      prev = A[j];
-      flags[B[j]] = 1;
-    }
-  }
-}
 
 // exclusive scan of count[0..n) into prefix[0..n]; one block of 1024 threads
 __global__ __launch_bounds__(1024) void k_scan_counts(const uint64_t *__restrict__ count, uint32_t n,
@@ -434,7 +464,7 @@ __device__ __forceinline__ uint32_t find_lab(const uint32_t *__restrict__ lab, u
 // ghs_implementation.py:186-196, initiator by (fragment_id, rank), ghs_implementation_mpi.py:
 // 237-239). Every hook adds exactly one MSF edge; one pair of atomics per block for the totals.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act, uint64_t nact,
+__global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
                                                 const uint64_t *__restrict__ best, const uint32_t *__restrict__ lab,
                                                 const uint32_t *__restrict__ eu, const uint32_t *__restrict__ ev,
                                                 uint32_t *__restrict__ par, uint8_t *__restrict__ in_mst,
@@ -442,6 +472,7 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
                                                 unsigned long long *__restrict__ err) {
   __shared__ unsigned long long s_w[BLOCK / WAVE], s_c[BLOCK / WAVE];
   unsigned long long wsum = 0, cnt = 0;
+  const uint64_t nact = *d_nact;
   for (uint64_t i = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; i < nact; i += (uint64_t)gridDim.x * BLOCK) {
     const uint32_t c = act ? act[i] : (uint32_t)i;
     const uint64_t k = best[c];
@@ -488,12 +519,93 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
 }
 
 // ------------------------------------------------------------------------------------------
+// Stage 2, edge form (single rank, many small fragments): every live edge (a, b, key) whose key
+// is the best of a fragment is that fragment's CONNECT edge — no gathers of the canonical
+// endpoints and no label walks (the edge already carries the current roots). A fragment c hooks
+// to the other end o unless the pair is mutual and c < o (the smaller label stays root, as in
+// k_hook). par[c] == c holds for every active root, so only hooking fragments are written.
+// ------------------------------------------------------------------------------------------
+GHS_STREAM_KERNEL void k_win(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
+                             const uint64_t *__restrict__ key, SegView in, const uint64_t *__restrict__ best,
+                             uint32_t *__restrict__ par, uint8_t *__restrict__ in_mst,
+                             unsigned long long *__restrict__ acc /* [0] weight, [1] edges */) {
+  __shared__ uint32_t s_seg[2];
+  __shared__ unsigned long long s_w[BLOCK / WAVE], s_c[BLOCK / WAVE];
+  const uint64_t T = in.prefix[in.nseg];
+  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
+  const uint64_t vb = Q * blockIdx.x;
+  const uint64_t ve = (vb + Q < T) ? vb + Q : T;
+  if (threadIdx.x == 0) {
+    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
+    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
+  }
+  __syncthreads();
+  const uint32_t slo = s_seg[0], shi = s_seg[1];
+  unsigned long long wsum = 0, cnt = 0;
+  EdgeTile cur, nxt;
+  tile_load(cur, src, dst, key, tile_phys(in, slo, shi, vb + (uint64_t)threadIdx.x * 4, ve));
+  for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
+    const uint64_t v = v0 + (uint64_t)threadIdx.x * 4;
+    const bool in_range = v < ve;
+    const uint32_t A[4] = {cur.a.x, cur.a.y, cur.a.z, cur.a.w}, B[4] = {cur.b.x, cur.b.y, cur.b.z, cur.b.w};
+    const uint64_t K[4] = {cur.k01.x, cur.k01.y, cur.k23.x, cur.k23.y};
+    bool live[4];
+    uint64_t ba[4], bb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      live[j] = in_range & (A[j] != LABEL_NONE);
+      ba[j] = best[live[j] ? A[j] : 0u];
+      bb[j] = best[live[j] ? B[j] : 0u];
+    }
+    tile_load(nxt, src, dst, key, tile_phys(in, slo, shi, v + ARCS_PER_BLOCK, ve));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool wa = live[j] & (ba[j] == K[j]), wb = live[j] & (bb[j] == K[j]);
+      const bool ha = wa & !(wb & (A[j] < B[j]));  // a hooks to b
+      const bool hb = wb & !(wa & (B[j] < A[j]));  // b hooks to a
+      if (ha) par[A[j]] = B[j];
+      if (hb) par[B[j]] = A[j];
+      if (ha | hb) {
+        in_mst[(uint32_t)K[j]] = 1;
+        wsum += K[j] >> 32;
+        cnt += 1;
+      }
+    }
+    cur = nxt;
+  }
+#pragma unroll
+  for (int d = WAVE / 2; d > 0; d >>= 1) {
+    wsum += __shfl_xor(wsum, d);
+    cnt += __shfl_xor(cnt, d);
+  }
+  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+  if (lane == 0) {
+    s_w[wid] = wsum;
+    s_c[wid] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long tw = 0, tc = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / WAVE; ++w) {
+      tw += s_w[w];
+      tc += s_c[w];
+    }
+    if (tc) {
+      atomicAdd(acc + 0, tw);
+      atomicAdd(acc + 1, tc);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Stage 3: pointer jumping (INITIATE broadcast of the new fragment id). Path splitting on par:
 // concurrent compression only moves a pointer to an ancestor, so stale reads are still valid
 // ancestors and every walk ends at its root. lab[c] = root.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act, uint64_t nact, uint32_t *par,
-                                                uint32_t *__restrict__ lab, unsigned long long *__restrict__ err) {
+__global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
+                                                uint32_t *par, uint32_t *__restrict__ lab, unsigned long long *__restrict__ err) {
+  const uint64_t nact = *d_nact;
   for (uint64_t i = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; i < nact; i += (uint64_t)gridDim.x * BLOCK) {
     const uint32_t c = act ? act[i] : (uint32_t)i;
     uint32_t x = c;
@@ -520,9 +632,11 @@ __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act
 // The list is produced by an order-preserving select, so every rank of a multi-GPU run holds
 // the same list in the same order and the all-reduce slots line up.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BLOCK) void k_flag_next(const uint32_t *__restrict__ act, uint64_t nact,
+__global__ __launch_bounds__(BLOCK) void k_flag_next(const uint32_t *__restrict__ act,
+                                                     const unsigned long long *__restrict__ d_nact,
                                                      const uint32_t *__restrict__ par, uint64_t *__restrict__ best,
                                                      uint8_t *__restrict__ flags) {
+  const uint64_t nact = *d_nact;
   for (uint64_t i = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; i < nact; i += (uint64_t)gridDim.x * BLOCK) {
     const uint32_t c = act ? act[i] : (uint32_t)i;
     const bool keep = (par[c] == c) && (best[c] != KEY_NONE);
@@ -543,10 +657,88 @@ __global__ __launch_bounds__(BLOCK) void k_resolve(uint32_t n, uint32_t *lab, ui
   }
 }
 
+// The giant fragment = the most frequent label among NSAMPLE evenly spaced vertices (ties: the
+// smaller label). One workgroup: bitonic sort of the sample in LDS, then an argmax over the run
+// lengths. No host round trip.
+constexpr uint32_t NSAMPLE = 2048;  // the giant holds >= ~10% of the vertices: 2048 samples find it
+__global__ __launch_bounds__(1024) void k_giant(uint32_t n, const uint32_t *__restrict__ lab, uint32_t *__restrict__ giant) {
+  __shared__ uint32_t x[NSAMPLE];
+  __shared__ unsigned long long s_best[1024 / WAVE];
+  const uint32_t ns = n < NSAMPLE ? n : NSAMPLE;
+  for (uint32_t i = threadIdx.x; i < NSAMPLE; i += 1024) {
+    const uint64_t v = ((uint64_t)i * n) / ns;
+    x[i] = i < ns ? lab[v] : 0xffffffffu;  // padding sorts last and is never counted
+  }
+  __syncthreads();
+  for (uint32_t k = 2; k <= NSAMPLE; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < NSAMPLE; i += 1024) {
+        const uint32_t p = i ^ j;
+        if (p > i) {
+          const uint32_t a = x[i], b = x[p];
+          const bool up = (i & k) == 0;
+          if ((a > b) == up) {
+            x[i] = b;
+            x[p] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // run starts by an inclusive max-scan of head positions (8 per thread, then across threads);
+  // at the last element of a run, length = i - start + 1. Pack (length, ~label) for a max.
+  constexpr uint32_t PER = NSAMPLE / 1024;
+  uint32_t rs[PER];
+  uint32_t run_start = 0;
+  const uint32_t b0 = threadIdx.x * PER;
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q) {
+    const uint32_t i = b0 + q;
+    if (i == 0 || x[i] != x[i - 1]) run_start = i;
+    rs[q] = run_start;
+  }
+  __shared__ uint32_t s_scan[1024];
+  s_scan[threadIdx.x] = rs[PER - 1];
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    const uint32_t o = threadIdx.x >= d ? s_scan[threadIdx.x - d] : 0u;
+    __syncthreads();
+    s_scan[threadIdx.x] = s_scan[threadIdx.x] > o ? s_scan[threadIdx.x] : o;
+    __syncthreads();
+  }
+  const uint32_t carry = threadIdx.x ? s_scan[threadIdx.x - 1] : 0u;  // run start entering this chunk
+  unsigned long long best = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q) {
+    const uint32_t i = b0 + q;
+    const uint32_t start = rs[q] > carry ? rs[q] : carry;
+    const bool last = (i + 1 >= ns) || (x[i + 1] != x[i]);
+    if (i < ns && last) {
+      const unsigned long long c = ((unsigned long long)(i - start + 1) << 32) | (0xffffffffu - x[i]);
+      best = c > best ? c : best;
+    }
+  }
+#pragma unroll
+  for (int d = WAVE / 2; d > 0; d >>= 1) {
+    const unsigned long long o = __shfl_xor(best, d);
+    best = o > best ? o : best;
+  }
+  if ((threadIdx.x & (WAVE - 1)) == 0) s_best[threadIdx.x / WAVE] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long b = 0;
+    for (int w = 0; w < 1024 / WAVE; ++w) b = s_best[w] > b ? s_best[w] : b;
+    giant[0] = 0xffffffffu - (uint32_t)b;
+    giant[1] = (uint32_t)(b >> 32);  // sampled vertices in the giant (stats / debug)
+  }
+}
+
 // giant-fragment membership bitmap: bit v = (lab[v] == giant); one u64 word per wave
-__global__ __launch_bounds__(BLOCK) void k_bitmap(uint32_t n, const uint32_t *__restrict__ lab, uint32_t giant,
-                                                  uint64_t *__restrict__ bits) {
+__global__ __launch_bounds__(BLOCK) void k_bitmap(uint32_t n, const uint32_t *__restrict__ lab,
+                                                  const uint32_t *__restrict__ giant_ptr, uint64_t *__restrict__ bits) {
   const uint64_t words = ((uint64_t)n + 63) / 64;
+  const uint32_t giant = giant_ptr[0];
   for (uint64_t base = blockIdx.x * (uint64_t)BLOCK; base < (uint64_t)n; base += (uint64_t)gridDim.x * BLOCK) {
     const uint64_t v = base + threadIdx.x;
     const bool in = v < n && lab[v] == giant;
@@ -555,12 +747,6 @@ __global__ __launch_bounds__(BLOCK) void k_bitmap(uint32_t n, const uint32_t *__
   }
 }
 
-__global__ void k_sample_labels(uint32_t n, const uint32_t *__restrict__ lab, uint32_t nsamp, uint32_t *__restrict__ out) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsamp; i += gridDim.x * blockDim.x) {
-    const uint64_t v = ((uint64_t)i * n) / nsamp;
-    out[i] = lab[v < n ? v : n - 1];
-  }
-}
 
 __global__ void k_sample_weights(uint64_t cnt, const uint32_t *__restrict__ w, uint32_t nsamp, uint32_t *__restrict__ out) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsamp; i += gridDim.x * blockDim.x) {
@@ -628,8 +814,10 @@ GHS_STREAM_KERNEL void k_canon_pass(uint32_t n, uint64_t e_lo, uint64_t e_hi, co
                                     uint64_t w_hi, const uint64_t *__restrict__ giant_bits,
                                     uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
                                     uint64_t *__restrict__ okey, uint64_t *__restrict__ ostart,
-                                    uint64_t *__restrict__ ocount, unsigned long long *__restrict__ err) {
+                                    uint64_t *__restrict__ ocount, uint8_t *__restrict__ mark,
+                                    unsigned long long *__restrict__ err) {
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
+  __shared__ WaveStage s_stage[BLOCK / WAVE];
   const uint64_t E0 = e_lo & ~3ull;
   const uint64_t T = e_hi - E0;
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
@@ -731,21 +919,20 @@ GHS_STREAM_KERNEL void k_canon_pass(uint32_t n, uint64_t e_lo, uint64_t e_hi, co
       cpa = npa;
       cpb = npb;
     }
-    uint32_t mine = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) mine += out[j] ? 1u : 0u;
-    uint32_t tot;
-    const uint32_t before = block_offsets(mine, s_wcnt, &tot);
-    uint64_t pos = vb + nout + before;
+    uint32_t omask = 0;
+    uint64_t key[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if (out[j]) {
-        osrc[pos] = a[j];
-        odst[pos] = b[j];
-        okey[pos] = ((uint64_t)w[j] << 32) | (uint32_t)(e0 + j);
-        ++pos;
+      omask |= out[j] ? (1u << j) : 0u;
+      key[j] = ((uint64_t)w[j] << 32) | (uint32_t)(e0 + j);
+      if (!FILTER && mark && out[j]) {  // active fragments of the level (single rank)
+        mark[a[j]] = 1;
+        mark[b[j]] = 1;
       }
     }
+    uint32_t le, wb, wc, tot;
+    block_offsets_w((uint32_t)__popc(omask), s_wcnt, &le, &wb, &wc, &tot);
+    stage_write(s_stage[threadIdx.x / WAVE], a, b, key, omask, le, wc, osrc, odst, okey, vb + nout + wb);
     nout += tot;
   }
   if (!FILTER && bad) atomicOr(err, 8ull);
@@ -777,10 +964,12 @@ GHS_STREAM_KERNEL void k_level_pass(const uint32_t *__restrict__ ru, const uint3
                                     uint32_t *__restrict__ lsrc, uint32_t *__restrict__ ldst,
                                     uint64_t *__restrict__ lkey, uint64_t *__restrict__ lstart,
                                     uint64_t *__restrict__ lcount, uint32_t *__restrict__ ou, uint32_t *__restrict__ ov, uint64_t *__restrict__ okey,
-                                    uint64_t *__restrict__ ostart, uint64_t *__restrict__ ocount) {
+                                    uint64_t *__restrict__ ostart, uint64_t *__restrict__ ocount,
+                                    uint8_t *__restrict__ mark) {
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
   __shared__ uint32_t s_seg[2];
-  const uint64_t T = in.total;
+  __shared__ WaveStage s_stage[BLOCK / WAVE];
+  const uint64_t T = in.prefix[in.nseg];
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
   const uint64_t vb = Q * blockIdx.x;
   const uint64_t ve = (vb + Q < T) ? vb + Q : T;
@@ -860,25 +1049,21 @@ GHS_STREAM_KERNEL void k_level_pass(const uint32_t *__restrict__ ru, const uint3
       mlev += lev[j] ? 1u : 0u;
       mrem += rem[j] ? 1u : 0u;
     }
-    uint32_t tlev, trem;
-    const uint32_t blev = block_offsets(mlev, s_wcnt, &tlev);
-    const uint32_t brem = block_offsets(mrem, s_wcnt, &trem);
-    uint64_t pl = vb + nlev + blev, pr = vb + nrem + brem;
+    uint32_t lmask = 0, rmask = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if (lev[j]) {
-        lsrc[pl] = la[j];
-        ldst[pl] = lb[j];
-        lkey[pl] = k[j];
-        ++pl;
-      }
-      if (rem[j]) {
-        ou[pr] = a[j];
-        ov[pr] = b[j];
-        okey[pr] = k[j];
-        ++pr;
+      lmask |= lev[j] ? (1u << j) : 0u;
+      rmask |= rem[j] ? (1u << j) : 0u;
+      if (lev[j] && mark) {  // active fragments of the level (single rank)
+        mark[la[j]] = 1;
+        mark[lb[j]] = 1;
       }
     }
+    uint32_t le, wb, wc, tlev, trem;
+    block_offsets_w(mlev, s_wcnt, &le, &wb, &wc, &tlev);
+    stage_write(s_stage[threadIdx.x / WAVE], la, lb, k, lmask, le, wc, lsrc, ldst, lkey, vb + nlev + wb);
+    block_offsets_w(mrem, s_wcnt, &le, &wb, &wc, &trem);
+    stage_write(s_stage[threadIdx.x / WAVE], a, b, k, rmask, le, wc, ou, ov, okey, vb + nrem + wb);
     nlev += tlev;
     nrem += trem;
   }
@@ -910,16 +1095,18 @@ __global__ void k_iota(uint32_t *__restrict__ a, uint64_t n) {
 }
 
 // dense all-reduce staging: int64 slot = key ^ 2^63 preserves unsigned order under signed MIN
-__global__ void k_pack_best(const uint32_t *__restrict__ act, uint64_t nact, const uint64_t *__restrict__ best,
-                            int64_t *__restrict__ dense) {
+__global__ void k_pack_best(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
+                            const uint64_t *__restrict__ best, int64_t *__restrict__ dense) {
+  const uint64_t nact = *d_nact;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nact; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t c = act ? act[i] : (uint32_t)i;
     dense[i] = (int64_t)(best[c] ^ 0x8000000000000000ull);
   }
 }
 
-__global__ void k_unpack_best(const uint32_t *__restrict__ act, uint64_t nact, uint64_t *__restrict__ best,
-                              const int64_t *__restrict__ dense) {
+__global__ void k_unpack_best(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
+                              uint64_t *__restrict__ best, const int64_t *__restrict__ dense) {
+  const uint64_t nact = *d_nact;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nact; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t c = act ? act[i] : (uint32_t)i;
     best[c] = (uint64_t)dense[i] ^ 0x8000000000000000ull;
@@ -933,9 +1120,11 @@ __global__ void k_unpack_best(const uint32_t *__restrict__ act, uint64_t nact, u
 // ------------------------------------------------------------------------------------------
 constexpr uint32_t SEL_PER_BLOCK = BLOCK * 16;
 
-__global__ __launch_bounds__(BLOCK) void k_sel_count(const uint8_t *__restrict__ flags, uint64_t count,
+__global__ __launch_bounds__(BLOCK) void k_sel_count(const uint8_t *__restrict__ flags,
+                                                     const unsigned long long *__restrict__ d_count,
                                                      uint64_t *__restrict__ bcount) {
   __shared__ uint32_t s_w[BLOCK / WAVE];
+  const uint64_t count = *d_count;
   const uint64_t i0 = (uint64_t)blockIdx.x * SEL_PER_BLOCK + threadIdx.x * 16ull;
   uint32_t c = 0;
   if (i0 + 16 <= count) {
@@ -959,9 +1148,10 @@ __global__ __launch_bounds__(BLOCK) void k_sel_count(const uint8_t *__restrict__
 }
 
 __global__ __launch_bounds__(BLOCK) void k_sel_write(const uint8_t *__restrict__ flags, const uint32_t *__restrict__ in,
-                                                     uint64_t count, const uint64_t *__restrict__ bprefix,
-                                                     uint32_t *__restrict__ out) {
+                                                     const unsigned long long *__restrict__ d_count,
+                                                     const uint64_t *__restrict__ bprefix, uint32_t *__restrict__ out) {
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
+  const uint64_t count = *d_count;
   const uint64_t i0 = (uint64_t)blockIdx.x * SEL_PER_BLOCK + threadIdx.x * 16ull;
   uint32_t bits = 0;  // bit k = flags[i0 + k]
   if (i0 + 16 <= count) {
@@ -982,6 +1172,15 @@ __global__ __launch_bounds__(BLOCK) void k_sel_write(const uint8_t *__restrict__
     const uint64_t i = i0 + k;
     out[pos++] = in ? in[i] : (uint32_t)i;
   }
+}
+
+// a round's results into the pinned host slot (one launch instead of three copies)
+__global__ void k_round_report(const unsigned long long *__restrict__ cnt, const unsigned long long *__restrict__ nact_out,
+                               unsigned long long *__restrict__ slot) {
+  slot[0] = cnt[0];      // live edges after this round's compaction
+  slot[1] = nact_out[0]; // active fragments of the next round
+  slot[2] = cnt[3];      // MSF edges so far
+  slot[3] = cnt[4];      // error bits
 }
 
 static inline unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap) {
@@ -1007,6 +1206,26 @@ struct ArcBuf {
   uint64_t *seg_start = nullptr, *seg_count = nullptr, *seg_prefix = nullptr;
 };
 
+// Device counters (cnt[], one 256-B line): every round's sizes stay on the device; kernels read
+// them there, so the host launches a round without knowing them (grid sizes are upper bounds).
+enum : int {
+  C_LIVE = 0,     // live edges (virtual total incl. padding) written by the last compaction scan
+  C_WEIGHT = 2,   // MSF weight so far
+  C_EDGES = 3,    // MSF edges so far (== hooks)
+  C_ERR = 4,      // invariant / canonicity error bits
+  C_PENDING = 5,  // pending edges (virtual total) after the last level pass
+  C_N = 6,        // n (the count of the identity active list)
+  C_ACT = 8,      // [8], [9]: lengths of the active lists act[0], act[1]
+  C_COUNT = 16
+};
+
+struct RoundSlot {  // pinned copy of a round's results (pipelined loop)
+  unsigned long long live_out, nact_out, edges, err;
+};
+constexpr int SLOT_RING = 8;
+constexpr int LOOKAHEAD = 2;            // rounds enqueued ahead of the host's termination check
+constexpr uint32_t LEVEL_ROUND_CAP = 64;  // hang guard: a level takes O(log n) rounds
+
 struct ghs_solver {
   uint32_t n = 0;
   uint64_t m = 0, e_lo = 0, e_hi = 0;
@@ -1019,36 +1238,40 @@ struct ghs_solver {
   uint64_t *best = nullptr, *bits = nullptr;
   uint8_t *flags = nullptr;
   uint32_t *sample = nullptr;
+  uint32_t *giant = nullptr;  // device [0] giant label, [1] its sampled vertex count
   uint64_t *sel_cnt = nullptr, *sel_pre = nullptr;  // select scratch (per-block counts / prefix)
-  ArcBuf buf[2];
-  ArcBuf rem[2];             // remaining (not yet levelled) edges: u, v, key as block regions
+  ArcBuf buf[2];             // a level's edges (regions) and the round double buffer
+  ArcBuf rem[2];             // pending (not yet levelled) edges: u, v, key as regions
   int rcur = 0;              // rem buffer holding the pending edges (level >= 1)
-  uint64_t rem_total = 0;    // pending edges (incl. padding) after the last level pass
-  bool debug = false;         // GHS_DEBUG=1: per-level sizes on stderr
-  bool pending_built = false; // the FILTER pass has run (levels >= 1 read the pending regions)
-  uint64_t stat_pending = 0; // pending edges (incl. padding) right after the FILTER pass
   uint32_t rem_nseg = 1;     // regions of the pending edges
+  uint64_t rem_total = 0;    // pending edges (incl. padding) after the last level pass (host copy)
+  bool pending_built = false; // the FILTER pass has run (levels >= 1 read the pending regions)
+  bool debug = false;        // GHS_DEBUG=1: per-level sizes on stderr
   uint64_t cap_arcs = 0;
-  unsigned long long *cnt = nullptr;    // device [0] scratch total, [1] active out, [2] weight, [3] edges, [4] err
+  unsigned long long *cnt = nullptr;    // device counters (C_*)
   unsigned long long *h_cnt = nullptr;  // pinned host mirror
+  RoundSlot *h_slot = nullptr;          // pinned ring of round results (host view)
+  RoundSlot *d_slot = nullptr;          // the same ring, device view
+  hipEvent_t slot_ev[SLOT_RING] = {};
   uint32_t *h_sample = nullptr;         // pinned host sample buffer
 
   // level plan (identical on every rank: computed from the global canonical list)
   std::vector<uint64_t> thresholds;  // level i: [thr[i], thr[i+1])
   uint32_t level = 0;                // index of the level being processed
   bool level_open = false;
-  uint64_t level_arcs = 0;           // arcs built for the current level (stats)
+  uint64_t level_arcs = 0;           // edges of the current level (incl. padding; stats)
 
-  // round state
+  // round state (host view)
   uint32_t round = 0;        // completed rounds (all levels)
-  uint32_t level_round = 0;  // completed rounds in this level
-  int phase = 0;             // 0: expect minedge, 1: expect contract, 2: done
-  int cur = 0;               // arc buffer holding the live arcs
-  uint32_t cur_nseg = 1;     // regions of the live edges
-  uint64_t cur_arcs = 0;     // live edges (virtual range incl. padding)
+  uint32_t level_round = 0;  // rounds issued in this level
+  int phase = 0;             // stepwise API: 0 expect minedge, 1 expect contract, 2 done
+  int cur = 0;               // edge buffer holding the live edges
+  uint32_t cur_nseg = 1;     // its regions
+  uint64_t cur_arcs = 0;     // live edges at level start (exact)
   int act_cur = 0;
-  bool act_ident = true;     // fragments are 0..n-1
-  uint64_t nact = 0;
+  bool act_ident = true;     // active fragments are 0..n-1 (count C_N)
+  uint64_t nact = 0;         // active fragments: exact in the stepwise API, an upper bound when pipelined
+  uint64_t level_nact = 0;   // active fragments at level start (exact)
   uint64_t edges_before = 0;
 
   std::vector<ghs_round_stats_t> stats;
@@ -1058,9 +1281,8 @@ struct ghs_solver {
 
 static std::mutex g_mutex;  // the one-shot entry points are serialised per process
 
-static constexpr uint32_t NSAMPLE = 8192;    // labels sampled to find the giant fragment
 static constexpr uint32_t NSAMPLE_W = 16384; // weights sampled for the level plan
-static constexpr uint32_t NSAMPLE_MAX = NSAMPLE_W > NSAMPLE ? NSAMPLE_W : NSAMPLE;
+static constexpr uint32_t NSAMPLE_MAX = NSAMPLE_W;
 
 static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, char *base) {
   size_t off = 0;
@@ -1078,8 +1300,9 @@ static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, 
   p = carve(N * 4); if (s) s->act[0] = (uint32_t *)p;
   p = carve(N * 4); if (s) s->act[1] = (uint32_t *)p;
   p = carve(N ? N : 1); if (s) s->flags = (uint8_t *)p;
-  p = carve(((N + 63) / 64) * 8 + 8); if (s) s->bits = (uint64_t *)p;
+  p = carve(((N + 127) / 128) * 16 + 16); if (s) s->bits = (uint64_t *)p;
   p = carve(NSAMPLE_MAX * 4); if (s) s->sample = (uint32_t *)p;
+  p = carve(16); if (s) s->giant = (uint32_t *)p;
   const size_t nsel = (N + SEL_PER_BLOCK - 1) / SEL_PER_BLOCK + 1;
   p = carve(nsel * 8); if (s) s->sel_cnt = (uint64_t *)p;
   p = carve((nsel + 1) * 8); if (s) s->sel_pre = (uint64_t *)p;
@@ -1091,17 +1314,16 @@ static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, 
     p = carve(SEG_G * 8); if (s) s->buf[b].seg_count = (uint64_t *)p;
     p = carve((SEG_G + 1) * 8); if (s) s->buf[b].seg_prefix = (uint64_t *)p;
   }
-  const uint64_t rcap = local_edges + 4 * SEG_G;
   for (int b = 0; b < 2; ++b) {
-    p = carve(rcap * 4); if (s) s->rem[b].src = (uint32_t *)p;
-    p = carve(rcap * 4); if (s) s->rem[b].dst = (uint32_t *)p;
-    p = carve(rcap * 8); if (s) s->rem[b].key = (uint64_t *)p;
+    p = carve(cap * 4); if (s) s->rem[b].src = (uint32_t *)p;
+    p = carve(cap * 4); if (s) s->rem[b].dst = (uint32_t *)p;
+    p = carve(cap * 8); if (s) s->rem[b].key = (uint64_t *)p;
     p = carve(SEG_G * 8); if (s) s->rem[b].seg_start = (uint64_t *)p;
     p = carve(SEG_G * 8); if (s) s->rem[b].seg_count = (uint64_t *)p;
     p = carve((SEG_G + 1) * 8); if (s) s->rem[b].seg_prefix = (uint64_t *)p;
   }
   if (s) s->cap_arcs = cap;
-  p = carve(8 * sizeof(unsigned long long)); if (s) s->cnt = (unsigned long long *)p;
+  p = carve(C_COUNT * sizeof(unsigned long long)); if (s) s->cnt = (unsigned long long *)p;
   return off;
 }
 
@@ -1121,17 +1343,18 @@ static void record(ghs_solver *s, int k) {
   if (ev) (void)hipEventRecord(ev, s->stream);
 }
 
-// order-preserving select of the flagged items of [0, count) (or of in[0, count)); *d_total = k
-static int select_flagged(ghs_solver *s, const uint8_t *flags, const uint32_t *in, uint64_t count, uint32_t *out,
-                          unsigned long long *d_total) {
-  if (count == 0) {
+// Order-preserving select of the flagged items of [0, count) (or of in[0, count)), count on the
+// device (d_count), bound >= count on the host; *d_total = k.
+static int select_flagged(ghs_solver *s, const uint8_t *flags, const uint32_t *in, const unsigned long long *d_count,
+                          uint64_t bound, uint32_t *out, unsigned long long *d_total) {
+  if (bound == 0) {
     GHS_HIP_CHECK(hipMemsetAsync(d_total, 0, 8, s->stream));
     return GHS_OK;
   }
-  const unsigned nb = (unsigned)((count + SEL_PER_BLOCK - 1) / SEL_PER_BLOCK);
-  k_sel_count<<<nb, BLOCK, 0, s->stream>>>(flags, count, s->sel_cnt);
+  const unsigned nb = (unsigned)((bound + SEL_PER_BLOCK - 1) / SEL_PER_BLOCK);
+  k_sel_count<<<nb, BLOCK, 0, s->stream>>>(flags, d_count, s->sel_cnt);
   k_scan_counts<<<1, 1024, 0, s->stream>>>(s->sel_cnt, nb, s->sel_pre, d_total);
-  k_sel_write<<<nb, BLOCK, 0, s->stream>>>(flags, in, count, s->sel_pre, out);
+  k_sel_write<<<nb, BLOCK, 0, s->stream>>>(flags, in, d_count, s->sel_pre, out);
   GHS_HIP_CHECK(hipGetLastError());
   return GHS_OK;
 }
@@ -1171,153 +1394,251 @@ static int plan_levels(ghs_solver *s) {
   return GHS_OK;
 }
 
-// ---- open the next level: split pending edges, build the level's arcs, set the active list ---
-// Returns GHS_OK with s->level_open set, or with the level skipped (single rank, no arcs).
+static int fail_counters(ghs_solver *s, unsigned long long err, const char *where) {
+  s->phase = 2;
+  if (err & 8) GHS_FAIL(GHS_E_NONCANON, "edge list is not canonical (need u < v < n, strictly ascending (u, v))");
+  GHS_FAIL(GHS_E_STATE, std::string("internal invariant violated ") + where + " (code " + std::to_string(err) + ")");
+}
+
+// ---- open the next level: select its edges, set its active list (one host sync) --------------
+// Returns GHS_OK with s->level_open set, or with the level skipped (single rank, no edges).
 static int open_level(ghs_solver *s) {
   const uint32_t lv = s->level;
   const uint64_t w_hi = s->thresholds[lv + 1];
   const bool first = (lv == 0);
+  const bool single = s->cfg.num_ranks <= 1;
   hipStream_t st = s->stream;
   ArcBuf &Y = s->buf[1];
-  const int rin = s->rcur, rout = s->rcur ^ 1;
-  ArcBuf &RI = s->rem[rin], &RO = s->rem[rout];
 
   if (!first) {
-    // compress labels, find the giant fragment from a sample, build its bitmap
-    k_resolve<<<grid_for(s->n, BLOCK, 16384), BLOCK, 0, st>>>(s->n, s->lab, s->flags, s->cnt + 4);
-    const uint32_t ns = std::min<uint32_t>(NSAMPLE, s->n);
-    k_sample_labels<<<grid_for(ns, 256, 256), 256, 0, st>>>(s->n, s->lab, ns, s->sample);
-    GHS_HIP_CHECK(hipGetLastError());
-    GHS_HIP_CHECK(hipMemcpyAsync(s->h_sample, s->sample, ns * 4, hipMemcpyDeviceToHost, st));
-    GHS_HIP_CHECK(hipStreamSynchronize(st));
-    std::vector<uint32_t> smp(s->h_sample, s->h_sample + ns);
-    std::sort(smp.begin(), smp.end());
-    uint32_t giant = smp[0];
-    size_t best_run = 0;
-    for (size_t i = 0; i < smp.size();) {
-      size_t j = i;
-      while (j < smp.size() && smp[j] == smp[i]) ++j;
-      if (j - i > best_run) {
-        best_run = j - i;
-        giant = smp[i];
-      }
-      i = j;
-    }
-    if (s->debug) fprintf(stderr, "[ghs] level %u: giant %u holds %zu/%zu sampled vertices\n", lv, giant, best_run, smp.size());
-    k_bitmap<<<grid_for(s->n, BLOCK, 16384), BLOCK, 0, st>>>(s->n, s->lab, giant, s->bits);
+    // compress labels, find the giant fragment from a sample, build its bitmap (all on device)
+    k_resolve<<<grid_for(s->n, BLOCK, 16384), BLOCK, 0, st>>>(s->n, s->lab, s->flags, s->cnt + C_ERR);
+    k_giant<<<1, 1024, 0, st>>>(s->n, s->lab, s->giant);
+    k_bitmap<<<grid_for(s->n, BLOCK, 16384), BLOCK, 0, st>>>(s->n, s->lab, s->giant, s->bits);
     GHS_HIP_CHECK(hipGetLastError());
   }
 
-  // 1. this level's edges -> regions of Y (level edges: a, b labels + key, canonical order)
+  // 1. this level's edges -> regions of Y (level edges: a, b labels + key, canonical order).
+  //    Single rank: the pass also flags both ends of every level edge (the level's active
+  //    fragments).
+  uint8_t *mark = single ? s->flags : nullptr;
+  if (mark) GHS_HIP_CHECK(hipMemsetAsync(s->flags, 0, s->n, st));
   unsigned G = 1;
-  uint64_t T = 0;
+  const uint64_t TC = s->e_hi > s->e_lo ? s->e_hi - (s->e_lo & ~3ull) : 0;  // canonical passes stream [e_lo & ~3, e_hi)
   if (first) {
     // SELECT over the canonical list: level-0 edges only (validates the list)
-    T = s->e_hi > s->e_lo ? s->e_hi - (s->e_lo & ~3ull) : 0;  // the canonical passes stream [e_lo & ~3, e_hi)
-    G = grid_for(T, ARCS_PER_BLOCK, SEG_G);
-    if (s->e_hi > s->e_lo) {
-      k_canon_pass<false><<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, 0, w_hi, nullptr, Y.src, Y.dst,
-                                               Y.key, Y.seg_start, Y.seg_count, s->cnt + 4);
+    G = grid_for(TC, ARCS_PER_BLOCK, SEG_G);
+    if (TC) {
+      k_canon_pass<false><<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, 0, w_hi, nullptr, Y.src,
+                                               Y.dst, Y.key, Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR);
       GHS_HIP_CHECK(hipGetLastError());
+      k_scan_counts<<<1, 1024, 0, st>>>(Y.seg_count, G, Y.seg_prefix, s->cnt + C_LIVE);
+    } else {
+      GHS_HIP_CHECK(hipMemsetAsync(Y.seg_prefix, 0, 16, st));
+      GHS_HIP_CHECK(hipMemsetAsync(s->cnt + C_LIVE, 0, 8, st));
     }
+    GHS_HIP_CHECK(hipMemsetAsync(s->cnt + C_PENDING, 0, 8, st));
   } else {
+    const int rin = s->rcur, rout = s->rcur ^ 1;
+    ArcBuf &RI = s->rem[rin], &RO = s->rem[rout];
     if (!s->pending_built) {
       // FILTER over the canonical list once level 0 is complete: every heavier edge not inside
       // the giant fragment becomes pending (regions of rem[rin])
-      const uint64_t TC = s->e_hi > s->e_lo ? s->e_hi - (s->e_lo & ~3ull) : 0;
       const unsigned GC = grid_for(TC, ARCS_PER_BLOCK, SEG_G);
-      if (s->e_hi > s->e_lo) {
+      if (TC) {
         k_canon_pass<true><<<GC, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, s->thresholds[lv], 0,
-                                                 s->bits, RI.src, RI.dst, RI.key, RI.seg_start, RI.seg_count,
-                                                 s->cnt + 4);
+                                                 s->bits, RI.src, RI.dst, RI.key, RI.seg_start, RI.seg_count, nullptr,
+                                                 s->cnt + C_ERR);
         GHS_HIP_CHECK(hipGetLastError());
-        k_scan_counts<<<1, 1024, 0, st>>>(RI.seg_count, GC, RI.seg_prefix, s->cnt + 5);
-        GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt + 5, s->cnt + 5, 8, hipMemcpyDeviceToHost, st));
-        GHS_HIP_CHECK(hipStreamSynchronize(st));
-        s->rem_total = s->h_cnt[5];
+        k_scan_counts<<<1, 1024, 0, st>>>(RI.seg_count, GC, RI.seg_prefix, s->cnt + C_PENDING);
       } else {
-        s->rem_total = 0;
+        GHS_HIP_CHECK(hipMemsetAsync(RI.seg_prefix, 0, 16, st));
       }
       s->rem_nseg = GC;
       s->pending_built = true;
-      s->stat_pending = s->rem_total;
     }
-    // split the pending edges: this level's inter-fragment edges -> Y staging; heavier
-    // survivors -> RO regions
-    T = s->rem_total;
-    G = grid_for(T, ARCS_PER_BLOCK, SEG_G);
-    if (T) {
-      SegView in{RI.seg_start, RI.seg_prefix, s->rem_nseg, T};
-      k_level_pass<<<G, BLOCK, 0, st>>>(RI.src, RI.dst, RI.key, in, w_hi, s->lab, s->bits, Y.src, Y.dst, Y.key,
-                                        Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key, RO.seg_start, RO.seg_count);
-      GHS_HIP_CHECK(hipGetLastError());
-      k_scan_counts<<<1, 1024, 0, st>>>(RO.seg_count, G, RO.seg_prefix, s->cnt + 5);
-    } else {
-      GHS_HIP_CHECK(hipMemsetAsync(s->cnt + 5, 0, 8, st));
-    }
-  }
-  if (T) {
-    k_scan_counts<<<1, 1024, 0, st>>>(Y.seg_count, G, Y.seg_prefix, s->cnt + 0);
+    // split the pending edges (total on the device): this level's inter-fragment edges -> Y;
+    // heavier survivors -> RO regions. Fixed grid: block b owns 1/SEG_G of the virtual range.
+    G = SEG_G;
+    SegView in{RI.seg_start, RI.seg_prefix, s->rem_nseg};
+    k_level_pass<<<G, BLOCK, 0, st>>>(RI.src, RI.dst, RI.key, in, w_hi, s->lab, s->bits, Y.src, Y.dst, Y.key,
+                                      Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key, RO.seg_start, RO.seg_count,
+                                      mark);
     GHS_HIP_CHECK(hipGetLastError());
-  } else {
-    GHS_HIP_CHECK(hipMemsetAsync(s->cnt, 0, 8, st));
-  }
-  GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-  GHS_HIP_CHECK(hipStreamSynchronize(st));
-  if (s->h_cnt[4] & 8) {
-    s->phase = 2;
-    GHS_FAIL(GHS_E_NONCANON, "edge list is not canonical (need u < v < n, strictly ascending (u, v))");
-  }
-  if (s->h_cnt[4]) {
-    s->phase = 2;
-    GHS_FAIL(GHS_E_STATE, "internal invariant violated (code " + std::to_string(s->h_cnt[4]) + ")");
-  }
-  const uint64_t S = s->h_cnt[0];
-  if (s->debug)
-    fprintf(stderr, "[ghs] level %u open: w_hi=%llu input=%llu level_edges=%llu pending_after=%llu (filter pass kept %llu)\n",
-            lv, (unsigned long long)w_hi, (unsigned long long)T, (unsigned long long)S,
-            (unsigned long long)(first ? 0 : s->h_cnt[5]), (unsigned long long)s->stat_pending);
-  if (!first) {
-    s->rem_total = s->h_cnt[5];
+    k_scan_counts<<<1, 1024, 0, st>>>(RO.seg_count, G, RO.seg_prefix, s->cnt + C_PENDING);
+    k_scan_counts<<<1, 1024, 0, st>>>(Y.seg_count, G, Y.seg_prefix, s->cnt + C_LIVE);
+    GHS_HIP_CHECK(hipGetLastError());
     s->rem_nseg = G;
     s->rcur = rout;
   }
+
+  // 2. active fragments. Single rank: the fragments that have an edge in this level.
+  //    Several ranks: every current root (first level: every vertex) — identical on every
+  //    rank without an exchange; roots without edges anywhere drop out after one round.
+  if (single || !first) {
+    if (int rc = select_flagged(s, s->flags, nullptr, s->cnt + C_N, s->n, s->act[0], s->cnt + C_ACT)) return rc;
+    s->act_ident = false;
+  } else {
+    s->act_ident = true;
+  }
+  s->act_cur = 0;
+  GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, C_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  GHS_HIP_CHECK(hipStreamSynchronize(st));
+  if (s->h_cnt[C_ERR]) return fail_counters(s, s->h_cnt[C_ERR], "opening a level");
+  const uint64_t S = s->h_cnt[C_LIVE];
+  s->rem_total = s->h_cnt[C_PENDING];
+  s->nact = s->act_ident ? s->n : s->h_cnt[C_ACT];
+  if (s->debug) {
+    uint32_t g[2] = {0, 0};
+    (void)hipMemcpy(g, s->giant, 8, hipMemcpyDeviceToHost);
+    fprintf(stderr, "[ghs] level %u open: w_hi=%llu level_edges=%llu active=%llu pending_after=%llu giant=%u (%u/2048 sampled)\n",
+            lv, (unsigned long long)w_hi, (unsigned long long)S, (unsigned long long)s->nact,
+            (unsigned long long)s->rem_total, first ? 0u : g[0], first ? 0u : g[1]);
+  }
   s->level_arcs = S;
-  if (S == 0 && s->cfg.num_ranks <= 1) {  // nothing to merge at this level (single rank only:
-    s->level_open = false;                // ranks must run the same rounds)
+  if (S == 0 && single) {  // nothing to merge at this level (single rank only: ranks must run the
+    s->level_open = false;   // same rounds)
     return GHS_OK;
   }
   s->cur = 1;  // the level's edges are Y's G regions (S entries incl. padding)
   s->cur_nseg = G;
   s->cur_arcs = S;
-  SegView lev{Y.seg_start, Y.seg_prefix, G, S};
-
-  // 2. active fragments. Single rank: the fragments that have an edge in this level.
-  //    Several ranks: every current root (first level: every vertex) — identical on every
-  //    rank without an exchange; roots without arcs anywhere drop out after one round.
-  if (s->cfg.num_ranks <= 1) {
-    GHS_HIP_CHECK(hipMemsetAsync(s->flags, 0, s->n, st));
-    if (S) k_mark_edges<<<grid_for(S, ARCS_PER_BLOCK, SEG_G), BLOCK, 0, st>>>(Y.src, Y.dst, lev, s->flags);
-    GHS_HIP_CHECK(hipGetLastError());
-    if (int rc = select_flagged(s, s->flags, nullptr, s->n, s->act[0], s->cnt + 1)) return rc;
-    GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt + 1, s->cnt + 1, 8, hipMemcpyDeviceToHost, st));
-    GHS_HIP_CHECK(hipStreamSynchronize(st));
-    s->act_ident = false;
-    s->act_cur = 0;
-    s->nact = s->h_cnt[1];
-  } else if (first) {
-    s->act_ident = true;
-    s->nact = s->n;
-  } else {
-    if (int rc = select_flagged(s, s->flags, nullptr, s->n, s->act[0], s->cnt + 1)) return rc;
-    GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt + 1, s->cnt + 1, 8, hipMemcpyDeviceToHost, st));
-    GHS_HIP_CHECK(hipStreamSynchronize(st));
-    s->act_ident = false;
-    s->act_cur = 0;
-    s->nact = s->h_cnt[1];
-  }
+  s->level_nact = s->nact;
   s->level_round = 0;
   s->level_open = true;
+  return GHS_OK;
+}
+
+static inline unsigned long long *act_count(ghs_solver *s, int which) { return s->cnt + C_ACT + which; }
+static inline const unsigned long long *cur_act_count(ghs_solver *s) {
+  return s->act_ident ? s->cnt + C_N : act_count(s, s->act_cur);
+}
+
+// ---- one round, enqueued without a host sync (sizes on the device; s->nact is a bound) --------
+static int enqueue_minedge(ghs_solver *s) {
+  record(s, 0);
+  const ArcBuf &I = s->buf[s->cur];
+  ArcBuf &O = s->buf[s->cur ^ 1];
+  SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
+  if (s->level_round == 0) {
+    if (s->cur_arcs)
+      k_minedge<true, false><<<grid_for(s->cur_arcs, ARCS_PER_BLOCK, SEG_G), BLOCK, 0, s->stream>>>(
+          I.src, I.dst, I.key, in, s->lab, s->best, nullptr, nullptr, nullptr, nullptr, nullptr);
+  } else {
+    // fixed grid: every one of the SEG_G blocks writes its region's count
+    k_minedge<false, true><<<SEG_G, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, O.src, O.dst,
+                                                          O.key, O.seg_start, O.seg_count);
+    k_scan_counts<<<1, 1024, 0, s->stream>>>(O.seg_count, SEG_G, O.seg_prefix, s->cnt + C_LIVE);
+  }
+  GHS_HIP_CHECK(hipGetLastError());
+  record(s, 1);
+  return GHS_OK;
+}
+
+static int enqueue_contract(ghs_solver *s) {
+  const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
+  const unsigned long long *d_nact = cur_act_count(s);
+  const uint64_t bound = s->nact;
+  const int nb = s->act_ident ? 0 : (s->act_cur ^ 1);
+  if (bound) {
+    const unsigned g = grid_for(bound, BLOCK, 65535);
+    // CONNECT: edge form while fragments are many and small (a level's first round: its edges
+    // carry the current roots), fragment form otherwise (and always with several ranks: a
+    // fragment's best edge may live on another rank)
+    const bool edge_form = s->cfg.num_ranks <= 1 && s->level_round == 0 && s->cur_arcs < 8 * bound;
+    if (edge_form) {
+      const ArcBuf &I = s->buf[s->cur];
+      SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
+      k_win<<<grid_for(s->cur_arcs, ARCS_PER_BLOCK, SEG_G), BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->best,
+                                                                                   s->par, s->in_mst, s->cnt + C_WEIGHT);
+    } else {
+      k_hook<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
+                                         s->cnt + C_WEIGHT, s->cnt + C_ERR);
+    }
+    GHS_HIP_CHECK(hipGetLastError());
+    record(s, 2);
+    k_jump<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->par, s->lab, s->cnt + C_ERR);
+    GHS_HIP_CHECK(hipGetLastError());
+    record(s, 3);
+    k_flag_next<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->par, s->best, s->flags);
+    GHS_HIP_CHECK(hipGetLastError());
+    if (int rc = select_flagged(s, s->flags, act, d_nact, bound, s->act[nb], act_count(s, nb))) return rc;
+  } else {
+    record(s, 2);
+    record(s, 3);
+    GHS_HIP_CHECK(hipMemsetAsync(act_count(s, nb), 0, 8, s->stream));
+  }
+  record(s, 4);
+  return GHS_OK;
+}
+
+// host-side bookkeeping after a round was enqueued (buffers / lists flip; no device values)
+static void advance_round(ghs_solver *s) {
+  if (s->level_round >= 1) {  // this round's min-edge kernel compacted into the other buffer
+    s->cur ^= 1;
+    s->cur_nseg = SEG_G;
+  }
+  s->act_cur = s->act_ident ? 0 : (s->act_cur ^ 1);
+  s->act_ident = false;
+  s->round += 1;
+  s->level_round += 1;
+}
+
+static void push_stats(ghs_solver *s, uint32_t level_round, uint64_t live_in, uint64_t nact_in, uint64_t edges_total) {
+  ghs_round_stats_t st{};
+  st.level = s->level;
+  st.level_arcs = level_round == 0 ? s->level_arcs : 0;
+  st.live_arcs = live_in;
+  st.active_components = nact_in;
+  st.hooks = edges_total - s->edges_before;
+  s->edges_before = edges_total;
+  s->stats.push_back(st);
+}
+
+static void close_level(ghs_solver *s) {
+  s->level_open = false;
+  s->level += 1;
+  const bool no_more =
+      (s->level + 1 >= s->thresholds.size()) || (s->cfg.num_ranks <= 1 && s->pending_built && s->rem_total == 0);
+  s->phase = no_more ? 2 : 0;
+}
+
+// ---- single-rank level loop: rounds are enqueued LOOKAHEAD ahead of the termination check ------
+// Each round copies (live, active, edges, err) to a pinned slot behind an event; the host waits
+// only for the round LOOKAHEAD back. Rounds past the last are no-ops on the device (zero active
+// fragments, zero live inter-fragment edges) and are discarded.
+static int run_level_pipelined(ghs_solver *s) {
+  const uint32_t round0 = s->round;
+  uint64_t live_prev = s->cur_arcs, nact_prev = s->level_nact;  // inputs of the next checked round
+  uint32_t issued = 0, checked = 0;
+  for (;;) {
+    if (issued < checked + 1 + LOOKAHEAD) {
+      if (issued >= LEVEL_ROUND_CAP) GHS_FAIL(GHS_E_ROUNDCAP, "round cap exceeded in a level");
+      if (int rc = enqueue_minedge(s)) return rc;
+      if (int rc = enqueue_contract(s)) return rc;
+      const int nb = s->act_ident ? 0 : (s->act_cur ^ 1);
+      const int slot = issued % SLOT_RING;
+      k_round_report<<<1, 1, 0, s->stream>>>(s->cnt, act_count(s, nb), &s->d_slot[slot].live_out);
+      GHS_HIP_CHECK(hipGetLastError());
+      GHS_HIP_CHECK(hipEventRecord(s->slot_ev[slot], s->stream));
+      advance_round(s);
+      ++issued;
+      continue;
+    }
+    GHS_HIP_CHECK(hipEventSynchronize(s->slot_ev[checked % SLOT_RING]));
+    const RoundSlot r = s->h_slot[checked % SLOT_RING];
+    if (r.err) return fail_counters(s, r.err, ("in round " + std::to_string(round0 + checked + 1)).c_str());
+    push_stats(s, checked, live_prev, nact_prev, r.edges);
+    // the live edges of round k + 1: round 0 does not compact (its input is read again)
+    live_prev = checked == 0 ? live_prev : r.live_out;
+    nact_prev = r.nact_out;
+    s->nact = r.nact_out;  // tighter bound for the rounds enqueued from here on
+    ++checked;
+    if (r.nact_out == 0) break;  // level complete after round `checked`
+  }
+  // rounds issued past the last real one were no-ops: rewind the round counter
+  s->round = round0 + checked;
+  close_level(s);
   return GHS_OK;
 }
 
@@ -1365,31 +1686,42 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   s->eu = d_u; s->ev = d_v; s->ew = d_w;
   s->in_mst = d_in_mst; s->stream = (hipStream_t)stream;
   { const char *dbg = getenv("GHS_DEBUG"); s->debug = dbg && dbg[0] == '1'; }
-
   if (cfg) s->cfg = *cfg; else default_config(&s->cfg);
   workspace_layout(n, e_hi - e_lo, s, (char *)d_workspace);
-  auto fail = [&](hipError_t e, const char *what) {
-    set_error(std::string(what) + ": " + hipGetErrorString(e));
-    if (s->h_cnt) (void)hipHostFree(s->h_cnt);
-    if (s->h_sample) (void)hipHostFree(s->h_sample);
-    delete s;
+  hipError_t e;
+  auto fail = [&](hipError_t err, const char *what) {
+    set_error(std::string(what) + ": " + hipGetErrorString(err));
+    ghs_solver_destroy(s);
     return GHS_E_HIP;
   };
-  hipError_t e;
-  if ((e = hipHostMalloc((void **)&s->h_cnt, 8 * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess)
+  if ((e = hipHostMalloc((void **)&s->h_cnt, C_COUNT * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess)
     return fail(e, "hipHostMalloc");
+  // round slots: pinned, coherent, written by k_round_report, read by the host after the slot's
+  // event has completed
+  if ((e = hipHostMalloc((void **)&s->h_slot, SLOT_RING * sizeof(RoundSlot), hipHostMallocMapped | hipHostMallocCoherent)) !=
+      hipSuccess)
+    return fail(e, "hipHostMalloc");
+  if ((e = hipHostGetDevicePointer((void **)&s->d_slot, s->h_slot, 0)) != hipSuccess)
+    return fail(e, "hipHostGetDevicePointer");
   if ((e = hipHostMalloc((void **)&s->h_sample, NSAMPLE_MAX * 4, hipHostMallocDefault)) != hipSuccess)
     return fail(e, "hipHostMalloc");
+  for (int i = 0; i < SLOT_RING; ++i)
+    if ((e = hipEventCreateWithFlags(&s->slot_ev[i], hipEventDisableTiming)) != hipSuccess)
+      return fail(e, "hipEventCreate");
   s->t0 = std::chrono::steady_clock::now();
   if (n) {
     if ((e = hipMemsetAsync(s->best, 0xff, (size_t)n * 8, s->stream)) != hipSuccess) return fail(e, "memset best");
     k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->lab, n);
+    k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->par, n);  // every root: par[r] == r
   }
   if (m && (e = hipMemsetAsync(s->in_mst, 0, m, s->stream)) != hipSuccess) return fail(e, "memset in_mst");
-  if ((e = hipMemsetAsync(s->cnt, 0, 8 * sizeof(unsigned long long), s->stream)) != hipSuccess)
+  if ((e = hipMemsetAsync(s->cnt, 0, C_COUNT * sizeof(unsigned long long), s->stream)) != hipSuccess)
     return fail(e, "memset counters");
+  const unsigned long long nn = n;
+  if ((e = hipMemcpyAsync(s->cnt + C_N, &nn, 8, hipMemcpyHostToDevice, s->stream)) != hipSuccess)
+    return fail(e, "counter init");
   if ((e = hipGetLastError()) != hipSuccess) return fail(e, "init kernels");
-  int rc = plan_levels(s);
+  int rc = plan_levels(s);  // syncs the stream (nn stays valid until then)
   if (rc) {
     ghs_solver_destroy(s);
     return rc;
@@ -1401,6 +1733,7 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   return GHS_OK;
 }
 
+// stepwise API: one round per minedge/contract pair, exact counts after every contract
 int ghs_solver_minedge(ghs_solver_t *s, uint64_t *num_active) {
   if (!s) GHS_FAIL(GHS_E_ARG, "solver is NULL");
   if (s->phase == 2) {
@@ -1417,28 +1750,9 @@ int ghs_solver_minedge(ghs_solver_t *s, uint64_t *num_active) {
     }
     int rc = open_level(s);
     if (rc) return rc;
-    if (!s->level_open) s->level += 1;  // skipped (no arcs)
+    if (!s->level_open) s->level += 1;  // skipped (no edges)
   }
-  record(s, 0);
-  const uint64_t A = s->cur_arcs;
-  const ArcBuf &I = s->buf[s->cur];
-  ArcBuf &O = s->buf[s->cur ^ 1];
-  if (A) {
-    SegView in{I.seg_start, I.seg_prefix, s->cur_nseg, A};
-    const unsigned G = grid_for(A, ARCS_PER_BLOCK, SEG_G);
-    if (s->level_round == 0) {
-      k_minedge<true, false><<<G, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, nullptr, nullptr,
-                                                         nullptr, nullptr, nullptr);
-    } else {
-      // unused segment slots of O (when G < SEG_G) stay zero-count
-      if (G < SEG_G) GHS_HIP_CHECK(hipMemsetAsync(O.seg_count + G, 0, (SEG_G - G) * 8, s->stream));
-      k_minedge<false, true><<<G, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, O.src, O.dst,
-                                                         O.key, O.seg_start, O.seg_count);
-      k_scan_counts<<<1, 1024, 0, s->stream>>>(O.seg_count, SEG_G, O.seg_prefix, s->cnt + 0);
-    }
-    GHS_HIP_CHECK(hipGetLastError());
-  }
-  record(s, 1);
+  if (int rc = enqueue_minedge(s)) return rc;
   s->phase = 1;
   if (num_active) *num_active = s->nact;
   return GHS_OK;
@@ -1449,7 +1763,7 @@ int ghs_solver_pack_best(ghs_solver_t *s, int64_t *d_dense) {
   if (s->phase != 1) GHS_FAIL(GHS_E_STATE, "pack_best must follow minedge");
   if (s->nact) {
     const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
-    k_pack_best<<<grid_for(s->nact, 256, 16384), 256, 0, s->stream>>>(act, s->nact, s->best, d_dense);
+    k_pack_best<<<grid_for(s->nact, 256, 16384), 256, 0, s->stream>>>(act, cur_act_count(s), s->best, d_dense);
     GHS_HIP_CHECK(hipGetLastError());
   }
   return GHS_OK;
@@ -1460,7 +1774,7 @@ int ghs_solver_unpack_best(ghs_solver_t *s, const int64_t *d_dense) {
   if (s->phase != 1) GHS_FAIL(GHS_E_STATE, "unpack_best must follow minedge");
   if (s->nact) {
     const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
-    k_unpack_best<<<grid_for(s->nact, 256, 16384), 256, 0, s->stream>>>(act, s->nact, s->best, d_dense);
+    k_unpack_best<<<grid_for(s->nact, 256, 16384), 256, 0, s->stream>>>(act, cur_act_count(s), s->best, d_dense);
     GHS_HIP_CHECK(hipGetLastError());
   }
   return GHS_OK;
@@ -1473,61 +1787,18 @@ int ghs_solver_contract(ghs_solver_t *s, int *done) {
     return GHS_OK;
   }
   if (s->phase != 1) GHS_FAIL(GHS_E_STATE, "contract must follow minedge");
-  const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
-  const uint64_t nact = s->nact;
-  const unsigned g = grid_for(nact, BLOCK, 65535);
-  if (nact) {
-    k_hook<<<grid_for(nact, BLOCK, 65535), BLOCK, 0, s->stream>>>(act, nact, s->best, s->lab, s->eu, s->ev, s->par,
-                                                                 s->in_mst, s->cnt + 2, s->cnt + 4);
-    GHS_HIP_CHECK(hipGetLastError());
-  }
-  record(s, 2);
-  if (nact) {
-    k_jump<<<g, BLOCK, 0, s->stream>>>(act, nact, s->par, s->lab, s->cnt + 4);
-    GHS_HIP_CHECK(hipGetLastError());
-  }
-  record(s, 3);
+  const uint64_t live_in = s->level_round <= 1 ? s->cur_arcs : s->h_cnt[C_LIVE];
+  const uint64_t nact_in = s->nact;
+  if (int rc = enqueue_contract(s)) return rc;
   const int nb = s->act_ident ? 0 : (s->act_cur ^ 1);
-  if (nact) {
-    k_flag_next<<<g, BLOCK, 0, s->stream>>>(act, nact, s->par, s->best, s->flags);
-    GHS_HIP_CHECK(hipGetLastError());
-    if (int rc = select_flagged(s, s->flags, act, nact, s->act[nb], s->cnt + 1)) return rc;
-  } else {
-    GHS_HIP_CHECK(hipMemsetAsync(s->cnt + 1, 0, 8, s->stream));
-  }
-  record(s, 4);
-  GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
+  GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, C_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
   GHS_HIP_CHECK(hipStreamSynchronize(s->stream));
-  if (s->h_cnt[4]) {
-    s->phase = 2;
-    GHS_FAIL(GHS_E_STATE, "internal invariant violated in round " + std::to_string(s->round + 1) + " (code " +
-                              std::to_string(s->h_cnt[4]) + ")");
-  }
-  ghs_round_stats_t st{};
-  st.level = s->level;
-  st.level_arcs = s->level_round == 0 ? s->level_arcs : 0;
-  st.live_arcs = s->cur_arcs;
-  st.active_components = nact;
-  st.hooks = s->h_cnt[3] - s->edges_before;
-  s->edges_before = s->h_cnt[3];
-  s->stats.push_back(st);
-
-  // the arcs compacted by this round's min-edge kernel are the next round's input
-  if (s->level_round >= 1 && s->cur_arcs) {
-    s->cur ^= 1;
-    s->cur_nseg = SEG_G;
-    s->cur_arcs = s->h_cnt[0];
-  }
-  s->act_cur = nb;
-  s->act_ident = false;
-  s->nact = s->h_cnt[1];
-  s->round += 1;
-  s->level_round += 1;
+  if (s->h_cnt[C_ERR]) return fail_counters(s, s->h_cnt[C_ERR], ("in round " + std::to_string(s->round + 1)).c_str());
+  push_stats(s, s->level_round, live_in, nact_in, s->h_cnt[C_EDGES]);
+  s->nact = s->h_cnt[C_ACT + nb];
+  advance_round(s);
   if (s->nact == 0) {  // level complete
-    s->level_open = false;
-    s->level += 1;
-    const bool no_more = (s->level + 1 >= s->thresholds.size()) || (s->cfg.num_ranks <= 1 && s->pending_built && s->rem_total == 0);
-    s->phase = no_more ? 2 : 0;
+    close_level(s);
   } else {
     s->phase = 0;
   }
@@ -1538,6 +1809,7 @@ int ghs_solver_contract(ghs_solver_t *s, int *done) {
 int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *stats) {
   if (!s) GHS_FAIL(GHS_E_ARG, "solver is NULL");
   if (s->phase != 2) GHS_FAIL(GHS_E_STATE, "finish before the loop terminated");
+  GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, C_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
   GHS_HIP_CHECK(hipStreamSynchronize(s->stream));
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s->t0).count();
   const uint32_t ns = (uint32_t)std::min<size_t>(s->stats.size(), GHS_MAX_ROUND_STATS);
@@ -1554,8 +1826,8 @@ int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *
     if (stats) stats[r] = s->stats[r];
   }
   if (result) {
-    result->num_mst_edges = s->n ? s->h_cnt[3] : 0;
-    result->total_weight = s->n ? s->h_cnt[2] : 0;
+    result->num_mst_edges = s->n ? s->h_cnt[C_EDGES] : 0;
+    result->total_weight = s->n ? s->h_cnt[C_WEIGHT] : 0;
     result->rounds = s->round;
     result->num_stats = ns;
     result->levels = (uint32_t)(s->thresholds.size() - 1);
@@ -1567,7 +1839,10 @@ int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *
 int ghs_solver_destroy(ghs_solver_t *s) {
   if (!s) return GHS_OK;
   for (hipEvent_t e : s->ev_pool) (void)hipEventDestroy(e);
+  for (int i = 0; i < SLOT_RING; ++i)
+    if (s->slot_ev[i]) (void)hipEventDestroy(s->slot_ev[i]);
   if (s->h_cnt) (void)hipHostFree(s->h_cnt);
+  if (s->h_slot) (void)hipHostFree(s->h_slot);
   if (s->h_sample) (void)hipHostFree(s->h_sample);
   delete s;
   return GHS_OK;
@@ -1578,12 +1853,25 @@ int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *
                    ghs_result_t *result, ghs_round_stats_t *stats) {
   std::lock_guard<std::mutex> lock(g_mutex);
   ghs_solver_t *s = nullptr;
-  int rc = ghs_solver_create(n, m, d_u, d_v, d_w, 0, m, cfg, d_workspace, workspace_bytes, d_in_mst, stream, &s);
+  ghs_config_t c;
+  if (cfg) c = *cfg; else default_config(&c);
+  c.num_ranks = 1;  // one device holds every edge
+  int rc = ghs_solver_create(n, m, d_u, d_v, d_w, 0, m, &c, d_workspace, workspace_bytes, d_in_mst, stream, &s);
   if (rc) return rc;
-  int done = (n == 0);
-  while (!done) {
-    if ((rc = ghs_solver_minedge(s, nullptr))) break;
-    if ((rc = ghs_solver_contract(s, &done))) break;
+  while (!rc && s->phase != 2) {
+    if (!s->level_open) {
+      if (s->level + 1 >= s->thresholds.size()) {
+        s->phase = 2;
+        break;
+      }
+      rc = open_level(s);
+      if (rc) break;
+      if (!s->level_open) {
+        s->level += 1;  // skipped (no edges)
+        continue;
+      }
+    }
+    rc = run_level_pipelined(s);
   }
   if (!rc) rc = ghs_solver_finish(s, result, stats);
   ghs_solver_destroy(s);
