@@ -604,12 +604,14 @@ GHS_STREAM_KERNEL void k_win(const uint32_t *__restrict__ src, const uint32_t *_
 // ancestors and every walk ends at its root. lab[c] = root.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
-                                                uint32_t *par, uint32_t *__restrict__ lab, unsigned long long *__restrict__ err) {
+                                                uint32_t *par, uint32_t *__restrict__ lab, uint64_t *__restrict__ best,
+                                                uint8_t *__restrict__ flags, unsigned long long *__restrict__ err) {
   const uint64_t nact = *d_nact;
   for (uint64_t i = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; i < nact; i += (uint64_t)gridDim.x * BLOCK) {
     const uint32_t c = act ? act[i] : (uint32_t)i;
     uint32_t x = c;
     uint32_t px = par[x];
+    const bool root = px == c;  // roots are never rewritten below: par[c] == c is stable
     uint32_t steps = 0;
     while (px != x) {
       const uint32_t ppx = par[px];
@@ -622,24 +624,12 @@ __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act
       }
     }
     lab[c] = x;
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Stage 3b: flags of the next active fragment list = roots that still had an outgoing edge
-// (their best slot is reset). A root with no outgoing edge is finished for this level (the
-// reference: "best_weight == inf at the core => terminate", ghs_implementation.py:316-320).
-// The list is produced by an order-preserving select, so every rank of a multi-GPU run holds
-// the same list in the same order and the all-reduce slots line up.
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BLOCK) void k_flag_next(const uint32_t *__restrict__ act,
-                                                     const unsigned long long *__restrict__ d_nact,
-                                                     const uint32_t *__restrict__ par, uint64_t *__restrict__ best,
-                                                     uint8_t *__restrict__ flags) {
-  const uint64_t nact = *d_nact;
-  for (uint64_t i = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; i < nact; i += (uint64_t)gridDim.x * BLOCK) {
-    const uint32_t c = act ? act[i] : (uint32_t)i;
-    const bool keep = (par[c] == c) && (best[c] != KEY_NONE);
+    // Stage 3b: the next active list = roots that still had an outgoing edge (their best slot
+    // is reset). A root with no outgoing edge is finished for this level (the reference:
+    // "best_weight == inf at the core => terminate", ghs_implementation.py:316-320). The list
+    // is produced by an order-preserving select, so every rank of a multi-GPU run holds the
+    // same list in the same order and the all-reduce slots line up.
+    const bool keep = root && best[c] != KEY_NONE;
     if (keep) best[c] = KEY_NONE;
     flags[i] = keep ? 1 : 0;
   }
@@ -1147,11 +1137,37 @@ __global__ __launch_bounds__(BLOCK) void k_sel_count(const uint8_t *__restrict__
   }
 }
 
+// Result of a round, written into coherent pinned host memory by the round's last kernel; the
+// host polls seq (written last, after a system-scope fence).
+struct RoundSlot {
+  unsigned long long live_out, nact_out, edges, err;
+  unsigned long long seq;
+  unsigned long long pad[3];
+};
+
+__device__ __forceinline__ void write_report(RoundSlot *slot, unsigned long long seq, const unsigned long long *cnt,
+                                             unsigned long long nact_out) {
+  slot->live_out = cnt[0];  // live edges after this round's compaction
+  slot->nact_out = nact_out;  // active fragments of the next round
+  slot->edges = cnt[3];     // MSF edges so far
+  slot->err = cnt[4];       // error bits
+  __threadfence_system();
+  __hip_atomic_store(&slot->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void k_round_report(RoundSlot *slot, unsigned long long seq, const unsigned long long *cnt,
+                               const unsigned long long *nact_out) {
+  write_report(slot, seq, cnt, *nact_out);
+}
+
 __global__ __launch_bounds__(BLOCK) void k_sel_write(const uint8_t *__restrict__ flags, const uint32_t *__restrict__ in,
                                                      const unsigned long long *__restrict__ d_count,
-                                                     const uint64_t *__restrict__ bprefix, uint32_t *__restrict__ out) {
+                                                     const uint64_t *__restrict__ bprefix, uint32_t *__restrict__ out,
+                                                     RoundSlot *slot, unsigned long long seq,
+                                                     const unsigned long long *__restrict__ cnt) {
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
   const uint64_t count = *d_count;
+  if (slot && blockIdx.x == 0 && threadIdx.x == 0) write_report(slot, seq, cnt, bprefix[gridDim.x]);
   const uint64_t i0 = (uint64_t)blockIdx.x * SEL_PER_BLOCK + threadIdx.x * 16ull;
   uint32_t bits = 0;  // bit k = flags[i0 + k]
   if (i0 + 16 <= count) {
@@ -1174,14 +1190,6 @@ __global__ __launch_bounds__(BLOCK) void k_sel_write(const uint8_t *__restrict__
   }
 }
 
-// a round's results into the pinned host slot (one launch instead of three copies)
-__global__ void k_round_report(const unsigned long long *__restrict__ cnt, const unsigned long long *__restrict__ nact_out,
-                               unsigned long long *__restrict__ slot) {
-  slot[0] = cnt[0];      // live edges after this round's compaction
-  slot[1] = nact_out[0]; // active fragments of the next round
-  slot[2] = cnt[3];      // MSF edges so far
-  slot[3] = cnt[4];      // error bits
-}
 
 static inline unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap) {
   uint64_t g = (items + per_block - 1) / per_block;
@@ -1219,12 +1227,42 @@ enum : int {
   C_COUNT = 16
 };
 
-struct RoundSlot {  // pinned copy of a round's results (pipelined loop)
-  unsigned long long live_out, nact_out, edges, err;
-};
 constexpr int SLOT_RING = 8;
 constexpr int LOOKAHEAD = 2;            // rounds enqueued ahead of the host's termination check
 constexpr uint32_t LEVEL_ROUND_CAP = 64;  // hang guard: a level takes O(log n) rounds
+
+// Host-side resources of a solve: pinned buffers and timing events. Creating them costs far
+// more than a small solve (page-pinning, event objects), so the one-shot entry point keeps one
+// set per device for the process and reuses it; a stepwise solver handle owns its own.
+struct HostRes {
+  unsigned long long *h_cnt = nullptr;  // pinned mirror of the device counters
+  RoundSlot *h_slot = nullptr;          // pinned, coherent ring of round reports (host view)
+  RoundSlot *d_slot = nullptr;          // the same ring, device view
+  uint32_t *h_sample = nullptr;         // pinned sample buffer
+  std::vector<hipEvent_t> ev_pool;      // timing events, 6 per round
+  unsigned long long seq = 0;           // round reports issued through h_slot (monotonic across solves)
+};
+
+static int hostres_init(HostRes *r) {
+  GHS_HIP_CHECK(hipHostMalloc((void **)&r->h_cnt, C_COUNT * sizeof(unsigned long long), hipHostMallocDefault));
+  // round slots: written by the round's last kernel, read by the host after seq has landed
+  GHS_HIP_CHECK(hipHostMalloc((void **)&r->h_slot, SLOT_RING * sizeof(RoundSlot), hipHostMallocMapped | hipHostMallocCoherent));
+  GHS_HIP_CHECK(hipHostGetDevicePointer((void **)&r->d_slot, r->h_slot, 0));
+  GHS_HIP_CHECK(hipHostMalloc((void **)&r->h_sample, 16384 * 4, hipHostMallocDefault));
+  memset(r->h_slot, 0, SLOT_RING * sizeof(RoundSlot));
+  return GHS_OK;
+}
+
+static void hostres_free(HostRes *r) {
+  for (hipEvent_t e : r->ev_pool) (void)hipEventDestroy(e);
+  r->ev_pool.clear();
+  if (r->h_cnt) (void)hipHostFree(r->h_cnt);
+  if (r->h_slot) (void)hipHostFree(r->h_slot);
+  if (r->h_sample) (void)hipHostFree(r->h_sample);
+  r->h_cnt = nullptr;
+  r->h_slot = r->d_slot = nullptr;
+  r->h_sample = nullptr;
+}
 
 struct ghs_solver {
   uint32_t n = 0;
@@ -1249,11 +1287,12 @@ struct ghs_solver {
   bool debug = false;        // GHS_DEBUG=1: per-level sizes on stderr
   uint64_t cap_arcs = 0;
   unsigned long long *cnt = nullptr;    // device counters (C_*)
-  unsigned long long *h_cnt = nullptr;  // pinned host mirror
-  RoundSlot *h_slot = nullptr;          // pinned ring of round results (host view)
-  RoundSlot *d_slot = nullptr;          // the same ring, device view
-  hipEvent_t slot_ev[SLOT_RING] = {};
-  uint32_t *h_sample = nullptr;         // pinned host sample buffer
+  HostRes own;                          // host resources owned by this handle (stepwise API)
+  HostRes *res = nullptr;               // the resources in use (own, or the process pool)
+  unsigned long long *h_cnt = nullptr;  // = res->h_cnt
+  RoundSlot *h_slot = nullptr;          // = res->h_slot
+  RoundSlot *d_slot = nullptr;          // = res->d_slot
+  uint32_t *h_sample = nullptr;         // = res->h_sample
 
   // level plan (identical on every rank: computed from the global canonical list)
   std::vector<uint64_t> thresholds;  // level i: [thr[i], thr[i+1])
@@ -1275,11 +1314,30 @@ struct ghs_solver {
   uint64_t edges_before = 0;
 
   std::vector<ghs_round_stats_t> stats;
-  std::vector<hipEvent_t> ev_pool;
+  std::vector<uint8_t> ev_rec;  // per round: bit k = event k recorded
+  bool detail = false;          // GHS_DETAIL=1: time every stage (adds ~5.7 us per event)
   std::chrono::steady_clock::time_point t0;
 };
 
 static std::mutex g_mutex;  // the one-shot entry points are serialised per process
+static HostRes *g_create_pool = nullptr;  // set (under g_mutex) while ghs_mst_device creates its solver
+
+// process-wide host resources of the one-shot entry point, one set per device (under g_mutex)
+static HostRes *pooled_res(int *rc) {
+  static std::unordered_map<int, HostRes *> pools;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  auto it = pools.find(dev);
+  if (it != pools.end()) return it->second;
+  HostRes *r = new HostRes();
+  if ((*rc = hostres_init(r)) != GHS_OK) {
+    hostres_free(r);
+    delete r;
+    return nullptr;
+  }
+  pools[dev] = r;
+  return r;
+}
 
 static constexpr uint32_t NSAMPLE_W = 16384; // weights sampled for the level plan
 static constexpr uint32_t NSAMPLE_MAX = NSAMPLE_W;
@@ -1330,31 +1388,42 @@ static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, 
 static hipEvent_t round_event(ghs_solver *s, uint32_t round, int k) {
   if (round >= GHS_MAX_ROUND_STATS) return nullptr;
   const size_t idx = (size_t)round * 6 + k;
-  while (s->ev_pool.size() <= idx) {
+  std::vector<hipEvent_t> &pool = s->res->ev_pool;
+  while (pool.size() <= idx) {
     hipEvent_t ev = nullptr;
     if (hipEventCreate(&ev) != hipSuccess) return nullptr;
-    s->ev_pool.push_back(ev);
+    pool.push_back(ev);
   }
-  return s->ev_pool[idx];
+  return pool[idx];
 }
 
+// Timing events cost ~5.7 us of GPU idle each between dependent kernels (measured), so by
+// default only the compacting min-edge launches are bracketed (the bench's roofline kernel);
+// GHS_DETAIL=1 brackets every stage of every round.
 static void record(ghs_solver *s, int k) {
   hipEvent_t ev = round_event(s, s->round, k);
-  if (ev) (void)hipEventRecord(ev, s->stream);
+  if (!ev) return;
+  if (hipEventRecord(ev, s->stream) != hipSuccess) return;
+  if (s->ev_rec.size() <= s->round) s->ev_rec.resize(s->round + 1, 0);
+  s->ev_rec[s->round] |= (uint8_t)(1u << k);
 }
 
 // Order-preserving select of the flagged items of [0, count) (or of in[0, count)), count on the
 // device (d_count), bound >= count on the host; *d_total = k.
+// slot != nullptr: the write kernel also reports the round (seq) to the pinned slot.
 static int select_flagged(ghs_solver *s, const uint8_t *flags, const uint32_t *in, const unsigned long long *d_count,
-                          uint64_t bound, uint32_t *out, unsigned long long *d_total) {
+                          uint64_t bound, uint32_t *out, unsigned long long *d_total, RoundSlot *slot = nullptr,
+                          unsigned long long seq = 0) {
   if (bound == 0) {
     GHS_HIP_CHECK(hipMemsetAsync(d_total, 0, 8, s->stream));
+    if (slot) k_round_report<<<1, 1, 0, s->stream>>>(slot, seq, s->cnt, d_total);
+    GHS_HIP_CHECK(hipGetLastError());
     return GHS_OK;
   }
   const unsigned nb = (unsigned)((bound + SEL_PER_BLOCK - 1) / SEL_PER_BLOCK);
   k_sel_count<<<nb, BLOCK, 0, s->stream>>>(flags, d_count, s->sel_cnt);
   k_scan_counts<<<1, 1024, 0, s->stream>>>(s->sel_cnt, nb, s->sel_pre, d_total);
-  k_sel_write<<<nb, BLOCK, 0, s->stream>>>(flags, in, d_count, s->sel_pre, out);
+  k_sel_write<<<nb, BLOCK, 0, s->stream>>>(flags, in, d_count, s->sel_pre, out, slot, seq, s->cnt);
   GHS_HIP_CHECK(hipGetLastError());
   return GHS_OK;
 }
@@ -1516,7 +1585,8 @@ static inline const unsigned long long *cur_act_count(ghs_solver *s) {
 
 // ---- one round, enqueued without a host sync (sizes on the device; s->nact is a bound) --------
 static int enqueue_minedge(ghs_solver *s) {
-  record(s, 0);
+  const bool timed = s->detail || s->level_round >= 1;
+  if (timed) record(s, 0);
   const ArcBuf &I = s->buf[s->cur];
   ArcBuf &O = s->buf[s->cur ^ 1];
   SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
@@ -1531,11 +1601,12 @@ static int enqueue_minedge(ghs_solver *s) {
     k_scan_counts<<<1, 1024, 0, s->stream>>>(O.seg_count, SEG_G, O.seg_prefix, s->cnt + C_LIVE);
   }
   GHS_HIP_CHECK(hipGetLastError());
-  record(s, 1);
+  if (timed) record(s, 1);
   return GHS_OK;
 }
 
-static int enqueue_contract(ghs_solver *s) {
+// slot != nullptr: the round's last kernel reports (live, active, edges, err, seq) to it
+static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned long long seq = 0) {
   const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
   const unsigned long long *d_nact = cur_act_count(s);
   const uint64_t bound = s->nact;
@@ -1556,19 +1627,30 @@ static int enqueue_contract(ghs_solver *s) {
                                          s->cnt + C_WEIGHT, s->cnt + C_ERR);
     }
     GHS_HIP_CHECK(hipGetLastError());
-    record(s, 2);
-    k_jump<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->par, s->lab, s->cnt + C_ERR);
+    if (s->detail) record(s, 2);
+    k_jump<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->par, s->lab, s->best, s->flags, s->cnt + C_ERR);
     GHS_HIP_CHECK(hipGetLastError());
-    record(s, 3);
-    k_flag_next<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->par, s->best, s->flags);
-    GHS_HIP_CHECK(hipGetLastError());
-    if (int rc = select_flagged(s, s->flags, act, d_nact, bound, s->act[nb], act_count(s, nb))) return rc;
+    if (s->detail) record(s, 3);
+    if (int rc = select_flagged(s, s->flags, act, d_nact, bound, s->act[nb], act_count(s, nb), slot, seq)) return rc;
   } else {
-    record(s, 2);
-    record(s, 3);
-    GHS_HIP_CHECK(hipMemsetAsync(act_count(s, nb), 0, 8, s->stream));
+    if (int rc = select_flagged(s, s->flags, act, d_nact, 0, s->act[nb], act_count(s, nb), slot, seq)) return rc;
   }
-  record(s, 4);
+  if (s->detail) record(s, 4);
+  return GHS_OK;
+}
+
+// spin until the round report with this seq has landed in the pinned slot (the stream keeps
+// running); a failed or drained stream without the report is an error, never a hang
+static int wait_slot(ghs_solver *s, const RoundSlot *hs, unsigned long long seq) {
+  unsigned spins = 0;
+  while (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) != seq) {
+    if ((++spins & 255) == 0) {
+      const hipError_t q = hipStreamQuery(s->stream);
+      if (q != hipSuccess && q != hipErrorNotReady) GHS_HIP_CHECK(q);
+      if (q == hipSuccess && __atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) != seq)
+        GHS_FAIL(GHS_E_STATE, "round report missing after the stream drained");
+    }
+  }
   return GHS_OK;
 }
 
@@ -1611,22 +1693,25 @@ static int run_level_pipelined(ghs_solver *s) {
   const uint32_t round0 = s->round;
   uint64_t live_prev = s->cur_arcs, nact_prev = s->level_nact;  // inputs of the next checked round
   uint32_t issued = 0, checked = 0;
+  std::vector<unsigned long long> seqs(LEVEL_ROUND_CAP + LOOKAHEAD + 1);
   for (;;) {
     if (issued < checked + 1 + LOOKAHEAD) {
       if (issued >= LEVEL_ROUND_CAP) GHS_FAIL(GHS_E_ROUNDCAP, "round cap exceeded in a level");
+      const unsigned long long seq = ++s->res->seq;
+      seqs[issued] = seq;
       if (int rc = enqueue_minedge(s)) return rc;
-      if (int rc = enqueue_contract(s)) return rc;
-      const int nb = s->act_ident ? 0 : (s->act_cur ^ 1);
-      const int slot = issued % SLOT_RING;
-      k_round_report<<<1, 1, 0, s->stream>>>(s->cnt, act_count(s, nb), &s->d_slot[slot].live_out);
-      GHS_HIP_CHECK(hipGetLastError());
-      GHS_HIP_CHECK(hipEventRecord(s->slot_ev[slot], s->stream));
+      if (int rc = enqueue_contract(s, &s->d_slot[issued % SLOT_RING], seq)) return rc;
       advance_round(s);
       ++issued;
       continue;
     }
-    GHS_HIP_CHECK(hipEventSynchronize(s->slot_ev[checked % SLOT_RING]));
-    const RoundSlot r = s->h_slot[checked % SLOT_RING];
+    const RoundSlot *hs = s->h_slot + (checked % SLOT_RING);
+    if (int rc = wait_slot(s, hs, seqs[checked])) return rc;
+    RoundSlot r;
+    r.live_out = hs->live_out;
+    r.nact_out = hs->nact_out;
+    r.edges = hs->edges;
+    r.err = hs->err;
     if (r.err) return fail_counters(s, r.err, ("in round " + std::to_string(round0 + checked + 1)).c_str());
     push_stats(s, checked, live_prev, nact_prev, r.edges);
     // the live edges of round k + 1: round 0 does not compact (its input is read again)
@@ -1636,8 +1721,10 @@ static int run_level_pipelined(ghs_solver *s) {
     ++checked;
     if (r.nact_out == 0) break;  // level complete after round `checked`
   }
-  // rounds issued past the last real one were no-ops: rewind the round counter
+  // rounds issued past the last real one were no-ops: rewind the round counter (their events
+  // are forgotten and re-recorded by the next level)
   s->round = round0 + checked;
+  if (s->ev_rec.size() > s->round) s->ev_rec.resize(s->round);
   close_level(s);
   return GHS_OK;
 }
@@ -1686,6 +1773,7 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   s->eu = d_u; s->ev = d_v; s->ew = d_w;
   s->in_mst = d_in_mst; s->stream = (hipStream_t)stream;
   { const char *dbg = getenv("GHS_DEBUG"); s->debug = dbg && dbg[0] == '1'; }
+  { const char *det = getenv("GHS_DETAIL"); s->detail = det && det[0] == '1'; }
   if (cfg) s->cfg = *cfg; else default_config(&s->cfg);
   workspace_layout(n, e_hi - e_lo, s, (char *)d_workspace);
   hipError_t e;
@@ -1694,20 +1782,19 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
     ghs_solver_destroy(s);
     return GHS_E_HIP;
   };
-  if ((e = hipHostMalloc((void **)&s->h_cnt, C_COUNT * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess)
-    return fail(e, "hipHostMalloc");
-  // round slots: pinned, coherent, written by k_round_report, read by the host after the slot's
-  // event has completed
-  if ((e = hipHostMalloc((void **)&s->h_slot, SLOT_RING * sizeof(RoundSlot), hipHostMallocMapped | hipHostMallocCoherent)) !=
-      hipSuccess)
-    return fail(e, "hipHostMalloc");
-  if ((e = hipHostGetDevicePointer((void **)&s->d_slot, s->h_slot, 0)) != hipSuccess)
-    return fail(e, "hipHostGetDevicePointer");
-  if ((e = hipHostMalloc((void **)&s->h_sample, NSAMPLE_MAX * 4, hipHostMallocDefault)) != hipSuccess)
-    return fail(e, "hipHostMalloc");
-  for (int i = 0; i < SLOT_RING; ++i)
-    if ((e = hipEventCreateWithFlags(&s->slot_ev[i], hipEventDisableTiming)) != hipSuccess)
-      return fail(e, "hipEventCreate");
+  if (g_create_pool) {
+    s->res = g_create_pool;
+  } else {
+    s->res = &s->own;
+    if (int rc = hostres_init(&s->own)) {
+      ghs_solver_destroy(s);
+      return rc;
+    }
+  }
+  s->h_cnt = s->res->h_cnt;
+  s->h_slot = s->res->h_slot;
+  s->d_slot = s->res->d_slot;
+  s->h_sample = s->res->h_sample;
   s->t0 = std::chrono::steady_clock::now();
   if (n) {
     if ((e = hipMemsetAsync(s->best, 0xff, (size_t)n * 8, s->stream)) != hipSuccess) return fail(e, "memset best");
@@ -1815,7 +1902,9 @@ int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *
   const uint32_t ns = (uint32_t)std::min<size_t>(s->stats.size(), GHS_MAX_ROUND_STATS);
   for (uint32_t r = 0; r < ns; ++r) {
     float t[4] = {0, 0, 0, 0};
+    const uint8_t rec = r < s->ev_rec.size() ? s->ev_rec[r] : 0;
     for (int k = 0; k < 4; ++k) {
+      if (((rec >> k) & 3) != 3) continue;  // both ends recorded
       hipEvent_t a = round_event(s, r, k), b = round_event(s, r, k + 1);
       if (a && b) (void)hipEventElapsedTime(&t[k], a, b);
     }
@@ -1838,12 +1927,7 @@ int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *
 
 int ghs_solver_destroy(ghs_solver_t *s) {
   if (!s) return GHS_OK;
-  for (hipEvent_t e : s->ev_pool) (void)hipEventDestroy(e);
-  for (int i = 0; i < SLOT_RING; ++i)
-    if (s->slot_ev[i]) (void)hipEventDestroy(s->slot_ev[i]);
-  if (s->h_cnt) (void)hipHostFree(s->h_cnt);
-  if (s->h_slot) (void)hipHostFree(s->h_slot);
-  if (s->h_sample) (void)hipHostFree(s->h_sample);
+  if (s->res == &s->own) hostres_free(&s->own);
   delete s;
   return GHS_OK;
 }
@@ -1856,7 +1940,12 @@ int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *
   ghs_config_t c;
   if (cfg) c = *cfg; else default_config(&c);
   c.num_ranks = 1;  // one device holds every edge
-  int rc = ghs_solver_create(n, m, d_u, d_v, d_w, 0, m, &c, d_workspace, workspace_bytes, d_in_mst, stream, &s);
+  int rc = GHS_OK;
+  HostRes *pool = pooled_res(&rc);
+  if (!pool) return rc;
+  g_create_pool = pool;
+  rc = ghs_solver_create(n, m, d_u, d_v, d_w, 0, m, &c, d_workspace, workspace_bytes, d_in_mst, stream, &s);
+  g_create_pool = nullptr;
   if (rc) return rc;
   while (!rc && s->phase != 2) {
     if (!s->level_open) {
