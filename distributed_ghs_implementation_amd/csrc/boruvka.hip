@@ -745,21 +745,6 @@ __global__ void k_sample_weights(uint64_t cnt, const uint32_t *__restrict__ w, u
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// Canonical passes: the two full streams over the caller's canonical list [e_lo, e_hi)
-// (u, v, w: 12 B per edge; key = w << 32 | eid built here).
-//  SELECT (opens level 0): validates canonicity (u < v < n, (u, v) strictly ascending) into err
-//    bit 8 — before any kernel indexes an array with these ids — and emits the edges with
-//    w < w_hi into this block's level staging region (every vertex is its own fragment, so the
-//    labels are the endpoints). Nothing else is written: the heavier edges stay where they are.
-//  FILTER (opens level 1): re-streams the list once level 0 is complete and drops, for good,
-//    every edge with w < w_lo (level 0: already decided) and every heavier edge whose ends both
-//    lie in the giant fragment (cycle property: the reference's REJECT for a whole weight class),
-//    tested on a 1-bit membership bitmap (n/8 bytes, resident in each XCD's L2) — no label
-//    gathers. The survivors (u, v, key) go to this block's PENDING region; the later level passes
-//    resolve them against the labels.
-// Block-private output regions: deterministic, no atomics.
-// ------------------------------------------------------------------------------------------
 // Buffer resource over [p, p + bytes) (bytes clipped to 2^31 - 1). Loads past the end return 0
 // instead of faulting, so the streaming loops issue every load unconditionally: no branch around
 // a load, hence no path-dependent outstanding-load count, and hipcc's waits stay counted
@@ -780,32 +765,21 @@ __device__ __forceinline__ uint32_t ld_b32(__amdgpu_buffer_rsrc_t r, uint32_t by
 }
 
 // ------------------------------------------------------------------------------------------
-// Canonical passes: the two full streams over the caller's canonical list [e_lo, e_hi)
+// SELECT (opens level 0): the first full stream over the caller's canonical list [e_lo, e_hi)
 // (u, v, w: 12 B per edge; key = w << 32 | eid built here). The stream runs over the aligned
-// range [E0, e_hi), E0 = e_lo & ~3 (edges below e_lo are masked), so every lane's 4-edge tile
-// is one 16-B load per array.
-//  SELECT (opens level 0): validates canonicity (u < v < n, (u, v) strictly ascending) into err
-//    bit 8 — before any kernel indexes an array with these ids — and emits the edges with
-//    w < w_hi into this block's level staging region (every vertex is its own fragment, so the
-//    labels are the endpoints). Nothing else is written: the heavier edges stay where they are.
-//  FILTER (opens level 1): re-streams the list once level 0 is complete and drops, for good,
-//    every edge with w < w_lo (level 0: already decided) and every heavier edge whose ends both
-//    lie in the giant fragment (cycle property: the reference's REJECT for a whole weight class),
-//    tested on a 1-bit membership bitmap (n/8 bytes, resident in each XCD's L2) — no label
-//    gathers. The survivors (u, v, key) go to this block's PENDING region; the later level passes
-//    resolve them against the labels.
-// Block-private output regions: deterministic, no atomics. Per iteration a lane issues its
-// bitmap probes for the tile in registers, then the next tile's loads, and only then waits for
-// the probes (loads complete in order), so one tile stays in flight across the compaction.
+// range [E0, e_hi), E0 = e_lo & ~3 (edges below e_lo are masked), so every lane's 4-edge tile is
+// one 16-B buffer load per array. Validates canonicity (u < v < n, (u, v) strictly ascending)
+// into err bit 8 — before any kernel indexes an array with these ids — and emits the edges with
+// w < w_hi into this block's level staging region (every vertex is its own fragment, so the
+// labels are the endpoints); single rank: flags both ends active. Nothing else is written: the
+// heavier edges stay where they are until k_filter. Block-private output regions: deterministic,
+// no atomics; the next tile's loads are issued before the current one is compacted.
 // ------------------------------------------------------------------------------------------
-template <bool FILTER>
-GHS_STREAM_KERNEL void k_canon_pass(uint32_t n, uint64_t e_lo, uint64_t e_hi, const uint32_t *__restrict__ eu,
-                                    const uint32_t *__restrict__ ev, const uint32_t *__restrict__ ew, uint64_t w_lo,
-                                    uint64_t w_hi, const uint64_t *__restrict__ giant_bits,
-                                    uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
-                                    uint64_t *__restrict__ okey, uint64_t *__restrict__ ostart,
-                                    uint64_t *__restrict__ ocount, uint8_t *__restrict__ mark,
-                                    unsigned long long *__restrict__ err) {
+GHS_STREAM_KERNEL void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, const uint32_t *__restrict__ eu,
+                                const uint32_t *__restrict__ ev, const uint32_t *__restrict__ ew, uint64_t w_hi,
+                                uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst, uint64_t *__restrict__ okey,
+                                uint64_t *__restrict__ ostart, uint64_t *__restrict__ ocount,
+                                uint8_t *__restrict__ mark, unsigned long long *__restrict__ err) {
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
   __shared__ WaveStage s_stage[BLOCK / WAVE];
   const uint64_t E0 = e_lo & ~3ull;
@@ -818,10 +792,10 @@ GHS_STREAM_KERNEL void k_canon_pass(uint32_t n, uint64_t e_lo, uint64_t e_hi, co
   const __amdgpu_buffer_rsrc_t ru = make_rsrc(eu + eb, nbytes);
   const __amdgpu_buffer_rsrc_t rv = make_rsrc(ev + eb, nbytes);
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(ew + eb, nbytes);
-  // validation: the edge before each lane's tile; offset -4 (the block's first tile) is out of
-  // range of the descriptor and is replaced by the block's predecessor edge, loaded once
+  // the edge before each lane's tile; offset -4 (the block's first tile) is out of range of the
+  // descriptor and is replaced by the block's predecessor edge, loaded once
   uint32_t bpa = 0, bpb = 0;
-  if (!FILTER && eb > 0 && ve > vb) {
+  if (eb > 0 && ve > vb) {
     bpa = eu[eb - 1];
     bpb = ev[eb - 1];
   }
@@ -829,11 +803,7 @@ GHS_STREAM_KERNEL void k_canon_pass(uint32_t n, uint64_t e_lo, uint64_t e_hi, co
   uint64_t nout = 0;
   bool bad = false;
   uint4 ca = ld_b128(ru, lane_off), cb = ld_b128(rv, lane_off), cw = ld_b128(rw, lane_off);
-  uint32_t cpa = 0, cpb = 0;
-  if (!FILTER) {
-    cpa = ld_b32(ru, lane_off - 4);
-    cpb = ld_b32(rv, lane_off - 4);
-  }
+  uint32_t cpa = ld_b32(ru, lane_off - 4), cpb = ld_b32(rv, lane_off - 4);
   for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
     const uint64_t v = v0 + (uint64_t)threadIdx.x * 4;
     const uint64_t e0 = E0 + v;
@@ -841,81 +811,38 @@ GHS_STREAM_KERNEL void k_canon_pass(uint32_t n, uint64_t e_lo, uint64_t e_hi, co
     // lane mask of the tile: edges in [e_lo, ve) (32-bit arithmetic, no branches)
     const uint32_t nv = v < ve ? (uint32_t)((ve - v) < 4 ? (ve - v) : 4) : 0u;
     const uint32_t nskip = e0 < e_lo ? (uint32_t)(e_lo - e0) : 0u;
-    bool live[4];
+    bool live[4], out[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) live[j] = ((uint32_t)j < nv) & ((uint32_t)j >= nskip);
-    bool out[4];
-    uint32_t gbw[4];
-    uint4 q0, q3;
-    uint32_t A0 = 0, A3 = 0;
-    if (FILTER) {
-      // probes, all issued before any is used. a is sorted: two 16-B probes cover the
-      // 128-vertex blocks of a[0] and a[3]; an a[j] outside both (a tile spanning > 2 blocks) is
-      // treated as outside the giant, so its edge is kept — always safe, the later level passes
-      // test it again. b is random: one 32-bit word per edge. Lanes that need no probe read
-      // word 0 (one request per wave instruction).
-      const uint4 *bits4 = reinterpret_cast<const uint4 *>(giant_bits);
-      const uint32_t *bits32 = reinterpret_cast<const uint32_t *>(giant_bits);
-      A0 = a[0] >> 7;
-      A3 = a[3] >> 7;
-      q0 = bits4[live[0] ? A0 : 0u];
-      q3 = bits4[live[3] ? A3 : 0u];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        out[j] = live[j] & ((uint64_t)w[j] >= w_lo);
-        gbw[j] = bits32[out[j] ? (b[j] >> 5) : 0u];
-      }
-    }
     // next tile (out-of-range offsets read 0)
     const uint32_t noff = (uint32_t)(v0 + ARCS_PER_BLOCK - vb) * 4u + lane_off;
     ca = ld_b128(ru, noff);
     cb = ld_b128(rv, noff);
     cw = ld_b128(rw, noff);
-    uint32_t npa = 0, npb = 0;
-    if (!FILTER) {
-      npa = ld_b32(ru, noff - 4);
-      npb = ld_b32(rv, noff - 4);
+    const uint32_t npa = ld_b32(ru, noff - 4), npb = ld_b32(rv, noff - 4);
+    // u < v < n and (u, v) strictly above the previous edge; bitwise (no short-circuit
+    // branches: hipcc turns && / || chains into exec-mask control flow here)
+    uint32_t pa = (v == vb) ? bpa : cpa, pb = (v == vb) ? bpb : cpb;
+    const uint32_t first = (e0 == 0) ? 1u : 0u;  // edge 0 has no predecessor
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t ordered = (j == 0 ? first : 0u) | (uint32_t)(pa < a[j]) | ((uint32_t)(pa == a[j]) & (uint32_t)(pb < b[j]));
+      const uint32_t ok = (uint32_t)(a[j] < b[j]) & (uint32_t)(b[j] < n) & ordered;
+      bad |= live[j] & (ok == 0u);
+      live[j] = live[j] & (ok != 0u);  // never index with an unchecked id
+      pa = a[j];
+      pb = b[j];
+      out[j] = live[j] & ((uint64_t)w[j] < w_hi);
     }
-    if (FILTER) {
-      uint32_t ga[4], gb[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t blk = a[j] >> 7, wsel = (a[j] >> 5) & 3;
-        const uint4 q = (blk == A0) ? q0 : q3;
-        const bool odd = wsel & 1;  // two-level select (an == chain becomes a branch tree)
-        const uint32_t lo = odd ? q.y : q.x, hi = odd ? q.w : q.z;
-        const uint32_t word = (wsel & 2) ? hi : lo;
-        ga[j] = ((blk == A0) | (blk == A3)) ? (word >> (a[j] & 31)) & 1u : 0u;
-        gb[j] = (gbw[j] >> (b[j] & 31)) & 1u;
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        out[j] = out[j] & ((ga[j] & gb[j]) == 0u);  // bitwise (no && : keeps the probes unsunk)
-    } else {
-      // u < v < n and (u, v) strictly above the previous edge; bitwise (no short-circuit
-      // branches: hipcc turns && / || chains into exec-mask control flow here)
-      uint32_t pa = (v == vb) ? bpa : cpa, pb = (v == vb) ? bpb : cpb;
-      const uint32_t first = (e0 == 0) ? 1u : 0u;  // edge 0 has no predecessor
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t ordered = (j == 0 ? first : 0u) | (uint32_t)(pa < a[j]) | ((uint32_t)(pa == a[j]) & (uint32_t)(pb < b[j]));
-        const uint32_t ok = (uint32_t)(a[j] < b[j]) & (uint32_t)(b[j] < n) & ordered;
-        bad |= live[j] & (ok == 0u);
-        live[j] = live[j] & (ok != 0u);  // never index with an unchecked id
-        pa = a[j];
-        pb = b[j];
-        out[j] = live[j] & ((uint64_t)w[j] < w_hi);
-      }
-      cpa = npa;
-      cpb = npb;
-    }
+    cpa = npa;
+    cpb = npb;
     uint32_t omask = 0;
     uint64_t key[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       omask |= out[j] ? (1u << j) : 0u;
       key[j] = ((uint64_t)w[j] << 32) | (uint32_t)(e0 + j);
-      if (!FILTER && mark && out[j]) {  // active fragments of the level (single rank)
+      if (mark && out[j]) {  // active fragments of the level (single rank)
         mark[a[j]] = 1;
         mark[b[j]] = 1;
       }
@@ -925,7 +852,7 @@ GHS_STREAM_KERNEL void k_canon_pass(uint32_t n, uint64_t e_lo, uint64_t e_hi, co
     stage_write(s_stage[threadIdx.x / WAVE], a, b, key, omask, le, wc, osrc, odst, okey, vb + nout + wb);
     nout += tot;
   }
-  if (!FILTER && bad) atomicOr(err, 8ull);
+  if (bad) atomicOr(err, 8ull);
   // output regions are padded to a multiple of 4 with dead entries (a = LABEL_NONE)
   const uint64_t padded = (nout + 3) & ~3ull;
   if (threadIdx.x < padded - nout) {
@@ -935,6 +862,136 @@ GHS_STREAM_KERNEL void k_canon_pass(uint32_t n, uint64_t e_lo, uint64_t e_hi, co
     okey[pos] = KEY_NONE;
   }
   if (threadIdx.x == 0) {
+    ostart[blockIdx.x] = vb;
+    ocount[blockIdx.x] = (vb < T) ? padded : 0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// FILTER + level split (opens level 1): re-streams the canonical list once level 0 is complete.
+//  - w < w_lo: level 0, already decided -> dropped;
+//  - both ends in the giant fragment (1-bit bitmap, resident in each XCD's L2) -> dropped for
+//    good (cycle property: the reference's REJECT for a whole weight class);
+//  - w < w_hi: a level-1 edge: its labels are gathered (the only gathers of the pass), and if
+//    they differ it goes to this block's region of the level staging (lab[u], lab[v], key) and
+//    both fragments are flagged active (mark, single rank);
+//  - otherwise: pending (u, v, key) for the later levels, tested there against their labels.
+// The b-probes are ~1 L2 request per heavy edge and do not overlap the stream (measured: they
+// add), so the pass costs stream + probes; splitting level 1 here saves a pass over the pending
+// edges.
+// ------------------------------------------------------------------------------------------
+GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__restrict__ eu,
+                                const uint32_t *__restrict__ ev, const uint32_t *__restrict__ ew, uint64_t w_lo,
+                                uint64_t w_hi, const uint64_t *__restrict__ giant_bits,
+                                const uint32_t *__restrict__ lab, uint32_t *__restrict__ lsrc,
+                                uint32_t *__restrict__ ldst, uint64_t *__restrict__ lkey,
+                                uint64_t *__restrict__ lstart, uint64_t *__restrict__ lcount,
+                                uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
+                                uint64_t *__restrict__ okey, uint64_t *__restrict__ ostart,
+                                uint64_t *__restrict__ ocount, uint8_t *__restrict__ mark) {
+  __shared__ uint32_t s_wcnt[BLOCK / WAVE];
+  __shared__ WaveStage s_stage[BLOCK / WAVE];
+  const uint64_t E0 = e_lo & ~3ull;
+  const uint64_t T = e_hi - E0;
+  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
+  const uint64_t vb = Q * blockIdx.x;
+  const uint64_t ve = (vb + Q < T) ? vb + Q : T;
+  const uint64_t eb = E0 + vb;  // first edge of this block
+  const uint64_t nbytes = ve > vb ? (ve - vb) * 4 : 0;
+  const __amdgpu_buffer_rsrc_t ru = make_rsrc(eu + eb, nbytes);
+  const __amdgpu_buffer_rsrc_t rv = make_rsrc(ev + eb, nbytes);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(ew + eb, nbytes);
+  const uint32_t lane_off = threadIdx.x * 16u;
+  const uint4 *bits4 = reinterpret_cast<const uint4 *>(giant_bits);
+  const uint32_t *bits32 = reinterpret_cast<const uint32_t *>(giant_bits);
+  uint64_t nlev = 0, nrem = 0;
+  uint4 ca = ld_b128(ru, lane_off), cb = ld_b128(rv, lane_off), cw = ld_b128(rw, lane_off);
+  for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
+    const uint64_t v = v0 + (uint64_t)threadIdx.x * 4;
+    const uint64_t e0 = E0 + v;
+    const uint32_t a[4] = {ca.x, ca.y, ca.z, ca.w}, b[4] = {cb.x, cb.y, cb.z, cb.w}, w[4] = {cw.x, cw.y, cw.z, cw.w};
+    const uint32_t nv = v < ve ? (uint32_t)((ve - v) < 4 ? (ve - v) : 4) : 0u;
+    const uint32_t nskip = e0 < e_lo ? (uint32_t)(e_lo - e0) : 0u;
+    bool out[4];
+    // probes, all issued before any is used. a is sorted: two 16-B probes cover the 128-vertex
+    // blocks of a[0] and a[3]; an a[j] outside both (a tile spanning > 2 blocks) counts as
+    // outside the giant, so its edge is kept — always safe. b is random: one 32-bit word per
+    // edge. Lanes that need no probe read word 0 (one request per wave instruction).
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[j] = ((uint32_t)j < nv) & ((uint32_t)j >= nskip) & ((uint64_t)w[j] >= w_lo);
+    // block indices and probed words from the same guard (an unguarded lane probes block 0 and
+    // says so): an in-range a is a checked vertex id; a masked one may not be
+    const bool in0 = ((uint32_t)0 < nv) & (0u >= nskip), in3 = (3u < nv) & (3u >= nskip);
+    const uint32_t A0 = in0 ? (a[0] >> 7) : 0u, A3 = in3 ? (a[3] >> 7) : 0u;
+    const uint4 q0 = bits4[A0];
+    const uint4 q3 = bits4[A3];
+    uint32_t gbw[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gbw[j] = bits32[out[j] ? (b[j] >> 5) : 0u];
+    // next tile (out-of-range offsets read 0)
+    const uint32_t noff = (uint32_t)(v0 + ARCS_PER_BLOCK - vb) * 4u + lane_off;
+    ca = ld_b128(ru, noff);
+    cb = ld_b128(rv, noff);
+    cw = ld_b128(rw, noff);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t blk = a[j] >> 7, wsel = (a[j] >> 5) & 3;
+      const uint4 q = (blk == A0) ? q0 : q3;
+      const bool odd = wsel & 1;  // two-level select (an == chain becomes a branch tree)
+      const uint32_t lo = odd ? q.y : q.x, hi = odd ? q.w : q.z;
+      const uint32_t word = (wsel & 2) ? hi : lo;
+      const uint32_t ga = ((blk == A0) | (blk == A3)) ? (word >> (a[j] & 31)) & 1u : 0u;
+      const uint32_t gb = (gbw[j] >> (b[j] & 31)) & 1u;
+      out[j] = out[j] & ((ga & gb) == 0u);  // bitwise (no && : keeps the probes unsunk)
+    }
+    // level-1 split: labels only for this level's edges
+    bool lev[4], rem[4];
+    uint32_t la[4], lb[4];
+    uint64_t key[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      lev[j] = out[j] & ((uint64_t)w[j] < w_hi);
+      rem[j] = out[j] & !lev[j];
+      la[j] = lab[lev[j] ? a[j] : 0u];
+      lb[j] = lab[lev[j] ? b[j] : 0u];
+      key[j] = ((uint64_t)w[j] << 32) | (uint32_t)(e0 + j);
+    }
+    uint32_t lmask = 0, rmask = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      lev[j] = lev[j] & (la[j] != lb[j]);
+      lmask |= lev[j] ? (1u << j) : 0u;
+      rmask |= rem[j] ? (1u << j) : 0u;
+      if (lev[j] && mark) {  // active fragments of the level (single rank)
+        mark[la[j]] = 1;
+        mark[lb[j]] = 1;
+      }
+    }
+    uint32_t le, wb, wc, tlev, trem;
+    block_offsets_w((uint32_t)__popc(lmask), s_wcnt, &le, &wb, &wc, &tlev);
+    stage_write(s_stage[threadIdx.x / WAVE], la, lb, key, lmask, le, wc, lsrc, ldst, lkey, vb + nlev + wb);
+    block_offsets_w((uint32_t)__popc(rmask), s_wcnt, &le, &wb, &wc, &trem);
+    stage_write(s_stage[threadIdx.x / WAVE], a, b, key, rmask, le, wc, osrc, odst, okey, vb + nrem + wb);
+    nlev += tlev;
+    nrem += trem;
+  }
+  // both outputs padded to a multiple of 4 with dead entries (a = LABEL_NONE)
+  const uint64_t padded = (nrem + 3) & ~3ull, lpadded = (nlev + 3) & ~3ull;
+  if (threadIdx.x < padded - nrem) {
+    const uint64_t pos = vb + nrem + threadIdx.x;
+    osrc[pos] = LABEL_NONE;
+    odst[pos] = 0;
+    okey[pos] = KEY_NONE;
+  }
+  if (threadIdx.x < lpadded - nlev) {
+    const uint64_t pos = vb + nlev + threadIdx.x;
+    lsrc[pos] = LABEL_NONE;
+    ldst[pos] = 0;
+    lkey[pos] = KEY_NONE;
+  }
+  if (threadIdx.x == 0) {
+    lstart[blockIdx.x] = vb;
+    lcount[blockIdx.x] = (vb < T) ? lpadded : 0;
     ostart[blockIdx.x] = vb;
     ocount[blockIdx.x] = (vb < T) ? padded : 0;
   }
@@ -995,9 +1052,10 @@ GHS_STREAM_KERNEL void k_level_pass(const uint32_t *__restrict__ ru, const uint3
     // giant-bitmap probes (a sorted within a region: two 16-B probes cover a[0]'s and a[3]'s
     // 128-vertex blocks; an a[j] outside both counts as outside the giant — safe), issued
     // before the next tile's loads
-    const uint32_t A0 = a[0] >> 7, A3 = a[3] >> 7;
-    const uint4 q0 = bits4[live[0] ? A0 : 0u];
-    const uint4 q3 = bits4[live[3] ? A3 : 0u];
+    // block indices and probed words from the same guard (a dead entry has a == LABEL_NONE)
+    const uint32_t A0 = live[0] ? (a[0] >> 7) : 0u, A3 = live[3] ? (a[3] >> 7) : 0u;
+    const uint4 q0 = bits4[A0];
+    const uint4 q3 = bits4[A3];
     uint32_t gbw[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) gbw[j] = bits32[live[j] ? (b[j] >> 5) : 0u];
@@ -1498,8 +1556,8 @@ static int open_level(ghs_solver *s) {
     // SELECT over the canonical list: level-0 edges only (validates the list)
     G = grid_for(TC, ARCS_PER_BLOCK, SEG_G);
     if (TC) {
-      k_canon_pass<false><<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, 0, w_hi, nullptr, Y.src,
-                                               Y.dst, Y.key, Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR);
+      k_select<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, w_hi, Y.src, Y.dst, Y.key,
+                                    Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR);
       GHS_HIP_CHECK(hipGetLastError());
       k_scan_counts<<<1, 1024, 0, st>>>(Y.seg_count, G, Y.seg_prefix, s->cnt + C_LIVE);
     } else {
@@ -1511,32 +1569,37 @@ static int open_level(ghs_solver *s) {
     const int rin = s->rcur, rout = s->rcur ^ 1;
     ArcBuf &RI = s->rem[rin], &RO = s->rem[rout];
     if (!s->pending_built) {
-      // FILTER over the canonical list once level 0 is complete: every heavier edge not inside
-      // the giant fragment becomes pending (regions of rem[rin])
-      const unsigned GC = grid_for(TC, ARCS_PER_BLOCK, SEG_G);
+      // FILTER + level split over the canonical list once level 0 is complete: level-1 edges
+      // not inside one fragment -> Y; heavier edges not inside the giant -> pending (rem[rout])
+      G = grid_for(TC, ARCS_PER_BLOCK, SEG_G);
       if (TC) {
-        k_canon_pass<true><<<GC, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, s->thresholds[lv], 0,
-                                                 s->bits, RI.src, RI.dst, RI.key, RI.seg_start, RI.seg_count, nullptr,
-                                                 s->cnt + C_ERR);
+        k_filter<<<G, BLOCK, 0, st>>>(s->e_lo, s->e_hi, s->eu, s->ev, s->ew, s->thresholds[lv], w_hi, s->bits, s->lab,
+                                      Y.src, Y.dst, Y.key, Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key,
+                                      RO.seg_start, RO.seg_count, mark);
         GHS_HIP_CHECK(hipGetLastError());
-        k_scan_counts<<<1, 1024, 0, st>>>(RI.seg_count, GC, RI.seg_prefix, s->cnt + C_PENDING);
+        k_scan_counts<<<1, 1024, 0, st>>>(RO.seg_count, G, RO.seg_prefix, s->cnt + C_PENDING);
+        k_scan_counts<<<1, 1024, 0, st>>>(Y.seg_count, G, Y.seg_prefix, s->cnt + C_LIVE);
       } else {
-        GHS_HIP_CHECK(hipMemsetAsync(RI.seg_prefix, 0, 16, st));
+        GHS_HIP_CHECK(hipMemsetAsync(RO.seg_prefix, 0, 16, st));
+        GHS_HIP_CHECK(hipMemsetAsync(Y.seg_prefix, 0, 16, st));
+        GHS_HIP_CHECK(hipMemsetAsync(s->cnt + C_LIVE, 0, 8, st));
+        GHS_HIP_CHECK(hipMemsetAsync(s->cnt + C_PENDING, 0, 8, st));
       }
-      s->rem_nseg = GC;
+      GHS_HIP_CHECK(hipGetLastError());
       s->pending_built = true;
+    } else {
+      // split the pending edges (total on the device): this level's inter-fragment edges -> Y;
+      // heavier survivors -> RO regions. Fixed grid: block b owns 1/SEG_G of the virtual range.
+      G = SEG_G;
+      SegView in{RI.seg_start, RI.seg_prefix, s->rem_nseg};
+      k_level_pass<<<G, BLOCK, 0, st>>>(RI.src, RI.dst, RI.key, in, w_hi, s->lab, s->bits, Y.src, Y.dst, Y.key,
+                                        Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key, RO.seg_start, RO.seg_count,
+                                        mark);
+      GHS_HIP_CHECK(hipGetLastError());
+      k_scan_counts<<<1, 1024, 0, st>>>(RO.seg_count, G, RO.seg_prefix, s->cnt + C_PENDING);
+      k_scan_counts<<<1, 1024, 0, st>>>(Y.seg_count, G, Y.seg_prefix, s->cnt + C_LIVE);
+      GHS_HIP_CHECK(hipGetLastError());
     }
-    // split the pending edges (total on the device): this level's inter-fragment edges -> Y;
-    // heavier survivors -> RO regions. Fixed grid: block b owns 1/SEG_G of the virtual range.
-    G = SEG_G;
-    SegView in{RI.seg_start, RI.seg_prefix, s->rem_nseg};
-    k_level_pass<<<G, BLOCK, 0, st>>>(RI.src, RI.dst, RI.key, in, w_hi, s->lab, s->bits, Y.src, Y.dst, Y.key,
-                                      Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key, RO.seg_start, RO.seg_count,
-                                      mark);
-    GHS_HIP_CHECK(hipGetLastError());
-    k_scan_counts<<<1, 1024, 0, st>>>(RO.seg_count, G, RO.seg_prefix, s->cnt + C_PENDING);
-    k_scan_counts<<<1, 1024, 0, st>>>(Y.seg_count, G, Y.seg_prefix, s->cnt + C_LIVE);
-    GHS_HIP_CHECK(hipGetLastError());
     s->rem_nseg = G;
     s->rcur = rout;
   }

@@ -42,6 +42,14 @@ __global__ __launch_bounds__(256) void k(const uint32_t *__restrict__ a, const u
   out[blockIdx.x * 256 + threadIdx.x] = acc;
 }
 
+__global__ void k_fill(uint32_t *b, uint64_t M) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < M; i += 256ull * gridDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u;
+    h ^= h >> 15; h *= 0x2c1b3c6du; h ^= h >> 12;
+    b[i] = h;
+  }
+}
+
 int main() {
   const uint64_t M = 260000000ull;
   const uint32_t nwords = (1u << 24) / 32;  // 16.8M vertices -> 2 MiB
@@ -49,7 +57,8 @@ int main() {
   CK(hipMalloc(&a, M * 4)); CK(hipMalloc(&b, M * 4)); CK(hipMalloc(&c, M * 4));
   CK(hipMalloc(&o, 1 << 26)); CK(hipMalloc(&bits, nwords * 4));
   CK(hipMemset(a, 1, M * 4)); CK(hipMemset(b, 7, M * 4)); CK(hipMemset(c, 3, M * 4)); CK(hipMemset(bits, 0x55, nwords * 4));
-  // b must hold varied values for random probes: fill with a hash
+  k_fill<<<8192, 256>>>(b, M);  // b holds random values: random probe indices
+  CK(hipDeviceSynchronize());
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const char *names[4] = {"probe", "stream", "both", "both_nt"};
   for (int grid : {2048, 8192}) {
