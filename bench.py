@@ -10,14 +10,16 @@ N>1 (torch.distributed.run, one rank per GPU, RCCL all-reduce MIN per round): ev
 the replicated canonical list and scans the arcs of its source-vertex range; scale
 min(26, 24 + log2 N) (config 4: s26 on 8 GPUs).
 
-Rank 0 prints ONE JSON line. `roofline` is for the dominant kernel (the relabel+compact
-min-edge kernel, k_minedge<false,true>): achieved = algorithmic bytes per launch / average
-launch duration, both from HIP events recorded by libghs_mst.so on the launch stream during the
-timed steps; algorithmic bytes per live arc = 24 (src 4 + dst 4 + key 8 + lab[src] 4 +
-lab[dst] 4) + 16 per surviving (written) arc. `traffic` comes from the committed PMC profile
-(profiles/*_pmc.json, rocprofv3 FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected) when one exists
-for this workload, else null. `cpu_baseline` = the oracle's C Kruskal (kind "port", 1 thread)
-on a bounded sample (R-MAT of a smaller scale, same generator), rank 0 at N=1 only.
+Rank 0 prints ONE JSON line. `roofline` is for the dominant kernel of the step (largest
+time over the timed steps) among the instrumented ones: k_filter (canonical stream + giant-bitmap
+filter + level-1 split; 12 B per canonical edge read + 16 B per entry written), k_select
+(validation + level-0 split; same accounting) and the compacting min-edge kernel (24 B per live
+edge + 16 B per survivor). Durations are HIP events recorded by libghs_mst.so on the launch
+stream inside the timed steps; all three are listed under "kernels". `traffic` comes from the
+committed PMC profile (profiles/**/<workload>_pmc.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes,
+gfx950-corrected, tools/gpu/pmc_traffic.sh) when one exists for this workload, else null.
+`cpu_baseline` = the oracle's C Kruskal (kind "port", 1 thread) on a bounded sample (R-MAT of a
+smaller scale, same generator), rank 0 at N=1 only.
 """
 import argparse
 import glob
@@ -51,15 +53,16 @@ def parse():
 
 
 def minedge_roofline(all_stats):
-    """Dominant kernel = min-edge with relabel + compaction (rounds >= 2). Returns
-    (achieved GB/s, bytes per launch, avg ms per launch, launches)."""
+    """The compacting min-edge kernel (rounds >= 2 of a level; SURVEY.md 8(d) stage 1): 24 B per
+    live edge read (a 4 + b 4 + key 8 + lab[a] 4 + lab[b] 4) + 16 B per surviving edge written.
+    Returns (achieved GB/s, bytes per launch, avg ms per launch, launches) or None."""
     tot_bytes = 0.0
     tot_ms = 0.0
     launches = 0
     for stats in all_stats:
         for r, st in enumerate(stats):
             first_of_level = r == 0 or stats[r - 1]["level"] != st["level"]
-            if first_of_level or st["live_arcs"] == 0:
+            if first_of_level or st["live_arcs"] == 0 or st["ms_minedge"] <= 0:
                 continue
             nxt = stats[r + 1] if r + 1 < len(stats) else None
             survivors = nxt["live_arcs"] if nxt is not None and nxt["level"] == st["level"] else 0
@@ -71,18 +74,42 @@ def minedge_roofline(all_stats):
     return tot_bytes / (tot_ms * 1e-3) / 1e9, tot_bytes / launches, tot_ms / launches, launches
 
 
-def load_traffic(workload_tag):
-    """Per-launch HBM bytes of k_minedge<false,true> from a committed PMC profile, if any."""
+def pass_roofline(results, which):
+    """A canonical pass (one launch per step): 12 B per canonical edge streamed (u, v, w) + 16 B
+    per entry written. k_filter's bitmap probes hit the L2-resident bitmap and are not HBM bytes.
+    Returns (achieved GB/s, bytes per launch, avg ms per launch, launches) or None."""
+    ms = [getattr(r, "ms_" + which) for r in results]
+    out = [getattr(r, which + "_out") for r in results]
+    if not ms or min(ms) <= 0:
+        return None
+    bpl = 12.0 * results[0].canon_edges + 16.0 * out[0]
+    avg = sum(ms) / len(ms)
+    return bpl / (avg * 1e-3) / 1e9, bpl, avg, len(ms)
+
+
+def load_traffic(workload_tag, kernel):
+    """Per-launch HBM bytes of `kernel` from a committed PMC profile (profiles/**/*_pmc.json)."""
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json"))):
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*_pmc.json"), recursive=True)):
         try:
             d = json.load(open(p))
         except Exception:
             continue
-        if d.get("workload") == workload_tag and d.get("kernel_traffic_bytes_per_launch"):
-            d["_path"] = p
-            best = d
+        k = d.get("kernels", {}).get(kernel)
+        if d.get("workload") == workload_tag and k and k.get("traffic_bytes_per_launch"):
+            best = dict(k, _path=os.path.relpath(p, ROOT))
     return best
+
+
+def roofline_obj(roof, kernel, tag, note):
+    ach, bpl, msl, launches = roof
+    traffic = load_traffic(tag, kernel)
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": (round(traffic["traffic_bytes_per_launch"]) if traffic else None),
+            "kernel": kernel, "note": note, "algorithmic_bytes_per_launch": round(bpl),
+            "avg_launch_ms": round(msl, 4), "launches": launches,
+            "traffic_source": traffic["_path"] if traffic else None}
 
 
 def cpu_baseline(scale, edgefactor):
@@ -154,10 +181,12 @@ def main():
     t0 = time.perf_counter()
     all_stats = []
     results = []
+    raw_results = []
     for _ in range(args.steps):
         res, stats = step()
         all_stats.append(stats)
         results.append((res.total_weight, res.num_mst_edges, res.rounds, res.ms_total, res.levels))
+        raw_results.append(res)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -169,23 +198,28 @@ def main():
     if len(set((r[0], r[1]) for r in results)) != 1:
         raise RuntimeError("non-deterministic MST across steps")
 
-    roof = minedge_roofline(all_stats)
+    roof_me = minedge_roofline(all_stats)
+    roof_f = pass_roofline(raw_results, "filter")
+    roof_s = pass_roofline(raw_results, "select")
     line = None
     if rank == 0:
         ms_per_step = dt * 1e3 / args.steps
         value = m * args.steps / dt
-        roofline = None
-        if roof:
-            ach, bpl, msl, launches = roof
-            traffic = load_traffic(tag)
-            roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(ach / HBM_PEAK_GBS, 4),
-                        "traffic": (traffic["kernel_traffic_bytes_per_launch"] if traffic else None),
-                        "kernel": "k_minedge<false,true> (relabel + min-edge + compaction, rounds >= 2)",
-                        "algorithmic_bytes_per_launch": round(bpl), "avg_launch_ms": round(msl, 4),
-                        "launches": launches,
-                        "traffic_source": (os.path.relpath(traffic["_path"], ROOT) if traffic and "_path" in traffic
-                                           else (traffic.get("source") if traffic else None))}
+        kernels = {}
+        if roof_f:
+            kernels["k_filter"] = roofline_obj(
+                roof_f, "k_filter", tag, "dominant kernel of the step: canonical stream (12 B/edge) + giant-bitmap "
+                "probe per heavy edge (L2-request bound, DESIGN.md) + level-1/pending writes (16 B/entry)")
+        if roof_s:
+            kernels["k_select"] = roofline_obj(roof_s, "k_select", tag,
+                                               "canonical stream + validation + level-0 split")
+        if roof_me:
+            kernels["k_minedge"] = roofline_obj(
+                roof_me, "k_minedge<false, true>", tag, "min-edge with relabel + compaction, rounds >= 2 "
+                "(SURVEY 8(d) stage 1: 24 B per live edge + 16 B per survivor)")
+        # the roofline object is the dominant kernel's (largest time per step)
+        dom = max(kernels.values(), key=lambda k: k["avg_launch_ms"] * k["launches"]) if kernels else None
+        roofline = dom
         s0 = all_stats[-1]
         breakdown = {
             "rounds": results[-1][2],
@@ -203,7 +237,7 @@ def main():
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
                 "data": "synthetic (generated on GPU)", "config": cfg, "roofline": roofline,
-                "cpu_baseline": cpu, "mst": {"total_weight": results[-1][0], "edges": results[-1][1]},
+                "cpu_baseline": cpu, "kernels": kernels, "mst": {"total_weight": results[-1][0], "edges": results[-1][1]},
                 "breakdown": breakdown}
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -66,6 +66,9 @@ class RoundStats(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
 
 
+ABI_VERSION = 2  # include/ghs_mst.h GHS_MST_ABI_VERSION
+
+
 class Result(ctypes.Structure):
     _fields_ = [
         ("num_mst_edges", ctypes.c_uint64),
@@ -75,6 +78,11 @@ class Result(ctypes.Structure):
         ("levels", ctypes.c_uint32),
         ("reserved", ctypes.c_uint32),
         ("ms_total", ctypes.c_double),
+        ("ms_select", ctypes.c_float),
+        ("ms_filter", ctypes.c_float),
+        ("canon_edges", ctypes.c_uint64),
+        ("select_out", ctypes.c_uint64),
+        ("filter_out", ctypes.c_uint64),
     ]
 
 
@@ -154,8 +162,8 @@ def load():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.ghs_abi_version() != 1:
-            raise ImportError(f"libghs_mst.so ABI {L.ghs_abi_version()} != 1")
+        if L.ghs_abi_version() != ABI_VERSION:
+            raise ImportError(f"libghs_mst.so ABI {L.ghs_abi_version()} != {ABI_VERSION}")
         _lib = L
         return _lib
 

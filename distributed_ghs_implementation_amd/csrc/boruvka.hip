@@ -1298,6 +1298,7 @@ struct HostRes {
   RoundSlot *d_slot = nullptr;          // the same ring, device view
   uint32_t *h_sample = nullptr;         // pinned sample buffer
   std::vector<hipEvent_t> ev_pool;      // timing events, 6 per round
+  hipEvent_t pass_ev[4] = {};           // the canonical passes' events
   unsigned long long seq = 0;           // round reports issued through h_slot (monotonic across solves)
 };
 
@@ -1307,6 +1308,7 @@ static int hostres_init(HostRes *r) {
   GHS_HIP_CHECK(hipHostMalloc((void **)&r->h_slot, SLOT_RING * sizeof(RoundSlot), hipHostMallocMapped | hipHostMallocCoherent));
   GHS_HIP_CHECK(hipHostGetDevicePointer((void **)&r->d_slot, r->h_slot, 0));
   GHS_HIP_CHECK(hipHostMalloc((void **)&r->h_sample, 16384 * 4, hipHostMallocDefault));
+  for (int i = 0; i < 4; ++i) GHS_HIP_CHECK(hipEventCreate(&r->pass_ev[i]));
   memset(r->h_slot, 0, SLOT_RING * sizeof(RoundSlot));
   return GHS_OK;
 }
@@ -1314,6 +1316,8 @@ static int hostres_init(HostRes *r) {
 static void hostres_free(HostRes *r) {
   for (hipEvent_t e : r->ev_pool) (void)hipEventDestroy(e);
   r->ev_pool.clear();
+  for (int i = 0; i < 4; ++i)
+    if (r->pass_ev[i]) (void)hipEventDestroy(r->pass_ev[i]);
   if (r->h_cnt) (void)hipHostFree(r->h_cnt);
   if (r->h_slot) (void)hipHostFree(r->h_slot);
   if (r->h_sample) (void)hipHostFree(r->h_sample);
@@ -1373,6 +1377,9 @@ struct ghs_solver {
 
   std::vector<ghs_round_stats_t> stats;
   std::vector<uint8_t> ev_rec;  // per round: bit k = event k recorded
+  hipEvent_t pass_ev[4] = {};   // around k_select [0,1] and k_filter [2,3] (from the host pool)
+  bool filter_run = false;
+  uint64_t select_out = 0, filter_out = 0;
   bool detail = false;          // GHS_DETAIL=1: time every stage (adds ~5.7 us per event)
   std::chrono::steady_clock::time_point t0;
 };
@@ -1556,8 +1563,10 @@ static int open_level(ghs_solver *s) {
     // SELECT over the canonical list: level-0 edges only (validates the list)
     G = grid_for(TC, ARCS_PER_BLOCK, SEG_G);
     if (TC) {
+      GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[0], st));
       k_select<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, w_hi, Y.src, Y.dst, Y.key,
                                     Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR);
+      GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[1], st));
       GHS_HIP_CHECK(hipGetLastError());
       k_scan_counts<<<1, 1024, 0, st>>>(Y.seg_count, G, Y.seg_prefix, s->cnt + C_LIVE);
     } else {
@@ -1573,10 +1582,13 @@ static int open_level(ghs_solver *s) {
       // not inside one fragment -> Y; heavier edges not inside the giant -> pending (rem[rout])
       G = grid_for(TC, ARCS_PER_BLOCK, SEG_G);
       if (TC) {
+        GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[2], st));
         k_filter<<<G, BLOCK, 0, st>>>(s->e_lo, s->e_hi, s->eu, s->ev, s->ew, s->thresholds[lv], w_hi, s->bits, s->lab,
                                       Y.src, Y.dst, Y.key, Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key,
                                       RO.seg_start, RO.seg_count, mark);
         GHS_HIP_CHECK(hipGetLastError());
+        GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[3], st));
+        s->filter_run = true;
         k_scan_counts<<<1, 1024, 0, st>>>(RO.seg_count, G, RO.seg_prefix, s->cnt + C_PENDING);
         k_scan_counts<<<1, 1024, 0, st>>>(Y.seg_count, G, Y.seg_prefix, s->cnt + C_LIVE);
       } else {
@@ -1619,6 +1631,8 @@ static int open_level(ghs_solver *s) {
   if (s->h_cnt[C_ERR]) return fail_counters(s, s->h_cnt[C_ERR], "opening a level");
   const uint64_t S = s->h_cnt[C_LIVE];
   s->rem_total = s->h_cnt[C_PENDING];
+  if (first) s->select_out = S;
+  else if (s->filter_run && !s->filter_out) s->filter_out = S + s->rem_total;
   s->nact = s->act_ident ? s->n : s->h_cnt[C_ACT];
   if (s->debug) {
     uint32_t g[2] = {0, 0};
@@ -1984,6 +1998,13 @@ int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *
     result->num_stats = ns;
     result->levels = (uint32_t)(s->thresholds.size() - 1);
     result->ms_total = ms;
+    float t = 0;
+    result->ms_select = (s->e_hi > s->e_lo && hipEventElapsedTime(&t, s->res->pass_ev[0], s->res->pass_ev[1]) == hipSuccess) ? t : 0.f;
+    t = 0;
+    result->ms_filter = (s->filter_run && hipEventElapsedTime(&t, s->res->pass_ev[2], s->res->pass_ev[3]) == hipSuccess) ? t : 0.f;
+    result->canon_edges = s->e_hi - s->e_lo;
+    result->select_out = s->select_out;
+    result->filter_out = s->filter_out;
   }
   return GHS_OK;
 }

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GHS_MST_ABI_VERSION 1
+#define GHS_MST_ABI_VERSION 2
 
 #define GHS_OK 0
 #define GHS_E_ARG (-1)        /* bad argument (null pointer, size, alignment) */
@@ -66,6 +66,12 @@ typedef struct ghs_result {
   uint32_t levels;            /* weight levels planned */
   uint32_t reserved;
   double ms_total;            /* host wall time of the solve (device-resident input -> flags) */
+  /* The two full streams over the canonical list (HIP events on the solve's stream). */
+  float ms_select;            /* k_select: validation + level-0 split */
+  float ms_filter;            /* k_filter: giant-bitmap filter + level-1 split (0 if not run) */
+  uint64_t canon_edges;       /* canonical edges each pass streams (the solver's range) */
+  uint64_t select_out;        /* entries k_select wrote (level-0 edges, incl. region padding) */
+  uint64_t filter_out;        /* entries k_filter wrote (level-1 + pending edges, incl. padding) */
 } ghs_result_t;
 
 /* Weight-level plan of the filter. Level 1 holds roughly the
