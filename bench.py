@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check the result against the oracle (slow at s24)")
     ap.add_argument("--stats", action="store_true", help="print per-round stats to stderr")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse ranks sharing a GPU)")
+    ap.add_argument("--verify-ranks", action="store_true", help="N>1: check every rank holds the same MSF")
     return ap.parse_args()
 
 
@@ -144,9 +147,9 @@ def main():
         if world == 1 and args.gpus > 1:
             print("run N>1 under torch.distributed.run (one rank per GPU)", file=sys.stderr)
             return 2
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if world > 1:
-        dist.init_process_group("nccl")
+        dist.init_process_group(args.backend)
 
     from distributed_ghs_implementation_amd.device import DeviceMST, generate_grid, generate_rmat
     from distributed_ghs_implementation_amd.distributed import DistributedMST
@@ -197,6 +200,19 @@ def main():
         dt = float(t.item())
     if len(set((r[0], r[1]) for r in results)) != 1:
         raise RuntimeError("non-deterministic MST across steps")
+    if world > 1 and args.verify_ranks:
+        # every rank must hold the same MSF: (weight, edges, checksum of the chosen eids)
+        flags = eng.engine.in_mst[:m]
+        chk = int((torch.nonzero(flags).flatten().to(torch.int64) % 1000003).sum().item())
+        mine = torch.tensor([results[-1][0], results[-1][1], chk], dtype=torch.int64)
+        if args.backend == "nccl":
+            mine = mine.cuda()
+        allv = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        if any(not torch.equal(a.cpu(), allv[0].cpu()) for a in allv):
+            raise RuntimeError(f"ranks disagree on the MSF: {[a.tolist() for a in allv]}")
+        if rank == 0:
+            print(f"ranks agree: weight {results[-1][0]} edges {results[-1][1]} eid checksum {chk}", file=sys.stderr)
 
     roof_me = minedge_roofline(all_stats)
     roof_f = pass_roofline(raw_results, "filter")

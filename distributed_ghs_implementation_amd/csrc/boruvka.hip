@@ -1497,7 +1497,7 @@ static void default_config(ghs_config_t *c) {
   c->max_levels = 8;
   c->num_ranks = 1;
   c->level1_edges_per_vertex = 0.5;
-  c->level_growth = 4.0;
+  c->level_growth = 8.0;  // R-MAT s24 sweep (tools/sweep_levels.py): 3 levels, 0.5n / 4n / rest
 }
 
 // ---- level planning: thresholds from a sample of the GLOBAL canonical weights ----------------

@@ -20,9 +20,7 @@ def main():
     e = generate_rmat(args.scale, 16, seed=1, wseed=2)
     torch.cuda.synchronize()
     ref = None
-    for L, l1, gr in itertools.product([1, 2, 3, 4, 8, 16], [0.125, 0.25, 0.5, 1.0], [2.0, 4.0, 8.0]):
-        if L == 1 and (l1 != 0.25 or gr != 2.0):
-            continue
+    for L, l1, gr in itertools.product([2, 3, 4, 6, 8], [0.25, 0.5, 1.0, 2.0], [2.0, 4.0, 8.0, 16.0]):
         if L == 2 and gr != 2.0:
             continue
         cfg = _native.make_config(max_levels=L, level1_edges_per_vertex=l1, level_growth=gr)
@@ -38,10 +36,10 @@ def main():
         if ref is None:
             ref = res.total_weight
         assert res.total_weight == ref
-        kern = sum(s["ms_minedge"] + s["ms_hook"] + s["ms_jump"] + s["ms_active"] for s in stats)
         print(json.dumps({"levels": L, "l1": l1, "growth": gr, "ms": round(min(ts), 3), "rounds": res.rounds,
-                          "planned_levels": res.levels, "round_kernels_ms": round(kern, 3),
-                          "arcs_per_level": [s["level_arcs"] for s in stats if s["level_arcs"]]}), flush=True)
+                          "planned_levels": res.levels, "ms_select": round(res.ms_select, 3),
+                          "ms_filter": round(res.ms_filter, 3), "filter_out": res.filter_out,
+                          "edges_per_level": [s["level_arcs"] for s in stats if s["level_arcs"]]}), flush=True)
         del eng
         torch.cuda.empty_cache()
 
