@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GHS_MST_LIB", os.path.join(_HERE, "lib", "libghs_mst.so"))
 
 GHS_OK = 0
+GHS_NEED_EXCHANGE = 1  # positive status of ghs_solver_minedge (several ranks opened a level)
 GHS_E_ARG = -1
 GHS_E_NONCANON = -2
 GHS_E_HIP = -3
@@ -34,7 +35,8 @@ EXPORTED_SYMBOLS = (
     "ghs_default_config", "ghs_workspace_bytes", "ghs_mst_device",
     "ghs_build_arcs_temp_bytes", "ghs_count_arcs_range", "ghs_build_arcs_range", "ghs_build_arcs",
     "ghs_check_canonical",
-    "ghs_solver_create", "ghs_solver_minedge", "ghs_solver_pack_best", "ghs_solver_unpack_best",
+    "ghs_solver_create", "ghs_solver_minedge", "ghs_solver_exchange_buffer", "ghs_solver_pack_best",
+    "ghs_solver_unpack_best",
     "ghs_solver_contract", "ghs_solver_finish", "ghs_solver_destroy",
     "ghs_rmat_temp_bytes", "ghs_rmat_generate", "ghs_grid_generate",
 )
@@ -149,6 +151,7 @@ def load():
             "ghs_mst_device": (i32, [u32, u64, vp, vp, vp, P(Config), vp, sz, vp, vp, P(Result), P(RoundStats)]),
             "ghs_solver_create": (i32, [u32, u64, vp, vp, vp, u64, u64, P(Config), vp, sz, vp, vp, P(vp)]),
             "ghs_solver_minedge": (i32, [vp, P(u64)]),
+            "ghs_solver_exchange_buffer": (i32, [vp, P(vp), P(u64)]),
             "ghs_solver_pack_best": (i32, [vp, vp]),
             "ghs_solver_unpack_best": (i32, [vp, vp]),
             "ghs_solver_contract": (i32, [vp, P(i32)]),
@@ -169,8 +172,8 @@ def load():
 
 
 def check(rc):
-    """Raise GHSError for a negative return code."""
-    if rc != GHS_OK:
+    """Raise GHSError for a negative return code (positive statuses are returned)."""
+    if rc < GHS_OK:
         msg = load().ghs_last_error()
         raise GHSError(rc, msg.decode() if msg else "")
     return rc

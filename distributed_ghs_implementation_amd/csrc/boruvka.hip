@@ -643,7 +643,7 @@ __global__ __launch_bounds__(BLOCK) void k_resolve(uint32_t n, uint32_t *lab, ui
   for (uint64_t v = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; v < n; v += (uint64_t)gridDim.x * BLOCK) {
     const uint32_t r = find_lab(lab, (uint32_t)v, err);
     lab[v] = r;
-    root_flag[v] = (r == (uint32_t)v) ? 1 : 0;
+    if (root_flag) root_flag[v] = (r == (uint32_t)v) ? 1 : 0;
   }
 }
 
@@ -771,7 +771,7 @@ __device__ __forceinline__ uint32_t ld_b32(__amdgpu_buffer_rsrc_t r, uint32_t by
 // one 16-B buffer load per array. Validates canonicity (u < v < n, (u, v) strictly ascending)
 // into err bit 8 — before any kernel indexes an array with these ids — and emits the edges with
 // w < w_hi into this block's level staging region (every vertex is its own fragment, so the
-// labels are the endpoints); single rank: flags both ends active. Nothing else is written: the
+// labels are the endpoints); flags both ends active. Nothing else is written: the
 // heavier edges stay where they are until k_filter. Block-private output regions: deterministic,
 // no atomics; the next tile's loads are issued before the current one is compacted.
 // ------------------------------------------------------------------------------------------
@@ -842,7 +842,7 @@ GHS_STREAM_KERNEL void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, const 
     for (int j = 0; j < 4; ++j) {
       omask |= out[j] ? (1u << j) : 0u;
       key[j] = ((uint64_t)w[j] << 32) | (uint32_t)(e0 + j);
-      if (mark && out[j]) {  // active fragments of the level (single rank)
+      if (mark && out[j]) {  // active fragments of the level
         mark[a[j]] = 1;
         mark[b[j]] = 1;
       }
@@ -874,7 +874,7 @@ GHS_STREAM_KERNEL void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, const 
 //    good (cycle property: the reference's REJECT for a whole weight class);
 //  - w < w_hi: a level-1 edge: its labels are gathered (the only gathers of the pass), and if
 //    they differ it goes to this block's region of the level staging (lab[u], lab[v], key) and
-//    both fragments are flagged active (mark, single rank);
+//    both fragments are flagged active (mark);
 //  - otherwise: pending (u, v, key) for the later levels, tested there against their labels.
 // The b-probes are ~1 L2 request per heavy edge and do not overlap the stream (measured: they
 // add), so the pass costs stream + probes; splitting level 1 here saves a pass over the pending
@@ -962,7 +962,7 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
       lev[j] = lev[j] & (la[j] != lb[j]);
       lmask |= lev[j] ? (1u << j) : 0u;
       rmask |= rem[j] ? (1u << j) : 0u;
-      if (lev[j] && mark) {  // active fragments of the level (single rank)
+      if (lev[j] && mark) {  // active fragments of the level
         mark[la[j]] = 1;
         mark[lb[j]] = 1;
       }
@@ -1102,7 +1102,7 @@ GHS_STREAM_KERNEL void k_level_pass(const uint32_t *__restrict__ ru, const uint3
     for (int j = 0; j < 4; ++j) {
       lmask |= lev[j] ? (1u << j) : 0u;
       rmask |= rem[j] ? (1u << j) : 0u;
-      if (lev[j] && mark) {  // active fragments of the level (single rank)
+      if (lev[j] && mark) {  // active fragments of the level
         mark[la[j]] = 1;
         mark[lb[j]] = 1;
       }
@@ -1379,6 +1379,8 @@ struct ghs_solver {
   std::vector<uint8_t> ev_rec;  // per round: bit k = event k recorded
   hipEvent_t pass_ev[4] = {};   // around k_select [0,1] and k_filter [2,3] (from the host pool)
   bool filter_run = false;
+  bool pending_exchange = false;  // multi-rank: a level's flags await the caller's OR all-reduce
+  unsigned open_G = 1;            // regions of the level's edges (between the two halves)
   uint64_t select_out = 0, filter_out = 0;
   bool detail = false;          // GHS_DETAIL=1: time every stage (adds ~5.7 us per event)
   std::chrono::steady_clock::time_point t0;
@@ -1534,8 +1536,11 @@ static int fail_counters(ghs_solver *s, unsigned long long err, const char *wher
   GHS_FAIL(GHS_E_STATE, std::string("internal invariant violated ") + where + " (code " + std::to_string(err) + ")");
 }
 
+static int open_level_finish(ghs_solver *s);
+
 // ---- open the next level: select its edges, set its active list (one host sync) --------------
-// Returns GHS_OK with s->level_open set, or with the level skipped (single rank, no edges).
+// Returns GHS_OK with s->level_open set, with the level skipped (no edges), or — several ranks —
+// with s->pending_exchange set (the caller OR-combines the flags, then open_level_finish).
 static int open_level(ghs_solver *s) {
   const uint32_t lv = s->level;
   const uint64_t w_hi = s->thresholds[lv + 1];
@@ -1546,17 +1551,16 @@ static int open_level(ghs_solver *s) {
 
   if (!first) {
     // compress labels, find the giant fragment from a sample, build its bitmap (all on device)
-    k_resolve<<<grid_for(s->n, BLOCK, 16384), BLOCK, 0, st>>>(s->n, s->lab, s->flags, s->cnt + C_ERR);
+    k_resolve<<<grid_for(s->n, BLOCK, 16384), BLOCK, 0, st>>>(s->n, s->lab, nullptr, s->cnt + C_ERR);
     k_giant<<<1, 1024, 0, st>>>(s->n, s->lab, s->giant);
     k_bitmap<<<grid_for(s->n, BLOCK, 16384), BLOCK, 0, st>>>(s->n, s->lab, s->giant, s->bits);
     GHS_HIP_CHECK(hipGetLastError());
   }
 
   // 1. this level's edges -> regions of Y (level edges: a, b labels + key, canonical order).
-  //    Single rank: the pass also flags both ends of every level edge (the level's active
-  //    fragments).
-  uint8_t *mark = single ? s->flags : nullptr;
-  if (mark) GHS_HIP_CHECK(hipMemsetAsync(s->flags, 0, s->n, st));
+  //    The pass also flags both ends of every level edge (the level's active fragments).
+  uint8_t *mark = s->flags;
+  GHS_HIP_CHECK(hipMemsetAsync(s->flags, 0, s->n, st));
   unsigned G = 1;
   const uint64_t TC = s->e_hi > s->e_lo ? s->e_hi - (s->e_lo & ~3ull) : 0;  // canonical passes stream [e_lo & ~3, e_hi)
   if (first) {
@@ -1616,24 +1620,37 @@ static int open_level(ghs_solver *s) {
     s->rcur = rout;
   }
 
-  // 2. active fragments. Single rank: the fragments that have an edge in this level.
-  //    Several ranks: every current root (first level: every vertex) — identical on every
-  //    rank without an exchange; roots without edges anywhere drop out after one round.
-  if (single || !first) {
-    if (int rc = select_flagged(s, s->flags, nullptr, s->cnt + C_N, s->n, s->act[0], s->cnt + C_ACT)) return rc;
-    s->act_ident = false;
-  } else {
-    s->act_ident = true;
+  if (!single) {  // the caller OR-combines the flags across ranks, then open_level_finish
+    s->pending_exchange = true;
+    s->open_G = G;
+    return GHS_OK;
   }
+  s->open_G = G;
+  return open_level_finish(s);
+}
+
+// ---- second half of opening a level: the active list and the one host sync ------------------
+// The active fragments are those with an edge in this level — on a multi-rank solve, on ANY rank
+// (the flags were OR-combined by the caller), so every rank selects the same list in the same
+// order and the all-reduce slots line up.
+static int open_level_finish(ghs_solver *s) {
+  hipStream_t st = s->stream;
+  const uint32_t lv = s->level;
+  const bool first = (lv == 0);
+  const uint64_t w_hi = s->thresholds[lv + 1];
+  const unsigned G = s->open_G;
+  s->pending_exchange = false;
+  if (int rc = select_flagged(s, s->flags, nullptr, s->cnt + C_N, s->n, s->act[0], s->cnt + C_ACT)) return rc;
+  s->act_ident = false;
   s->act_cur = 0;
   GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, C_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   GHS_HIP_CHECK(hipStreamSynchronize(st));
   if (s->h_cnt[C_ERR]) return fail_counters(s, s->h_cnt[C_ERR], "opening a level");
   const uint64_t S = s->h_cnt[C_LIVE];
   s->rem_total = s->h_cnt[C_PENDING];
+  s->nact = s->h_cnt[C_ACT];
   if (first) s->select_out = S;
   else if (s->filter_run && !s->filter_out) s->filter_out = S + s->rem_total;
-  s->nact = s->act_ident ? s->n : s->h_cnt[C_ACT];
   if (s->debug) {
     uint32_t g[2] = {0, 0};
     (void)hipMemcpy(g, s->giant, 8, hipMemcpyDeviceToHost);
@@ -1642,8 +1659,8 @@ static int open_level(ghs_solver *s) {
             (unsigned long long)s->rem_total, first ? 0u : g[0], first ? 0u : g[1]);
   }
   s->level_arcs = S;
-  if (S == 0 && single) {  // nothing to merge at this level (single rank only: ranks must run the
-    s->level_open = false;   // same rounds)
+  if (s->nact == 0) {  // no edge of this level on any rank (every rank sees the same flags)
+    s->level_open = false;
     return GHS_OK;
   }
   s->cur = 1;  // the level's edges are Y's G regions (S entries incl. padding)
@@ -1907,6 +1924,11 @@ int ghs_solver_minedge(ghs_solver_t *s, uint64_t *num_active) {
   if (s->phase != 0) GHS_FAIL(GHS_E_STATE, "minedge called twice without contract");
   if (s->round >= 16 * GHS_MAX_ROUND_STATS) GHS_FAIL(GHS_E_ROUNDCAP, "round cap exceeded");
   while (!s->level_open) {
+    if (s->pending_exchange) {  // the caller has OR-combined the level's flags
+      if (int rc = open_level_finish(s)) return rc;
+      if (!s->level_open) s->level += 1;  // no edge of this level on any rank
+      continue;
+    }
     if (s->level + 1 >= s->thresholds.size()) {  // every level done
       s->phase = 2;
       if (num_active) *num_active = 0;
@@ -1914,11 +1936,24 @@ int ghs_solver_minedge(ghs_solver_t *s, uint64_t *num_active) {
     }
     int rc = open_level(s);
     if (rc) return rc;
+    if (s->pending_exchange) {
+      if (num_active) *num_active = 0;
+      return GHS_NEED_EXCHANGE;
+    }
     if (!s->level_open) s->level += 1;  // skipped (no edges)
   }
   if (int rc = enqueue_minedge(s)) return rc;
   s->phase = 1;
   if (num_active) *num_active = s->nact;
+  return GHS_OK;
+}
+
+int ghs_solver_exchange_buffer(ghs_solver_t *s, uint8_t **d_flags, uint64_t *bytes) {
+  if (!s || !d_flags || !bytes) GHS_FAIL(GHS_E_ARG, "solver/d_flags/bytes is NULL");
+  if (!s->pending_exchange) GHS_FAIL(GHS_E_STATE, "no exchange pending");
+  GHS_HIP_CHECK(hipStreamSynchronize(s->stream));  // the flags are complete before the caller reads them
+  *d_flags = s->flags;
+  *bytes = s->n;
   return GHS_OK;
 }
 

@@ -4,10 +4,12 @@ Replaces the reference's MPI path (ghs_implementation_mpi.py:884-954: one rank P
 pickled point-to-point messages, bcast/Barrier/gather) with one rank per GPU and ONE collective
 per round:
 
-  * partition: rank r owns the contiguous canonical-edge range [r*m/N, (r+1)*m/N) and builds
-    the arcs of ITS edges only (both directions); the canonical edge list (read by the level
-    pass and to resolve a chosen edge's endpoints) and the fragment state are replicated;
-  * per round: local min-edge over the rank's arcs -> dense best[] slots of the active
+  * partition: rank r owns the contiguous canonical-edge range [r*m/N, (r+1)*m/N) and streams
+    only ITS edges through the level passes; the canonical edge list (to resolve a chosen
+    edge's endpoints) and the fragment state are replicated;
+  * per level: the fragments with a level edge on ANY rank (n-byte flags, all_reduce MAX) form
+    the identical active list of every rank;
+  * per round: local min-edge over the rank's level edges -> dense best[] slots of the active
     fragments -> all_reduce(MIN) -> identical hook / pointer-jump / next-list on every rank;
   * result: in_mst is identical on every rank by construction (same inputs, same decisions);
     rank 0 writes the output (the reference gathered BRANCH edges to rank 0,
@@ -41,9 +43,20 @@ class HipStepper:
         self.dense = torch.empty(max(ed.n, 1), dtype=torch.int64, device=ed.device)
 
     def minedge(self):
+        """Local min-edge of the round; None when a level was opened and its fragment flags must
+        be OR-combined across ranks first (exchange_buffer, then minedge again)."""
         c = ctypes.c_uint64(0)
-        _native.check(self.L.ghs_solver_minedge(self.h, ctypes.byref(c)))
+        rc = _native.check(self.L.ghs_solver_minedge(self.h, ctypes.byref(c)))
+        if rc == _native.GHS_NEED_EXCHANGE:
+            return None
         return int(c.value)
+
+    def exchange_buffer(self):
+        """The level's active-fragment flags (uint8, n) as a torch view to all-reduce with MAX."""
+        p = ctypes.c_void_p(0)
+        nb = ctypes.c_uint64(0)
+        _native.check(self.L.ghs_solver_exchange_buffer(self.h, ctypes.byref(p), ctypes.byref(nb)))
+        return _device_u8_view(p.value, int(nb.value), self.e.edges.device, self.e.ws)
 
     def pack(self, count):
         _native.check(self.L.ghs_solver_pack_best(self.h, _ptr(self.dense)))
@@ -75,15 +88,20 @@ class HipStepper:
             pass
 
 
-def run_rounds(stepper, allreduce_min, max_rounds=4096):
-    """The level loop shared by every backend: min-edge, all-reduce MIN, contract.
+def run_rounds(stepper, allreduce_min, max_rounds=4096, allreduce_max=None):
+    """The level loop shared by every backend: (level open: OR the fragment flags), min-edge,
+    all-reduce MIN, contract.
 
-    `allreduce_min(tensor)` reduces in place across ranks (identity for one rank). Returns the
-    number of rounds executed (all weight levels). Raises RuntimeError past `max_rounds` (hang
-    guard; Boruvka needs at most ceil(log2 n) + 1 rounds per level)."""
+    `allreduce_min(tensor)` / `allreduce_max(tensor)` reduce in place across ranks (identity for
+    one rank; allreduce_max defaults to allreduce_min's backend with MAX). Returns the number of
+    rounds executed (all weight levels). Raises RuntimeError past `max_rounds` (hang guard;
+    Boruvka needs at most ceil(log2 n) + 1 rounds per level)."""
     rounds = 0
     while True:
         count = stepper.minedge()
+        while count is None:  # a level opened: its active fragments = flagged on ANY rank
+            (allreduce_max or allreduce_min.max)(stepper.exchange_buffer())
+            count = stepper.minedge()
         if count:
             dense = stepper.pack(count)
             allreduce_min(dense)
@@ -96,11 +114,27 @@ def run_rounds(stepper, allreduce_min, max_rounds=4096):
             raise RuntimeError("round cap exceeded")
 
 
-def torch_allreduce_min(group=None):
+def _torch_allreduce(op, group=None):
     def fn(t):
         if dist.is_initialized() and dist.get_world_size(group) > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+            dist.all_reduce(t, op=op, group=group)
     return fn
+
+
+def torch_allreduce_min(group=None):
+    fn = _torch_allreduce(dist.ReduceOp.MIN, group)
+    fn.max = _torch_allreduce(dist.ReduceOp.MAX, group)
+    return fn
+
+
+def _device_u8_view(ptr, nbytes, device, owner):
+    """A torch uint8 tensor over nbytes of device memory inside `owner`'s storage (the solver's
+    workspace) — no copy, so the all-reduce combines the engine's own flag array."""
+    base = owner.data_ptr()
+    off = ptr - base
+    if off < 0 or off + nbytes > owner.numel() * owner.element_size():
+        raise RuntimeError("exchange buffer outside the workspace")
+    return owner.view(torch.uint8)[off:off + nbytes]
 
 
 class DistributedMST:

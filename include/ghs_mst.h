@@ -34,6 +34,8 @@ extern "C" {
 #define GHS_MST_ABI_VERSION 2
 
 #define GHS_OK 0
+#define GHS_NEED_EXCHANGE 1   /* ghs_solver_minedge on a multi-rank solver opened a level: OR-combine
+                                 the level's fragment flags across ranks, then call it again */
 #define GHS_E_ARG (-1)        /* bad argument (null pointer, size, alignment) */
 #define GHS_E_NONCANON (-2)   /* input edge list is not canonical */
 #define GHS_E_HIP (-3)        /* HIP runtime error */
@@ -141,7 +143,10 @@ int ghs_check_canonical(uint32_t n, uint64_t m, const uint32_t *d_u, const uint3
  * canonical list and owns the contiguous edge range [e_lo, e_hi); per round it scans the arcs of
  * ITS edges and the per-fragment best keys are combined with an all-reduce MIN by the caller:
  *   h = ghs_solver_create(...)
- *   loop: ghs_solver_minedge(h, &C)            local min-edge per fragment (opens levels)
+ *   loop: rc = ghs_solver_minedge(h, &C)       local min-edge per fragment (opens levels)
+ *         while rc == GHS_NEED_EXCHANGE:       a level was opened (several ranks): its active
+ *           <caller: all_reduce(flags, MAX)>     fragments = those with a level edge on ANY rank
+ *           rc = ghs_solver_minedge(h, &C)       (ghs_solver_exchange_buffer: n uint8 flags)
  *         ghs_solver_pack_best(h, d_dense)     C int64 slots, order-preserving (key ^ 2^63)
  *         <caller: all_reduce(d_dense[0:C], MIN)>
  *         ghs_solver_unpack_best(h, d_dense)
@@ -154,6 +159,8 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
                       size_t workspace_bytes, uint8_t *d_in_mst, void *stream, ghs_solver_t **out);
 /* runs the min-edge kernel; *num_active = fragments whose best slot must be all-reduced */
 int ghs_solver_minedge(ghs_solver_t *h, uint64_t *num_active);
+/* the n-byte flag array to OR-combine (uint8 MAX all-reduce) after GHS_NEED_EXCHANGE */
+int ghs_solver_exchange_buffer(ghs_solver_t *h, uint8_t **d_flags, uint64_t *bytes);
 int ghs_solver_pack_best(ghs_solver_t *h, int64_t *d_dense);
 int ghs_solver_unpack_best(ghs_solver_t *h, const int64_t *d_dense);
 /* hook + jump + next list; *done = 1 when every level is complete */

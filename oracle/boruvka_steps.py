@@ -9,8 +9,9 @@ different fragments (both directions, over the rank's edges only); per round eve
 fragment's minimum outgoing key (w << 32 | eid) over the rank's arcs; after the caller's
 all-reduce MIN, hook to the other fragment of the best edge (mutual pair: smaller label stays
 root), pointer-jump to roots, next active list = roots that had an outgoing edge, ascending
-(the HIP select is order-preserving, so the lists agree across ranks). A level starts with every
-current root active (first level: every vertex).
+(the HIP select is order-preserving, so the lists agree across ranks). A level starts with the
+fragments that have a level edge on ANY rank: minedge returns None after opening a level, the
+caller OR-combines exchange_buffer() across ranks (all-reduce MAX) and calls minedge again.
 """
 import numpy as np
 
@@ -51,17 +52,32 @@ class CpuStepper:
         self.src = np.concatenate([cu, cv])
         self.dst = np.concatenate([cv, cu])
         self.akey = np.concatenate([self.key[e], self.key[e]])
-        if self.level == 0:
-            self.active = np.arange(self.n, dtype=np.int64)
-        else:
-            self.active = np.flatnonzero(self.comp == np.arange(self.n)).astype(np.int64)
-        self.level_open = True
+        # the level's active fragments: flagged locally here, OR-combined across ranks by the
+        # caller (exchange_buffer), then selected in ascending order (ghs_solver_exchange_buffer)
+        self.flags = self.torch.zeros(self.n, dtype=self.torch.uint8)
+        self.flags[self.torch.from_numpy(np.concatenate([cu, cv]))] = 1
+        self.exchange_pending = True
+
+    def exchange_buffer(self):
+        return self.flags
 
     def minedge(self):
-        if self.done:
-            return 0
-        if not self.level_open:
+        while True:
+            if self.done:
+                return 0
+            if self.level_open:
+                break
+            if getattr(self, "exchange_pending", False):
+                self.exchange_pending = False
+                self.active = np.flatnonzero(self.flags.numpy()).astype(np.int64)
+                if len(self.active) == 0:  # no edge of this level on any rank
+                    self.level += 1
+                    self.done = self.level + 1 >= len(self.thr)
+                    continue
+                self.level_open = True
+                break
             self._open_level()
+            return None
         cs = self.comp[self.src]
         cd = self.comp[self.dst]
         mk = cs != cd

@@ -35,7 +35,10 @@ def _worker(rank, world, port, n, u, v, w, thr, out):
     def ar(t):
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
 
-    rounds = run_rounds(st, ar)
+    def ar_max(t):
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+
+    rounds = run_rounds(st, ar, allreduce_max=ar_max)
     total, count = st.finish()
     out[rank] = (st.in_mst.tolist(), total, count, rounds)
     dist.barrier()

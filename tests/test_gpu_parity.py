@@ -164,6 +164,15 @@ def test_partitioned_ranks_emulated_on_one_gpu(world, torch_cuda):
     done = False
     while not done:
         counts = [s.minedge() for s in steppers]
+        while counts[0] is None:  # a level opened: OR-combine the fragment flags (emulated MAX)
+            assert all(c is None for c in counts)
+            bufs = [s.exchange_buffer() for s in steppers]
+            red = bufs[0].clone()
+            for b in bufs[1:]:
+                red = torch.maximum(red, b)
+            for b in bufs:
+                b.copy_(red)
+            counts = [s.minedge() for s in steppers]
         assert len(set(counts)) == 1
         if counts[0]:
             dense = [s.pack(counts[0]).clone() for s in steppers]
