@@ -1383,6 +1383,7 @@ struct ghs_solver {
   unsigned open_G = 1;            // regions of the level's edges (between the two halves)
   uint64_t select_out = 0, filter_out = 0;
   bool detail = false;          // GHS_DETAIL=1: time every stage (adds ~5.7 us per event)
+  uint32_t seg_g = SEG_G;       // blocks of the streaming kernels (GHS_SEG_G, 256..SEG_G)
   std::chrono::steady_clock::time_point t0;
 };
 
@@ -1565,7 +1566,7 @@ static int open_level(ghs_solver *s) {
   const uint64_t TC = s->e_hi > s->e_lo ? s->e_hi - (s->e_lo & ~3ull) : 0;  // canonical passes stream [e_lo & ~3, e_hi)
   if (first) {
     // SELECT over the canonical list: level-0 edges only (validates the list)
-    G = grid_for(TC, ARCS_PER_BLOCK, SEG_G);
+    G = grid_for(TC, ARCS_PER_BLOCK, s->seg_g);
     if (TC) {
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[0], st));
       k_select<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, w_hi, Y.src, Y.dst, Y.key,
@@ -1584,7 +1585,7 @@ static int open_level(ghs_solver *s) {
     if (!s->pending_built) {
       // FILTER + level split over the canonical list once level 0 is complete: level-1 edges
       // not inside one fragment -> Y; heavier edges not inside the giant -> pending (rem[rout])
-      G = grid_for(TC, ARCS_PER_BLOCK, SEG_G);
+      G = grid_for(TC, ARCS_PER_BLOCK, s->seg_g);
       if (TC) {
         GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[2], st));
         k_filter<<<G, BLOCK, 0, st>>>(s->e_lo, s->e_hi, s->eu, s->ev, s->ew, s->thresholds[lv], w_hi, s->bits, s->lab,
@@ -1605,8 +1606,8 @@ static int open_level(ghs_solver *s) {
       s->pending_built = true;
     } else {
       // split the pending edges (total on the device): this level's inter-fragment edges -> Y;
-      // heavier survivors -> RO regions. Fixed grid: block b owns 1/SEG_G of the virtual range.
-      G = SEG_G;
+      // heavier survivors -> RO regions. Fixed grid: block b owns 1/seg_g of the virtual range.
+      G = s->seg_g;
       SegView in{RI.seg_start, RI.seg_prefix, s->rem_nseg};
       k_level_pass<<<G, BLOCK, 0, st>>>(RI.src, RI.dst, RI.key, in, w_hi, s->lab, s->bits, Y.src, Y.dst, Y.key,
                                         Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key, RO.seg_start, RO.seg_count,
@@ -1686,13 +1687,13 @@ static int enqueue_minedge(ghs_solver *s) {
   SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
   if (s->level_round == 0) {
     if (s->cur_arcs)
-      k_minedge<true, false><<<grid_for(s->cur_arcs, ARCS_PER_BLOCK, SEG_G), BLOCK, 0, s->stream>>>(
+      k_minedge<true, false><<<grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->seg_g), BLOCK, 0, s->stream>>>(
           I.src, I.dst, I.key, in, s->lab, s->best, nullptr, nullptr, nullptr, nullptr, nullptr);
   } else {
-    // fixed grid: every one of the SEG_G blocks writes its region's count
-    k_minedge<false, true><<<SEG_G, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, O.src, O.dst,
+    // fixed grid: every one of the seg_g blocks writes its region's count
+    k_minedge<false, true><<<s->seg_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, O.src, O.dst,
                                                           O.key, O.seg_start, O.seg_count);
-    k_scan_counts<<<1, 1024, 0, s->stream>>>(O.seg_count, SEG_G, O.seg_prefix, s->cnt + C_LIVE);
+    k_scan_counts<<<1, 1024, 0, s->stream>>>(O.seg_count, s->seg_g, O.seg_prefix, s->cnt + C_LIVE);
   }
   GHS_HIP_CHECK(hipGetLastError());
   if (timed) record(s, 1);
@@ -1714,7 +1715,7 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
     if (edge_form) {
       const ArcBuf &I = s->buf[s->cur];
       SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
-      k_win<<<grid_for(s->cur_arcs, ARCS_PER_BLOCK, SEG_G), BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->best,
+      k_win<<<grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->seg_g), BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->best,
                                                                                    s->par, s->in_mst, s->cnt + C_WEIGHT);
     } else {
       k_hook<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
@@ -1752,7 +1753,7 @@ static int wait_slot(ghs_solver *s, const RoundSlot *hs, unsigned long long seq)
 static void advance_round(ghs_solver *s) {
   if (s->level_round >= 1) {  // this round's min-edge kernel compacted into the other buffer
     s->cur ^= 1;
-    s->cur_nseg = SEG_G;
+    s->cur_nseg = s->seg_g;
   }
   s->act_cur = s->act_ident ? 0 : (s->act_cur ^ 1);
   s->act_ident = false;
@@ -1868,6 +1869,10 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   s->in_mst = d_in_mst; s->stream = (hipStream_t)stream;
   { const char *dbg = getenv("GHS_DEBUG"); s->debug = dbg && dbg[0] == '1'; }
   { const char *det = getenv("GHS_DETAIL"); s->detail = det && det[0] == '1'; }
+  if (const char *g = getenv("GHS_SEG_G")) {  // A/B tests: blocks of the streaming kernels
+    const long v = strtol(g, nullptr, 10);
+    s->seg_g = (uint32_t)(v < 256 ? 256 : (v > (long)SEG_G ? SEG_G : v));
+  }
   if (cfg) s->cfg = *cfg; else default_config(&s->cfg);
   workspace_layout(n, e_hi - e_lo, s, (char *)d_workspace);
   hipError_t e;

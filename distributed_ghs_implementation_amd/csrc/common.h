@@ -22,7 +22,15 @@ void set_error(const std::string &msg);
 // admits 8 resident 256-thread blocks per CU only while .sgpr_count <= 80 (MI355X_MICROARCH.md,
 // "Residency"); at 82-96 it admits 7 and a 2048-block grid runs a second, nearly empty wave of
 // blocks — half the throughput of an equal-work grid. The cap keeps these kernels at 8.
-#define GHS_STREAM_KERNEL __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(72)))
+// VGPRs are NOT capped: k_filter / k_level_pass / k_minedge use 75-80 (6 waves per SIMD), and
+// forcing 8 waves (GHS_STREAM_WAVES=8, <= 64 VGPRs) spills 8-14 of them to scratch and measured
+// slower (R-MAT s24: 7.41 vs 7.00 ms per step); a grid sized to 6 blocks per CU (GHS_SEG_G=1536)
+// measured the same as 2048 (7.04-7.12 ms). Second argument: min waves per SIMD.
+#ifndef GHS_STREAM_WAVES
+#define GHS_STREAM_WAVES 1
+#endif
+#define GHS_STREAM_KERNEL \
+  __global__ __launch_bounds__(BLOCK, GHS_STREAM_WAVES) __attribute__((amdgpu_num_sgpr(72)))
 
 // bijective 32-bit mixer (xorshift-multiply; every step is invertible on u32)
 __host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
