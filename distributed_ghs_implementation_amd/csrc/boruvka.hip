@@ -599,9 +599,13 @@ GHS_STREAM_KERNEL void k_win(const uint32_t *__restrict__ src, const uint32_t *_
 }
 
 // ------------------------------------------------------------------------------------------
-// Stage 3: pointer jumping (INITIATE broadcast of the new fragment id). Path splitting on par:
-// concurrent compression only moves a pointer to an ancestor, so stale reads are still valid
-// ancestors and every walk ends at its root. lab[c] = root.
+// Stage 3: pointer jumping (INITIATE broadcast of the new fragment id), one fragment per thread
+// (every walk of the round in flight at once). Path splitting on par: concurrent compression
+// only moves a pointer to an ancestor, so stale reads are still valid ancestors and every walk
+// ends at its root; lab[c] = root. Stage 3b: the next active list = roots that still had an
+// outgoing edge (their best slot is reset); keep byte -> flags[i] for k_select_lb. A root with
+// no outgoing edge is finished for the level (the reference: "best_weight == inf at the core =>
+// terminate", ghs_implementation.py:316-320).
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
                                                 uint32_t *par, uint32_t *__restrict__ lab, uint64_t *__restrict__ best,
@@ -611,7 +615,7 @@ __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act
     const uint32_t c = act ? act[i] : (uint32_t)i;
     uint32_t x = c;
     uint32_t px = par[x];
-    const bool root = px == c;  // roots are never rewritten below: par[c] == c is stable
+    const bool root = px == c;
     uint32_t steps = 0;
     while (px != x) {
       const uint32_t ppx = par[px];
@@ -624,11 +628,6 @@ __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act
       }
     }
     lab[c] = x;
-    // Stage 3b: the next active list = roots that still had an outgoing edge (their best slot
-    // is reset). A root with no outgoing edge is finished for this level (the reference:
-    // "best_weight == inf at the core => terminate", ghs_implementation.py:316-320). The list
-    // is produced by an order-preserving select, so every rank of a multi-GPU run holds the
-    // same list in the same order and the all-reduce slots line up.
     const bool keep = root && best[c] != KEY_NONE;
     if (keep) best[c] = KEY_NONE;
     flags[i] = keep ? 1 : 0;
@@ -1161,42 +1160,10 @@ __global__ void k_unpack_best(const uint32_t *__restrict__ act, const unsigned l
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// Order-preserving select of flagged items: out[k] = (in ? in[i] : i) for the k-th i with
-// flags[i] != 0. Two passes over the byte flags (16 per lane per load) around a scan of
-// per-block counts; every rank of a multi-GPU run produces the same list in the same order.
-// ------------------------------------------------------------------------------------------
-constexpr uint32_t SEL_PER_BLOCK = BLOCK * 16;
-
-__global__ __launch_bounds__(BLOCK) void k_sel_count(const uint8_t *__restrict__ flags,
-                                                     const unsigned long long *__restrict__ d_count,
-                                                     uint64_t *__restrict__ bcount) {
-  __shared__ uint32_t s_w[BLOCK / WAVE];
-  const uint64_t count = *d_count;
-  const uint64_t i0 = (uint64_t)blockIdx.x * SEL_PER_BLOCK + threadIdx.x * 16ull;
-  uint32_t c = 0;
-  if (i0 + 16 <= count) {
-    const uint4 f = *reinterpret_cast<const uint4 *>(flags + i0);
-    const uint32_t x[4] = {f.x, f.y, f.z, f.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) c += __popc((x[k] | (x[k] >> 1) | (x[k] >> 2) | (x[k] >> 3) | (x[k] >> 4) | (x[k] >> 5) | (x[k] >> 6) | (x[k] >> 7)) & 0x01010101u);
-  } else {
-    for (uint64_t i = i0; i < count && i < i0 + 16; ++i) c += flags[i] ? 1u : 0u;
-  }
-#pragma unroll
-  for (int d = WAVE / 2; d > 0; d >>= 1) c += __shfl_xor(c, d);
-  if ((threadIdx.x & (WAVE - 1)) == 0) s_w[threadIdx.x / WAVE] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
-#pragma unroll
-    for (int w = 0; w < BLOCK / WAVE; ++w) t += s_w[w];
-    bcount[blockIdx.x] = t;
-  }
-}
-
 // Result of a round, written into coherent pinned host memory by the round's last kernel; the
 // host polls seq (written last, after a system-scope fence).
+constexpr int C_ERR_IDX = 4;  // == C_ERR (counter layout below)
+
 struct RoundSlot {
   unsigned long long live_out, nact_out, edges, err;
   unsigned long long seq;
@@ -1205,10 +1172,11 @@ struct RoundSlot {
 
 __device__ __forceinline__ void write_report(RoundSlot *slot, unsigned long long seq, const unsigned long long *cnt,
                                              unsigned long long nact_out) {
-  slot->live_out = cnt[0];  // live edges after this round's compaction
-  slot->nact_out = nact_out;  // active fragments of the next round
-  slot->edges = cnt[3];     // MSF edges so far
-  slot->err = cnt[4];       // error bits
+  // device-scope loads: the error bits may come from other workgroups of the writing launch
+  slot->live_out = __hip_atomic_load(cnt + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // live edges after this round's compaction
+  slot->nact_out = nact_out;                                                               // active fragments of the next round
+  slot->edges = __hip_atomic_load(cnt + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);    // MSF edges so far
+  slot->err = __hip_atomic_load(cnt + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);      // error bits
   __threadfence_system();
   __hip_atomic_store(&slot->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1218,36 +1186,131 @@ __global__ void k_round_report(RoundSlot *slot, unsigned long long seq, const un
   write_report(slot, seq, cnt, *nact_out);
 }
 
-__global__ __launch_bounds__(BLOCK) void k_sel_write(const uint8_t *__restrict__ flags, const uint32_t *__restrict__ in,
-                                                     const unsigned long long *__restrict__ d_count,
-                                                     const uint64_t *__restrict__ bprefix, uint32_t *__restrict__ out,
-                                                     RoundSlot *slot, unsigned long long seq,
-                                                     const unsigned long long *__restrict__ cnt) {
-  __shared__ uint32_t s_wcnt[BLOCK / WAVE];
-  const uint64_t count = *d_count;
-  if (slot && blockIdx.x == 0 && threadIdx.x == 0) write_report(slot, seq, cnt, bprefix[gridDim.x]);
-  const uint64_t i0 = (uint64_t)blockIdx.x * SEL_PER_BLOCK + threadIdx.x * 16ull;
-  uint32_t bits = 0;  // bit k = flags[i0 + k]
-  if (i0 + 16 <= count) {
-    const uint4 f = *reinterpret_cast<const uint4 *>(flags + i0);
-    const uint32_t x[4] = {f.x, f.y, f.z, f.w};
+// ------------------------------------------------------------------------------------------
+// Order-preserving select in ONE launch: out[k] = (act ? act[i] : i) for the k-th i < *d_count
+// with flags[i] != 0; every rank of a multi-GPU run produces the same list in the same order.
+// (Opening a level: the flagged vertices. A round: the fragments k_jump kept.)
+//  - at most LB_MAX_TILES (1024) workgroups of 256 threads: <= 4 per CU, always co-resident
+//    (cdna_hip_programming.md §1), so waiting on another tile of the launch cannot deadlock
+//    whatever the dispatch order; a tile covers LB_GROUP * G items (G from the host).
+//  - pass 1 counts the tile's flagged items, the tile publishes its count as one 8-byte granule
+//    {tag = epoch, count} by an agent-scope atomic store (the data is the flag: G16 R2), then
+//    sums the counts of all lower tiles (one wave, <= 16 agent-scope granule loads per lane,
+//    re-polled until every tag matches; a granule of another launch carries another tag). No
+//    ticket counter: one device-scope counter costs ~12 ns per arrival (MI355X_MICROARCH.md,
+//    fanin) — 50 us for 4096 tiles, measured.
+//  - pass 2 re-reads the flags and writes the tile's items at its prefix.
+//  - the last tile's prefix + count is the total: that block writes *d_total and, for a round,
+//    the round report (live, active, edges, err, seq) to the pinned slot.
+//  - every spin is bounded: a timeout sets err bit 16 and the block writes nothing.
+// Replaces count + scan + write (3 launches). Fusing k_jump into pass 1 as well measured slower
+// (6.88 vs 6.72 ms per step, R-MAT s24): 1024 co-resident tiles leave each lane 8 walks in lock
+// step, where k_jump has every walk of the round in flight.
+// ------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+constexpr uint32_t LB_MAX_TILES = 1024;
+constexpr uint32_t LB_GROUP = BLOCK * 16;     // items per group: 16 keep bytes per lane (one 16-B load)
+constexpr uint32_t LB_MAX_SPINS = 1u << 16;   // x (load latency + s_sleep) ~ 0.1 s, never reached in a sane run
+
+__device__ __forceinline__ unsigned long long lb_granule(uint32_t tag, uint32_t v) {
+  return ((unsigned long long)tag << 32) | v;
+}
+
+// sum of the counts of tiles [0, t); ONE wave (all 64 lanes); false on timeout
+__device__ bool lb_prefix(unsigned long long *state, uint32_t t, uint32_t tag, uint64_t *out) {
+  constexpr int R = LB_MAX_TILES / WAVE;
+  const int lane = threadIdx.x & (WAVE - 1);
+  gu64 *st = (gu64 *)state;
+  uint32_t spins = 0;
+  for (;;) {
+    uint64_t sum = 0;
+    bool ready = true;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) bits |= (((x[k >> 2] >> (8 * (k & 3))) & 0xffu) ? 1u : 0u) << k;
-  } else {
-    for (int k = 0; k < 16; ++k)
-      if (i0 + k < count && flags[i0 + k]) bits |= 1u << k;
-  }
-  uint32_t tot;
-  const uint32_t before = block_offsets((uint32_t)__popc(bits), s_wcnt, &tot);
-  uint64_t pos = bprefix[blockIdx.x] + before;
-  while (bits) {
-    const int k = __ffs(bits) - 1;
-    bits &= bits - 1;
-    const uint64_t i = i0 + k;
-    out[pos++] = in ? in[i] : (uint32_t)i;
+    for (int r = 0; r < R; ++r) {
+      const uint32_t idx = (uint32_t)lane + (uint32_t)(WAVE * r);
+      if (idx < t) {
+        const unsigned long long g = __hip_atomic_load(st + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ready &= (uint32_t)(g >> 32) == tag;
+        sum += (uint32_t)g;
+      }
+    }
+    if (__all(ready)) {
+#pragma unroll
+      for (int d = WAVE / 2; d > 0; d >>= 1) sum += __shfl_xor(sum, d);
+      *out = sum;
+      return true;
+    }
+    if (++spins > LB_MAX_SPINS) return false;
+    __builtin_amdgcn_s_sleep(2);
   }
 }
 
+__device__ __forceinline__ uint32_t keep_bits16(const uint8_t *__restrict__ flags, uint64_t i0, uint64_t count) {
+  uint32_t bits = 0;
+  if (i0 + 16 <= count) {
+    const uint4 f = *reinterpret_cast<const uint4 *>(flags + i0);
+    const uint32_t w[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) bits |= (((w[k >> 2] >> (8 * (k & 3))) & 0xffu) ? 1u : 0u) << k;
+  } else {
+    for (uint32_t k = 0; k < 16; ++k)
+      if (i0 + k < count && flags[i0 + k]) bits |= 1u << k;
+  }
+  return bits;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_select_lb(const uint8_t *__restrict__ flags, const uint32_t *__restrict__ act,
+                                                     const unsigned long long *__restrict__ d_count, uint32_t groups,
+                                                     uint32_t *__restrict__ out, unsigned long long *__restrict__ d_total,
+                                                     unsigned long long *state, uint32_t tag, RoundSlot *slot,
+                                                     unsigned long long seq, unsigned long long *cnt) {
+  __shared__ uint32_t s_wcnt[BLOCK / WAVE];
+  __shared__ uint64_t s_excl;
+  __shared__ int s_ok;
+  const uint32_t t = blockIdx.x;
+  const uint64_t count = *d_count;
+  const uint64_t tb = (uint64_t)t * groups * LB_GROUP;  // first item of the tile
+  uint32_t mine = 0;  // kept items of this lane (pass 1)
+  for (uint32_t g = 0; g < groups; ++g)
+    mine += __popc(keep_bits16(flags, tb + (uint64_t)g * LB_GROUP + (uint64_t)threadIdx.x * 16, count));
+  uint32_t tot;
+  (void)block_offsets(mine, s_wcnt, &tot);  // block total (barriers inside)
+  if (threadIdx.x == 0) {
+    __hip_atomic_store((gu64 *)state + t, lb_granule(tag, tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_excl = 0;
+    s_ok = 1;
+  }
+  if (t > 0 && threadIdx.x < WAVE) {
+    uint64_t ex = 0;
+    const bool ok = lb_prefix(state, t, tag, &ex);
+    if (threadIdx.x == 0) {
+      s_excl = ex;
+      s_ok = ok ? 1 : 0;
+      if (!ok) atomicOr(cnt + C_ERR_IDX, 16ull);
+    }
+  }
+  __syncthreads();
+  if (!s_ok) return;
+  // pass 2: the keep bytes again (L2-resident) -> out, in item order
+  uint64_t run = s_excl;
+  for (uint32_t g = 0; g < groups; ++g) {
+    const uint64_t i0 = tb + (uint64_t)g * LB_GROUP + (uint64_t)threadIdx.x * 16;
+    uint32_t bits = keep_bits16(flags, i0, count);
+    uint32_t gt;
+    const uint32_t before = block_offsets((uint32_t)__popc(bits), s_wcnt, &gt);
+    uint64_t pos = run + before;
+    while (bits) {
+      const int k = __ffs(bits) - 1;
+      bits &= bits - 1;
+      out[pos++] = act ? act[i0 + k] : (uint32_t)(i0 + k);
+    }
+    run += gt;
+  }
+  if (t == gridDim.x - 1 && threadIdx.x == 0) {
+    *d_total = s_excl + tot;
+    if (slot) write_report(slot, seq, cnt, s_excl + tot);
+  }
+}
 
 static inline unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap) {
   uint64_t g = (items + per_block - 1) / per_block;
@@ -1278,7 +1341,7 @@ enum : int {
   C_LIVE = 0,     // live edges (virtual total incl. padding) written by the last compaction scan
   C_WEIGHT = 2,   // MSF weight so far
   C_EDGES = 3,    // MSF edges so far (== hooks)
-  C_ERR = 4,      // invariant / canonicity error bits
+  C_ERR = C_ERR_IDX,  // invariant / canonicity error bits
   C_PENDING = 5,  // pending edges (virtual total) after the last level pass
   C_N = 6,        // n (the count of the identity active list)
   C_ACT = 8,      // [8], [9]: lengths of the active lists act[0], act[1]
@@ -1339,7 +1402,8 @@ struct ghs_solver {
   uint8_t *flags = nullptr;
   uint32_t *sample = nullptr;
   uint32_t *giant = nullptr;  // device [0] giant label, [1] its sampled vertex count
-  uint64_t *sel_cnt = nullptr, *sel_pre = nullptr;  // select scratch (per-block counts / prefix)
+  unsigned long long *lb_state = nullptr;  // single-pass select: tile granules (zeroed at create)
+  uint32_t lb_epoch = 0;                   // tag of the last select launch
   ArcBuf buf[2];             // a level's edges (regions) and the round double buffer
   ArcBuf rem[2];             // pending (not yet levelled) edges: u, v, key as regions
   int rcur = 0;              // rem buffer holding the pending edges (level >= 1)
@@ -1383,6 +1447,7 @@ struct ghs_solver {
   unsigned open_G = 1;            // regions of the level's edges (between the two halves)
   uint64_t select_out = 0, filter_out = 0;
   bool detail = false;          // GHS_DETAIL=1: time every stage (adds ~5.7 us per event)
+  bool time_rounds = false;     // GHS_TIME_ROUNDS=1: time the compacting min-edge launches (bench)
   uint32_t seg_g = SEG_G;       // blocks of the streaming kernels (GHS_SEG_G, 256..SEG_G)
   std::chrono::steady_clock::time_point t0;
 };
@@ -1429,9 +1494,7 @@ static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, 
   p = carve(((N + 127) / 128) * 16 + 16); if (s) s->bits = (uint64_t *)p;
   p = carve(NSAMPLE_MAX * 4); if (s) s->sample = (uint32_t *)p;
   p = carve(16); if (s) s->giant = (uint32_t *)p;
-  const size_t nsel = (N + SEL_PER_BLOCK - 1) / SEL_PER_BLOCK + 1;
-  p = carve(nsel * 8); if (s) s->sel_cnt = (uint64_t *)p;
-  p = carve((nsel + 1) * 8); if (s) s->sel_pre = (uint64_t *)p;
+  p = carve(LB_MAX_TILES * 8); if (s) s->lb_state = (unsigned long long *)p;  // select tile granules
   for (int b = 0; b < 2; ++b) {
     p = carve(cap * 4); if (s) s->buf[b].src = (uint32_t *)p;
     p = carve(cap * 4); if (s) s->buf[b].dst = (uint32_t *)p;
@@ -1465,9 +1528,9 @@ static hipEvent_t round_event(ghs_solver *s, uint32_t round, int k) {
   return pool[idx];
 }
 
-// Timing events cost ~5.7 us of GPU idle each between dependent kernels (measured), so by
-// default only the compacting min-edge launches are bracketed (the bench's roofline kernel);
-// GHS_DETAIL=1 brackets every stage of every round.
+// Timing events cost ~5.7 us of GPU idle each between dependent kernels (measured), so rounds
+// are not timed by default; GHS_TIME_ROUNDS=1 brackets the compacting min-edge launches (the
+// bench's instrumented step), GHS_DETAIL=1 every stage of every round.
 static void record(ghs_solver *s, int k) {
   hipEvent_t ev = round_event(s, s->round, k);
   if (!ev) return;
@@ -1476,22 +1539,29 @@ static void record(ghs_solver *s, int k) {
   s->ev_rec[s->round] |= (uint8_t)(1u << k);
 }
 
-// Order-preserving select of the flagged items of [0, count) (or of in[0, count)), count on the
-// device (d_count), bound >= count on the host; *d_total = k.
-// slot != nullptr: the write kernel also reports the round (seq) to the pinned slot.
-static int select_flagged(ghs_solver *s, const uint8_t *flags, const uint32_t *in, const unsigned long long *d_count,
-                          uint64_t bound, uint32_t *out, unsigned long long *d_total, RoundSlot *slot = nullptr,
-                          unsigned long long seq = 0) {
+static uint32_t next_tag(ghs_solver *s) {
+  if (++s->lb_epoch == 0) s->lb_epoch = 1;  // 0 is the zeroed state's tag
+  return s->lb_epoch;
+}
+
+// Order-preserving select, one launch: (act ? act[i] : i) for the i < *d_count with flags[i] != 0
+// (bound >= *d_count on the host sizes the grid). *d_total = kept items.
+// slot != nullptr: the kernel also reports the round (seq) to the pinned slot.
+static int select_lb(ghs_solver *s, const uint32_t *act, const unsigned long long *d_count, uint64_t bound,
+                     uint32_t *out, unsigned long long *d_total, RoundSlot *slot = nullptr, unsigned long long seq = 0) {
   if (bound == 0) {
     GHS_HIP_CHECK(hipMemsetAsync(d_total, 0, 8, s->stream));
     if (slot) k_round_report<<<1, 1, 0, s->stream>>>(slot, seq, s->cnt, d_total);
     GHS_HIP_CHECK(hipGetLastError());
     return GHS_OK;
   }
-  const unsigned nb = (unsigned)((bound + SEL_PER_BLOCK - 1) / SEL_PER_BLOCK);
-  k_sel_count<<<nb, BLOCK, 0, s->stream>>>(flags, d_count, s->sel_cnt);
-  k_scan_counts<<<1, 1024, 0, s->stream>>>(s->sel_cnt, nb, s->sel_pre, d_total);
-  k_sel_write<<<nb, BLOCK, 0, s->stream>>>(flags, in, d_count, s->sel_pre, out, slot, seq, s->cnt);
+  // tiles of G groups, at most LB_MAX_TILES of them (co-resident)
+  const uint64_t per = (uint64_t)LB_MAX_TILES * LB_GROUP;
+  const uint64_t G = (bound + per - 1) / per;
+  const uint64_t nb = (bound + G * LB_GROUP - 1) / (G * LB_GROUP);
+  if (nb > LB_MAX_TILES || G >= (1ull << 20)) GHS_FAIL(GHS_E_STATE, "select: bad tiling");
+  k_select_lb<<<(unsigned)nb, BLOCK, 0, s->stream>>>(s->flags, act, d_count, (uint32_t)G, out, d_total, s->lb_state,
+                                                     next_tag(s), slot, seq, s->cnt);
   GHS_HIP_CHECK(hipGetLastError());
   return GHS_OK;
 }
@@ -1641,7 +1711,7 @@ static int open_level_finish(ghs_solver *s) {
   const uint64_t w_hi = s->thresholds[lv + 1];
   const unsigned G = s->open_G;
   s->pending_exchange = false;
-  if (int rc = select_flagged(s, s->flags, nullptr, s->cnt + C_N, s->n, s->act[0], s->cnt + C_ACT)) return rc;
+  if (int rc = select_lb(s, nullptr, s->cnt + C_N, s->n, s->act[0], s->cnt + C_ACT)) return rc;
   s->act_ident = false;
   s->act_cur = 0;
   GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, C_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
@@ -1680,7 +1750,7 @@ static inline const unsigned long long *cur_act_count(ghs_solver *s) {
 
 // ---- one round, enqueued without a host sync (sizes on the device; s->nact is a bound) --------
 static int enqueue_minedge(ghs_solver *s) {
-  const bool timed = s->detail || s->level_round >= 1;
+  const bool timed = s->detail || (s->time_rounds && s->level_round >= 1);
   if (timed) record(s, 0);
   const ArcBuf &I = s->buf[s->cur];
   ArcBuf &O = s->buf[s->cur ^ 1];
@@ -1723,12 +1793,13 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
     }
     GHS_HIP_CHECK(hipGetLastError());
     if (s->detail) record(s, 2);
+    // Stage 3, then the next active list (one launch each)
     k_jump<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->par, s->lab, s->best, s->flags, s->cnt + C_ERR);
     GHS_HIP_CHECK(hipGetLastError());
     if (s->detail) record(s, 3);
-    if (int rc = select_flagged(s, s->flags, act, d_nact, bound, s->act[nb], act_count(s, nb), slot, seq)) return rc;
+    if (int rc = select_lb(s, act, d_nact, bound, s->act[nb], act_count(s, nb), slot, seq)) return rc;
   } else {
-    if (int rc = select_flagged(s, s->flags, act, d_nact, 0, s->act[nb], act_count(s, nb), slot, seq)) return rc;
+    if (int rc = select_lb(s, act, d_nact, 0, s->act[nb], act_count(s, nb), slot, seq)) return rc;
   }
   if (s->detail) record(s, 4);
   return GHS_OK;
@@ -1814,7 +1885,10 @@ static int run_level_pipelined(ghs_solver *s) {
     nact_prev = r.nact_out;
     s->nact = r.nact_out;  // tighter bound for the rounds enqueued from here on
     ++checked;
-    if (r.nact_out == 0) break;  // level complete after round `checked`
+    // level complete after round `checked`: no active fragment left, or one — every remaining
+    // level edge then lies inside it (a fragment drops out only with no outgoing edge, so all
+    // other fragments of the level were hooked into this tree)
+    if (r.nact_out <= 1) break;
   }
   // rounds issued past the last real one were no-ops: rewind the round counter (their events
   // are forgotten and re-recorded by the next level)
@@ -1869,6 +1943,7 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   s->in_mst = d_in_mst; s->stream = (hipStream_t)stream;
   { const char *dbg = getenv("GHS_DEBUG"); s->debug = dbg && dbg[0] == '1'; }
   { const char *det = getenv("GHS_DETAIL"); s->detail = det && det[0] == '1'; }
+  { const char *tr = getenv("GHS_TIME_ROUNDS"); s->time_rounds = tr && tr[0] == '1'; }
   if (const char *g = getenv("GHS_SEG_G")) {  // A/B tests: blocks of the streaming kernels
     const long v = strtol(g, nullptr, 10);
     s->seg_g = (uint32_t)(v < 256 ? 256 : (v > (long)SEG_G ? SEG_G : v));
@@ -1901,6 +1976,7 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
     k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->par, n);  // every root: par[r] == r
   }
   if (m && (e = hipMemsetAsync(s->in_mst, 0, m, s->stream)) != hipSuccess) return fail(e, "memset in_mst");
+  if ((e = hipMemsetAsync(s->lb_state, 0, LB_MAX_TILES * 8, s->stream)) != hipSuccess) return fail(e, "memset select state");
   if ((e = hipMemsetAsync(s->cnt, 0, C_COUNT * sizeof(unsigned long long), s->stream)) != hipSuccess)
     return fail(e, "memset counters");
   const unsigned long long nn = n;
@@ -2001,7 +2077,7 @@ int ghs_solver_contract(ghs_solver_t *s, int *done) {
   push_stats(s, s->level_round, live_in, nact_in, s->h_cnt[C_EDGES]);
   s->nact = s->h_cnt[C_ACT + nb];
   advance_round(s);
-  if (s->nact == 0) {  // level complete
+  if (s->nact <= 1) {  // level complete (one active fragment: its remaining edges are internal)
     close_level(s);
   } else {
     s->phase = 0;

@@ -9,7 +9,8 @@ different fragments (both directions, over the rank's edges only); per round eve
 fragment's minimum outgoing key (w << 32 | eid) over the rank's arcs; after the caller's
 all-reduce MIN, hook to the other fragment of the best edge (mutual pair: smaller label stays
 root), pointer-jump to roots, next active list = roots that had an outgoing edge, ascending
-(the HIP select is order-preserving, so the lists agree across ranks). A level starts with the
+(the HIP select is order-preserving, so the lists agree across ranks); a level closes when that
+list holds at most one fragment. A level starts with the
 fragments that have a level edge on ANY rank: minedge returns None after opening a level, the
 caller OR-combines exchange_buffer() across ranks (all-reduce MAX) and calls minedge again.
 """
@@ -119,7 +120,7 @@ class CpuStepper:
         self.best[:] = KEY_NONE
         self.comp = par[self.comp]
         self.active = np.sort(act[keep])
-        if len(self.active) == 0:
+        if len(self.active) <= 1:  # one fragment left: its remaining level edges are internal
             self.level_open = False
             self.level += 1
             self.done = self.level + 1 >= len(self.thr)

@@ -17,7 +17,7 @@ def short(n):
 
 def main():
     db = sys.argv[1]
-    pat = sys.argv[2] if len(sys.argv) > 2 else r"k_select"
+    pat = sys.argv[2] if len(sys.argv) > 2 else r"^k_select\b(?!_)"
     c = sqlite3.connect(db)
     rows = c.execute("select name, start, end, duration from kernels order by start").fetchall()
     idx = [i for i, r in enumerate(rows) if re.search(pat, r[0].replace("ghs::", ""))]
