@@ -178,6 +178,47 @@ __device__ __forceinline__ void wave_sync_lds() {
 // lane_excl.. in the wave's private LDS region (256 entries), then the wave writes its
 // contiguous output range [out, out + wave_cnt) with coalesced stores (lane i: items i, i + 64,
 // ...) instead of 12 scattered per-lane stores.
+// Buffer resource over [p, p + bytes) (bytes clipped to 2^31 - 1). Loads past the end return 0
+// instead of faulting, so the streaming loops issue every load unconditionally: no branch around
+// a load, hence no path-dependent outstanding-load count, and hipcc's waits stay counted
+// (vmcnt(N)) instead of draining the prefetched tile (cdna_hip_programming.md T8/T20). Built
+// from block-uniform values only.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint64_t bytes) {
+  const int nb = (int)(bytes > 0x7fffffffull ? 0x7fffffffull : bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, nb, 0x00020000);
+}
+
+__device__ __forceinline__ uint4 ld_b128(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 0);
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
+
+__device__ __forceinline__ uint32_t ld_b32(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, 0, 0);
+}
+
+
+// Buffer stores through a resource: a lane whose byte offset is >= the resource's size stores
+// nothing (the bounds check drops it), so a masked store is still ONE instruction issued in
+// every iteration. A streaming loop whose store count per iteration is fixed keeps hipcc's
+// waits counted: with a data-dependent number of stores behind the prefetch loads it emits
+// vmcnt(0) at the loop top, which also waits for every store acknowledgement.
+constexpr uint32_t ST_DROP = 0xffffffffu;  // an offset past every resource
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_u32(const void *p, uint64_t bytes) {
+  const uint32_t nb = (uint32_t)(bytes > 0xfffffffeull ? 0xfffffffeull : bytes);  // < ST_DROP
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)nb, 0x00020000);
+}
+__device__ __forceinline__ void st_b8(uint8_t v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  __builtin_amdgcn_raw_buffer_store_b8(v, r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void st_b32(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void st_b64(uint64_t v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)v, (uint32_t)(v >> 32)}, r, (int)off, 0, 0);
+}
+
 struct WaveStage {
   uint32_t a[WAVE * 4];
   uint32_t b[WAVE * 4];
@@ -204,6 +245,37 @@ __device__ __forceinline__ void stage_write(WaveStage &ws, const uint32_t a[4], 
     oa[out + i] = ws.a[i];
     ob[out + i] = ws.b[i];
     ok[out + i] = ws.k[i];
+  }
+  wave_sync_lds();  // the region is rewritten next iteration
+}
+
+// The same with a fixed store count: 4 rounds of 64 lanes (a wave stages <= 256 entries) to the
+// block's output region through resources based at the region (ra/rb: 4-B entries, rk: 8-B
+// keys); rel = the wave's first entry relative to the region. Lanes past wave_cnt drop.
+__device__ __forceinline__ void stage_write_rs(WaveStage &ws, const uint32_t a[4], const uint32_t b[4],
+                                               const uint64_t k[4], uint32_t mask, uint32_t lane_excl,
+                                               uint32_t wave_cnt, __amdgpu_buffer_rsrc_t ra,
+                                               __amdgpu_buffer_rsrc_t rb, __amdgpu_buffer_rsrc_t rk, uint32_t rel) {
+  uint32_t p = lane_excl;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (mask & (1u << j)) {
+      ws.a[p] = a[j];
+      ws.b[p] = b[j];
+      ws.k[p] = k[j];
+      ++p;
+    }
+  }
+  wave_sync_lds();
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+#pragma unroll
+  for (uint32_t r = 0; r < 4; ++r) {
+    const uint32_t i = lane + WAVE * r;
+    const bool ok = i < wave_cnt;
+    const uint32_t e = rel + i;
+    st_b32(ws.a[i], ra, ok ? e * 4u : ST_DROP);
+    st_b32(ws.b[i], rb, ok ? e * 4u : ST_DROP);
+    st_b64(ws.k[i], rk, ok ? e * 8u : ST_DROP);
   }
   wave_sync_lds();  // the region is rewritten next iteration
 }
@@ -332,7 +404,11 @@ GHS_STREAM_KERNEL void k_minedge(const uint32_t *__restrict__ src, const uint32_
     // b-side: one candidate per live edge
 #pragma unroll
     for (int j = 0; j < 4; ++j)
+#if defined(GHS_EXP_NOBSIDE)
+      if (!IDENT && (smask & (1u << j))) hot_min(s_hl, s_hk, best, D[j], V[j]);
+#else
       if (smask & (1u << j)) hot_min(s_hl, s_hk, best, D[j], V[j]);
+#endif
     // a-side. Deferred run of the previous iteration (wave-uniform carry): a run that reaches
     // the wave's end is not flushed but carried, and merged into the next run of the same label
     // (min is associative, contiguity is not needed).
@@ -744,25 +820,6 @@ __global__ void k_sample_weights(uint64_t cnt, const uint32_t *__restrict__ w, u
   }
 }
 
-// Buffer resource over [p, p + bytes) (bytes clipped to 2^31 - 1). Loads past the end return 0
-// instead of faulting, so the streaming loops issue every load unconditionally: no branch around
-// a load, hence no path-dependent outstanding-load count, and hipcc's waits stay counted
-// (vmcnt(N)) instead of draining the prefetched tile (cdna_hip_programming.md T8/T20). Built
-// from block-uniform values only.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint64_t bytes) {
-  const int nb = (int)(bytes > 0x7fffffffull ? 0x7fffffffull : bytes);
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, nb, 0x00020000);
-}
-
-__device__ __forceinline__ uint4 ld_b128(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
-  const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 0);
-  return make_uint4(x.x, x.y, x.z, x.w);
-}
-
-__device__ __forceinline__ uint32_t ld_b32(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
-  return __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, 0, 0);
-}
-
 // ------------------------------------------------------------------------------------------
 // SELECT (opens level 0): the first full stream over the caller's canonical list [e_lo, e_hi)
 // (u, v, w: 12 B per edge; key = w << 32 | eid built here). The stream runs over the aligned
@@ -793,6 +850,10 @@ GHS_STREAM_KERNEL void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, const 
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(ew + eb, nbytes);
   // the edge before each lane's tile; offset -4 (the block's first tile) is out of range of the
   // descriptor and is replaced by the block's predecessor edge, loaded once
+  // output region [vb, vb + Q) of each array, and the active-fragment marks
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc_u32(osrc + vb, Q * 4), rb = make_rsrc_u32(odst + vb, Q * 4);
+  const __amdgpu_buffer_rsrc_t rk = make_rsrc_u32(okey + vb, Q * 8);
+  const __amdgpu_buffer_rsrc_t rm = make_rsrc_u32(mark, mark ? n : 0);
   uint32_t bpa = 0, bpb = 0;
   if (eb > 0 && ve > vb) {
     bpa = eu[eb - 1];
@@ -803,6 +864,11 @@ GHS_STREAM_KERNEL void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, const 
   bool bad = false;
   uint4 ca = ld_b128(ru, lane_off), cb = ld_b128(rv, lane_off), cw = ld_b128(rw, lane_off);
   uint32_t cpa = ld_b32(ru, lane_off - 4), cpb = ld_b32(rv, lane_off - 4);
+  // Every tile's loads are consumed at the END of the iteration that issued them (the empty
+  // asm "uses" below): the wait then sits behind a fixed number of stores and stays counted,
+  // and the loop header receives no pending load from either edge (a pending prologue load
+  // merged into the header made hipcc drain the stores there on every iteration).
+  asm volatile("" ::"v"(ca.x), "v"(cb.x), "v"(cw.x), "v"(cpa), "v"(cpb));
   for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
     const uint64_t v = v0 + (uint64_t)threadIdx.x * 4;
     const uint64_t e0 = E0 + v;
@@ -841,15 +907,19 @@ GHS_STREAM_KERNEL void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, const 
     for (int j = 0; j < 4; ++j) {
       omask |= out[j] ? (1u << j) : 0u;
       key[j] = ((uint64_t)w[j] << 32) | (uint32_t)(e0 + j);
-      if (mark && out[j]) {  // active fragments of the level
-        mark[a[j]] = 1;
-        mark[b[j]] = 1;
-      }
+#if defined(GHS_EXP_NOMARK)
+#elif defined(GHS_EXP_CONDMARK)
+      if (out[j]) { mark[a[j]] = 1; mark[b[j]] = 1; }
+#else
+      st_b8(1, rm, out[j] ? a[j] : ST_DROP);  // active fragments of the level
+      st_b8(1, rm, out[j] ? b[j] : ST_DROP);
+#endif
     }
     uint32_t le, wb, wc, tot;
     block_offsets_w((uint32_t)__popc(omask), s_wcnt, &le, &wb, &wc, &tot);
-    stage_write(s_stage[threadIdx.x / WAVE], a, b, key, omask, le, wc, osrc, odst, okey, vb + nout + wb);
+    stage_write_rs(s_stage[threadIdx.x / WAVE], a, b, key, omask, le, wc, ra, rb, rk, (uint32_t)(nout + wb));
     nout += tot;
+    asm volatile("" ::"v"(ca.x), "v"(cb.x), "v"(cw.x), "v"(cpa), "v"(cpb));  // next tile landed (see above)
   }
   if (bad) atomicOr(err, 8ull);
   // output regions are padded to a multiple of 4 with dead entries (a = LABEL_NONE)
@@ -1349,12 +1419,20 @@ enum : int {
 };
 
 constexpr int SLOT_RING = 8;
-constexpr int LOOKAHEAD = 2;            // rounds enqueued ahead of the host's termination check
+// rounds enqueued ahead of the host's termination check (GHS_LOOKAHEAD: 0..4). R-MAT s24: 1 ->
+// 6.40-6.43 ms per step, 2 -> 6.48-6.59, 3 -> 6.62 (each extra round of lookahead ends every
+// level with one more no-op round of ~25 us; one round hides the host's reaction time).
+constexpr int LOOKAHEAD = 1;
 constexpr uint32_t LEVEL_ROUND_CAP = 64;  // hang guard: a level takes O(log n) rounds
 
 // Host-side resources of a solve: pinned buffers and timing events. Creating them costs far
 // more than a small solve (page-pinning, event objects), so the one-shot entry point keeps one
 // set per device for the process and reuses it; a stepwise solver handle owns its own.
+// counters: all zero, C_N = n (the vertex count as a device-side item count)
+__global__ void k_init_counters(unsigned long long *cnt, uint32_t n) {
+  for (int i = threadIdx.x; i < C_COUNT; i += blockDim.x) cnt[i] = (i == C_N) ? (unsigned long long)n : 0ull;
+}
+
 struct HostRes {
   unsigned long long *h_cnt = nullptr;  // pinned mirror of the device counters
   RoundSlot *h_slot = nullptr;          // pinned, coherent ring of round reports (host view)
@@ -1362,6 +1440,7 @@ struct HostRes {
   uint32_t *h_sample = nullptr;         // pinned sample buffer
   std::vector<hipEvent_t> ev_pool;      // timing events, 6 per round
   hipEvent_t pass_ev[4] = {};           // the canonical passes' events
+  hipEvent_t plan_ev = nullptr;         // the weight sample has landed in h_sample
   unsigned long long seq = 0;           // round reports issued through h_slot (monotonic across solves)
 };
 
@@ -1372,6 +1451,7 @@ static int hostres_init(HostRes *r) {
   GHS_HIP_CHECK(hipHostGetDevicePointer((void **)&r->d_slot, r->h_slot, 0));
   GHS_HIP_CHECK(hipHostMalloc((void **)&r->h_sample, 16384 * 4, hipHostMallocDefault));
   for (int i = 0; i < 4; ++i) GHS_HIP_CHECK(hipEventCreate(&r->pass_ev[i]));
+  GHS_HIP_CHECK(hipEventCreateWithFlags(&r->plan_ev, hipEventDisableTiming));
   memset(r->h_slot, 0, SLOT_RING * sizeof(RoundSlot));
   return GHS_OK;
 }
@@ -1381,6 +1461,7 @@ static void hostres_free(HostRes *r) {
   r->ev_pool.clear();
   for (int i = 0; i < 4; ++i)
     if (r->pass_ev[i]) (void)hipEventDestroy(r->pass_ev[i]);
+  if (r->plan_ev) (void)hipEventDestroy(r->plan_ev);
   if (r->h_cnt) (void)hipHostFree(r->h_cnt);
   if (r->h_slot) (void)hipHostFree(r->h_slot);
   if (r->h_sample) (void)hipHostFree(r->h_sample);
@@ -1449,6 +1530,7 @@ struct ghs_solver {
   bool detail = false;          // GHS_DETAIL=1: time every stage (adds ~5.7 us per event)
   bool time_rounds = false;     // GHS_TIME_ROUNDS=1: time the compacting min-edge launches (bench)
   uint32_t seg_g = SEG_G;       // blocks of the streaming kernels (GHS_SEG_G, 256..SEG_G)
+  uint32_t lookahead = LOOKAHEAD;  // rounds in flight ahead of the termination check (GHS_LOOKAHEAD)
   std::chrono::steady_clock::time_point t0;
 };
 
@@ -1574,25 +1656,42 @@ static void default_config(ghs_config_t *c) {
 }
 
 // ---- level planning: thresholds from a sample of the GLOBAL canonical weights ----------------
-static int plan_levels(ghs_solver *s) {
-  s->thresholds.clear();
-  s->thresholds.push_back(0);
-  const uint32_t L = std::max<uint32_t>(1, std::min<uint32_t>(s->cfg.max_levels, 32));
-  if (L > 1 && s->m > 0) {
+// Split so the host's quantile selection overlaps the solver's init kernels: the sample and its
+// copy are enqueued first (plan_levels_enqueue), the host waits for them alone (plan_ev) while
+// the GPU clears its arrays, then picks the thresholds (plan_levels_finish).
+static uint32_t plan_levels_count(const ghs_solver *s) {
+  return std::max<uint32_t>(1, std::min<uint32_t>(s->cfg.max_levels, 32));
+}
+
+static int plan_levels_enqueue(ghs_solver *s) {
+  if (plan_levels_count(s) > 1 && s->m > 0) {
     const uint32_t ns = (uint32_t)std::min<uint64_t>(NSAMPLE_W, s->m);
     k_sample_weights<<<grid_for(ns, 256, 256), 256, 0, s->stream>>>(s->m, s->ew, ns, s->sample);
     GHS_HIP_CHECK(hipGetLastError());
     GHS_HIP_CHECK(hipMemcpyAsync(s->h_sample, s->sample, ns * 4, hipMemcpyDeviceToHost, s->stream));
-    GHS_HIP_CHECK(hipStreamSynchronize(s->stream));
+    GHS_HIP_CHECK(hipEventRecord(s->res->plan_ev, s->stream));
+  }
+  return GHS_OK;
+}
+
+static int plan_levels_finish(ghs_solver *s) {
+  s->thresholds.clear();
+  s->thresholds.push_back(0);
+  const uint32_t L = plan_levels_count(s);
+  if (L > 1 && s->m > 0) {
+    const uint32_t ns = (uint32_t)std::min<uint64_t>(NSAMPLE_W, s->m);
+    GHS_HIP_CHECK(hipEventSynchronize(s->res->plan_ev));
     std::vector<uint32_t> w(s->h_sample, s->h_sample + ns);
     double target = s->cfg.level1_edges_per_vertex * (double)s->n;
+    size_t lo = 0;  // quantiles ascend: each selection works on the part above the last one
     for (uint32_t i = 1; i < L; ++i) {
       const double frac = target / (double)s->m;
       if (frac >= 1.0) break;
       const size_t q = (size_t)(frac * ns);
       target *= std::max(1.01, s->cfg.level_growth);
-      if (q == 0) continue;
-      std::nth_element(w.begin(), w.begin() + q, w.end());
+      if (q == 0 || q < lo) continue;
+      std::nth_element(w.begin() + lo, w.begin() + q, w.end());
+      lo = q;
       const uint64_t thr = (uint64_t)w[q];
       if (thr > s->thresholds.back()) s->thresholds.push_back(thr);
     }
@@ -1859,9 +1958,9 @@ static int run_level_pipelined(ghs_solver *s) {
   const uint32_t round0 = s->round;
   uint64_t live_prev = s->cur_arcs, nact_prev = s->level_nact;  // inputs of the next checked round
   uint32_t issued = 0, checked = 0;
-  std::vector<unsigned long long> seqs(LEVEL_ROUND_CAP + LOOKAHEAD + 1);
+  std::vector<unsigned long long> seqs(LEVEL_ROUND_CAP + s->lookahead + 1);
   for (;;) {
-    if (issued < checked + 1 + LOOKAHEAD) {
+    if (issued < checked + 1 + s->lookahead) {
       if (issued >= LEVEL_ROUND_CAP) GHS_FAIL(GHS_E_ROUNDCAP, "round cap exceeded in a level");
       const unsigned long long seq = ++s->res->seq;
       seqs[issued] = seq;
@@ -1944,6 +2043,10 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   { const char *dbg = getenv("GHS_DEBUG"); s->debug = dbg && dbg[0] == '1'; }
   { const char *det = getenv("GHS_DETAIL"); s->detail = det && det[0] == '1'; }
   { const char *tr = getenv("GHS_TIME_ROUNDS"); s->time_rounds = tr && tr[0] == '1'; }
+  if (const char *la = getenv("GHS_LOOKAHEAD")) {  // A/B tests: rounds in flight ahead of the check
+    const long v = strtol(la, nullptr, 10);
+    s->lookahead = (uint32_t)(v < 0 ? 0 : (v > 4 ? 4 : v));
+  }
   if (const char *g = getenv("GHS_SEG_G")) {  // A/B tests: blocks of the streaming kernels
     const long v = strtol(g, nullptr, 10);
     s->seg_g = (uint32_t)(v < 256 ? 256 : (v > (long)SEG_G ? SEG_G : v));
@@ -1970,6 +2073,11 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   s->d_slot = s->res->d_slot;
   s->h_sample = s->res->h_sample;
   s->t0 = std::chrono::steady_clock::now();
+  int rc = plan_levels_enqueue(s);
+  if (rc) {
+    ghs_solver_destroy(s);
+    return rc;
+  }
   if (n) {
     if ((e = hipMemsetAsync(s->best, 0xff, (size_t)n * 8, s->stream)) != hipSuccess) return fail(e, "memset best");
     k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->lab, n);
@@ -1977,13 +2085,9 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   }
   if (m && (e = hipMemsetAsync(s->in_mst, 0, m, s->stream)) != hipSuccess) return fail(e, "memset in_mst");
   if ((e = hipMemsetAsync(s->lb_state, 0, LB_MAX_TILES * 8, s->stream)) != hipSuccess) return fail(e, "memset select state");
-  if ((e = hipMemsetAsync(s->cnt, 0, C_COUNT * sizeof(unsigned long long), s->stream)) != hipSuccess)
-    return fail(e, "memset counters");
-  const unsigned long long nn = n;
-  if ((e = hipMemcpyAsync(s->cnt + C_N, &nn, 8, hipMemcpyHostToDevice, s->stream)) != hipSuccess)
-    return fail(e, "counter init");
+  k_init_counters<<<1, 64, 0, s->stream>>>(s->cnt, n);
   if ((e = hipGetLastError()) != hipSuccess) return fail(e, "init kernels");
-  int rc = plan_levels(s);  // syncs the stream (nn stays valid until then)
+  rc = plan_levels_finish(s);  // waits for the weight sample only
   if (rc) {
     ghs_solver_destroy(s);
     return rc;

@@ -21,7 +21,10 @@ def main():
     c = sqlite3.connect(db)
     rows = c.execute("select name, start, end, duration from kernels order by start").fetchall()
     idx = [i for i, r in enumerate(rows) if re.search(pat, r[0].replace("ghs::", ""))]
-    s = idx[-1]
+    occ = int(sys.argv[3]) if len(sys.argv) > 3 else -1  # which step (-1: the last)
+    s = idx[occ]
+    e = idx[occ + 1] if occ + 1 < 0 else len(rows)  # up to the next step's marker
+    rows = rows[:e]
     t0 = rows[s][1]
     prev = t0
     busy = 0
