@@ -404,11 +404,7 @@ GHS_STREAM_KERNEL void k_minedge(const uint32_t *__restrict__ src, const uint32_
     // b-side: one candidate per live edge
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-#if defined(GHS_EXP_NOBSIDE)
-      if (!IDENT && (smask & (1u << j))) hot_min(s_hl, s_hk, best, D[j], V[j]);
-#else
       if (smask & (1u << j)) hot_min(s_hl, s_hk, best, D[j], V[j]);
-#endif
     // a-side. Deferred run of the previous iteration (wave-uniform carry): a run that reaches
     // the wave's end is not flushed but carried, and merged into the next run of the same label
     // (min is associative, contiguity is not needed).
@@ -540,12 +536,43 @@ __device__ __forceinline__ uint32_t find_lab(const uint32_t *__restrict__ lab, u
 // ghs_implementation.py:186-196, initiator by (fragment_id, rank), ghs_implementation_mpi.py:
 // 237-239). Every hook adds exactly one MSF edge; one pair of atomics per block for the totals.
 // ------------------------------------------------------------------------------------------
+// Exclusive scan of count[0..n) into prefix[0..n] (prefix[n] = *total) by ONE 256-thread block.
+// k_hook's last block runs it for the compaction of the same round (the consumers — the next
+// round's min-edge and the round report — run later), which saves a launch per round.
+__device__ void block_scan_counts(const uint64_t *__restrict__ count, uint32_t n, uint64_t *__restrict__ prefix,
+                                  unsigned long long *__restrict__ total) {
+  __shared__ uint64_t s_part[BLOCK];
+  const uint32_t per = (n + BLOCK - 1) / BLOCK;
+  const uint32_t b = threadIdx.x * per;
+  uint64_t sum = 0;
+  for (uint32_t i = 0; i < per && b + i < n; ++i) sum += count[b + i];
+  s_part[threadIdx.x] = sum;
+  __syncthreads();
+  for (int d = 1; d < BLOCK; d <<= 1) {
+    const uint64_t o = threadIdx.x >= (unsigned)d ? s_part[threadIdx.x - d] : 0;
+    __syncthreads();
+    s_part[threadIdx.x] += o;
+    __syncthreads();
+  }
+  uint64_t run = s_part[threadIdx.x] - sum;
+  for (uint32_t i = 0; i < per && b + i < n; ++i) {
+    prefix[b + i] = run;
+    run += count[b + i];
+  }
+  if (threadIdx.x == BLOCK - 1) {
+    prefix[n] = s_part[BLOCK - 1];
+    *total = s_part[BLOCK - 1];
+  }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
                                                 const uint64_t *__restrict__ best, const uint32_t *__restrict__ lab,
                                                 const uint32_t *__restrict__ eu, const uint32_t *__restrict__ ev,
                                                 uint32_t *__restrict__ par, uint8_t *__restrict__ in_mst,
                                                 unsigned long long *__restrict__ acc /* [0] weight, [1] edges */,
-                                                unsigned long long *__restrict__ err) {
+                                                unsigned long long *__restrict__ err,
+                                                const uint64_t *__restrict__ scan_count, uint32_t scan_n,
+                                                uint64_t *__restrict__ scan_prefix, unsigned long long *__restrict__ scan_total) {
   __shared__ unsigned long long s_w[BLOCK / WAVE], s_c[BLOCK / WAVE];
   unsigned long long wsum = 0, cnt = 0;
   const uint64_t nact = *d_nact;
@@ -592,6 +619,7 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
       atomicAdd(acc + 1, tc);
     }
   }
+  if (scan_count && blockIdx.x == gridDim.x - 1) block_scan_counts(scan_count, scan_n, scan_prefix, scan_total);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -850,10 +878,9 @@ GHS_STREAM_KERNEL void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, const 
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(ew + eb, nbytes);
   // the edge before each lane's tile; offset -4 (the block's first tile) is out of range of the
   // descriptor and is replaced by the block's predecessor edge, loaded once
-  // output region [vb, vb + Q) of each array, and the active-fragment marks
+  // output region [vb, vb + Q) of each array
   const __amdgpu_buffer_rsrc_t ra = make_rsrc_u32(osrc + vb, Q * 4), rb = make_rsrc_u32(odst + vb, Q * 4);
   const __amdgpu_buffer_rsrc_t rk = make_rsrc_u32(okey + vb, Q * 8);
-  const __amdgpu_buffer_rsrc_t rm = make_rsrc_u32(mark, mark ? n : 0);
   uint32_t bpa = 0, bpb = 0;
   if (eb > 0 && ve > vb) {
     bpa = eu[eb - 1];
@@ -907,13 +934,10 @@ GHS_STREAM_KERNEL void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, const 
     for (int j = 0; j < 4; ++j) {
       omask |= out[j] ? (1u << j) : 0u;
       key[j] = ((uint64_t)w[j] << 32) | (uint32_t)(e0 + j);
-#if defined(GHS_EXP_NOMARK)
-#elif defined(GHS_EXP_CONDMARK)
-      if (out[j]) { mark[a[j]] = 1; mark[b[j]] = 1; }
-#else
-      st_b8(1, rm, out[j] ? a[j] : ST_DROP);  // active fragments of the level
-      st_b8(1, rm, out[j] ? b[j] : ST_DROP);
-#endif
+      if (mark && out[j]) {  // active fragments of the level (~3% of the edges: branched, measured
+        mark[a[j]] = 1;  // faster than 8 unconditional dropped-lane stores per tile)
+        mark[b[j]] = 1;
+      }
     }
     uint32_t le, wb, wc, tot;
     block_offsets_w((uint32_t)__popc(omask), s_wcnt, &le, &wb, &wc, &tot);
@@ -1237,23 +1261,35 @@ constexpr int C_ERR_IDX = 4;  // == C_ERR (counter layout below)
 struct RoundSlot {
   unsigned long long live_out, nact_out, edges, err;
   unsigned long long seq;
-  unsigned long long pad[3];
+  unsigned long long nact_in;  // active fragments this round started from (a level's first round: the level's)
+  unsigned long long pending;  // pending edges after the level's pass (counter C_PENDING)
+  unsigned long long pad;
 };
 
 __device__ __forceinline__ void write_report(RoundSlot *slot, unsigned long long seq, const unsigned long long *cnt,
-                                             unsigned long long nact_out) {
+                                             unsigned long long nact_out, unsigned long long nact_in) {
   // device-scope loads: the error bits may come from other workgroups of the writing launch
-  slot->live_out = __hip_atomic_load(cnt + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // live edges after this round's compaction
-  slot->nact_out = nact_out;                                                               // active fragments of the next round
-  slot->edges = __hip_atomic_load(cnt + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);    // MSF edges so far
-  slot->err = __hip_atomic_load(cnt + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);      // error bits
-  __threadfence_system();
+  const unsigned long long live = __hip_atomic_load(cnt + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long edges = __hip_atomic_load(cnt + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long err = __hip_atomic_load(cnt + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long pending = __hip_atomic_load(cnt + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // The slot is coherent (uncached) host memory: its stores bypass the L2, so draining them
+  // (vmcnt(0)) before the seq store orders them for the host's acquire load of seq. No
+  // __threadfence_system(): its L2 write-back of every dirty line held the next round's first
+  // kernel back by ~6 us (measured, every round).
+  slot->live_out = live;          // live edges after this round's compaction
+  slot->nact_out = nact_out;      // active fragments of the next round
+  slot->edges = edges;            // MSF edges so far
+  slot->err = err;                // error bits
+  slot->nact_in = nact_in;
+  slot->pending = pending;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(&slot->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ void k_round_report(RoundSlot *slot, unsigned long long seq, const unsigned long long *cnt,
-                               const unsigned long long *nact_out) {
-  write_report(slot, seq, cnt, *nact_out);
+                               const unsigned long long *nact_out, const unsigned long long *nact_in) {
+  write_report(slot, seq, cnt, *nact_out, *nact_in);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1378,7 +1414,7 @@ __global__ __launch_bounds__(BLOCK) void k_select_lb(const uint8_t *__restrict__
   }
   if (t == gridDim.x - 1 && threadIdx.x == 0) {
     *d_total = s_excl + tot;
-    if (slot) write_report(slot, seq, cnt, s_excl + tot);
+    if (slot) write_report(slot, seq, cnt, s_excl + tot, count);
   }
 }
 
@@ -1417,6 +1453,7 @@ enum : int {
   C_ACT = 8,      // [8], [9]: lengths of the active lists act[0], act[1]
   C_COUNT = 16
 };
+static_assert(C_ERR == 4 && C_PENDING == 5, "write_report reads the counters by index");
 
 constexpr int SLOT_RING = 8;
 // rounds enqueued ahead of the host's termination check (GHS_LOOKAHEAD: 0..4). R-MAT s24: 1 ->
@@ -1530,6 +1567,10 @@ struct ghs_solver {
   bool detail = false;          // GHS_DETAIL=1: time every stage (adds ~5.7 us per event)
   bool time_rounds = false;     // GHS_TIME_ROUNDS=1: time the compacting min-edge launches (bench)
   uint32_t seg_g = SEG_G;       // blocks of the streaming kernels (GHS_SEG_G, 256..SEG_G)
+  bool open_async = false;      // the open level's counts arrive with its first round's report
+  bool scan_pending = false;    // the last compaction's region counts are not scanned yet
+  const ArcBuf *scan_buf = nullptr;
+  bool arcs_known = true;       // cur_arcs holds the exact live edge count (else: unknown, grids sized for the bound)
   uint32_t lookahead = LOOKAHEAD;  // rounds in flight ahead of the termination check (GHS_LOOKAHEAD)
   std::chrono::steady_clock::time_point t0;
 };
@@ -1633,7 +1674,7 @@ static int select_lb(ghs_solver *s, const uint32_t *act, const unsigned long lon
                      uint32_t *out, unsigned long long *d_total, RoundSlot *slot = nullptr, unsigned long long seq = 0) {
   if (bound == 0) {
     GHS_HIP_CHECK(hipMemsetAsync(d_total, 0, 8, s->stream));
-    if (slot) k_round_report<<<1, 1, 0, s->stream>>>(slot, seq, s->cnt, d_total);
+    if (slot) k_round_report<<<1, 1, 0, s->stream>>>(slot, seq, s->cnt, d_total, d_count);
     GHS_HIP_CHECK(hipGetLastError());
     return GHS_OK;
   }
@@ -1711,7 +1752,9 @@ static int open_level_finish(ghs_solver *s);
 // ---- open the next level: select its edges, set its active list (one host sync) --------------
 // Returns GHS_OK with s->level_open set, with the level skipped (no edges), or — several ranks —
 // with s->pending_exchange set (the caller OR-combines the flags, then open_level_finish).
-static int open_level(ghs_solver *s) {
+static int open_level_async(ghs_solver *s);
+
+static int open_level(ghs_solver *s, bool async_open = false) {
   const uint32_t lv = s->level;
   const uint64_t w_hi = s->thresholds[lv + 1];
   const bool first = (lv == 0);
@@ -1796,7 +1839,7 @@ static int open_level(ghs_solver *s) {
     return GHS_OK;
   }
   s->open_G = G;
-  return open_level_finish(s);
+  return async_open ? open_level_async(s) : open_level_finish(s);
 }
 
 // ---- second half of opening a level: the active list and the one host sync ------------------
@@ -1842,9 +1885,36 @@ static int open_level_finish(ghs_solver *s) {
   return GHS_OK;
 }
 
+// ---- single rank: open the level without a host sync ---------------------------------------
+// The active list is selected on the device and the level's first round is enqueued right
+// behind it; the level's counts (edges, active fragments, pending edges, errors) come back with
+// that round's report (run_level_pipelined). Until then the grids are sized for the bounds
+// (n fragments, the streaming grid for the edges). An empty level runs one no-op round.
+static int open_level_async(ghs_solver *s) {
+  if (int rc = select_lb(s, nullptr, s->cnt + C_N, s->n, s->act[0], s->cnt + C_ACT)) return rc;
+  s->act_ident = false;
+  s->act_cur = 0;
+  s->nact = s->n;  // bound
+  s->level_nact = s->n;
+  s->cur = 1;
+  s->cur_nseg = s->open_G;
+  s->cur_arcs = 0;
+  s->arcs_known = false;
+  s->open_async = true;
+  s->level_round = 0;
+  s->level_open = true;
+  return GHS_OK;
+}
+
 static inline unsigned long long *act_count(ghs_solver *s, int which) { return s->cnt + C_ACT + which; }
 static inline const unsigned long long *cur_act_count(ghs_solver *s) {
   return s->act_ident ? s->cnt + C_N : act_count(s, s->act_cur);
+}
+
+// the pending region scan as its own launch (when no hook kernel follows to carry it)
+static void flush_scan(ghs_solver *s) {
+  k_scan_counts<<<1, 1024, 0, s->stream>>>(s->scan_buf->seg_count, s->seg_g, s->scan_buf->seg_prefix, s->cnt + C_LIVE);
+  s->scan_pending = false;
 }
 
 // ---- one round, enqueued without a host sync (sizes on the device; s->nact is a bound) --------
@@ -1855,14 +1925,17 @@ static int enqueue_minedge(ghs_solver *s) {
   ArcBuf &O = s->buf[s->cur ^ 1];
   SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
   if (s->level_round == 0) {
-    if (s->cur_arcs)
-      k_minedge<true, false><<<grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->seg_g), BLOCK, 0, s->stream>>>(
+    if (s->cur_arcs || !s->arcs_known)
+      k_minedge<true, false><<<s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->seg_g) : s->seg_g, BLOCK, 0, s->stream>>>(
           I.src, I.dst, I.key, in, s->lab, s->best, nullptr, nullptr, nullptr, nullptr, nullptr);
   } else {
     // fixed grid: every one of the seg_g blocks writes its region's count
     k_minedge<false, true><<<s->seg_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, O.src, O.dst,
                                                           O.key, O.seg_start, O.seg_count);
-    k_scan_counts<<<1, 1024, 0, s->stream>>>(O.seg_count, s->seg_g, O.seg_prefix, s->cnt + C_LIVE);
+    // the regions' prefix scan is left to the round's hook kernel (or a scan launch before the
+    // next consumer): s->scan_pending
+    s->scan_pending = true;
+    s->scan_buf = &O;
   }
   GHS_HIP_CHECK(hipGetLastError());
   if (timed) record(s, 1);
@@ -1876,19 +1949,24 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
   const uint64_t bound = s->nact;
   const int nb = s->act_ident ? 0 : (s->act_cur ^ 1);
   if (bound) {
-    const unsigned g = grid_for(bound, BLOCK, 65535);
+    const unsigned g = grid_for(bound, BLOCK, 16384);  // grid-stride beyond 4M fragments
     // CONNECT: edge form while fragments are many and small (a level's first round: its edges
     // carry the current roots), fragment form otherwise (and always with several ranks: a
     // fragment's best edge may live on another rank)
-    const bool edge_form = s->cfg.num_ranks <= 1 && s->level_round == 0 && s->cur_arcs < 8 * bound;
+    const bool edge_form =
+        s->cfg.num_ranks <= 1 && s->level_round == 0 && (!s->arcs_known || s->cur_arcs < 8 * bound);
+    if (edge_form && s->scan_pending) flush_scan(s);
     if (edge_form) {
       const ArcBuf &I = s->buf[s->cur];
       SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
-      k_win<<<grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->seg_g), BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->best,
+      k_win<<<s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->seg_g) : s->seg_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->best,
                                                                                    s->par, s->in_mst, s->cnt + C_WEIGHT);
     } else {
+      const ArcBuf *sb = s->scan_pending ? s->scan_buf : nullptr;
       k_hook<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
-                                         s->cnt + C_WEIGHT, s->cnt + C_ERR);
+                                         s->cnt + C_WEIGHT, s->cnt + C_ERR, sb ? sb->seg_count : nullptr, s->seg_g,
+                                         sb ? sb->seg_prefix : nullptr, s->cnt + C_LIVE);
+      s->scan_pending = false;
     }
     GHS_HIP_CHECK(hipGetLastError());
     if (s->detail) record(s, 2);
@@ -1898,6 +1976,7 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
     if (s->detail) record(s, 3);
     if (int rc = select_lb(s, act, d_nact, bound, s->act[nb], act_count(s, nb), slot, seq)) return rc;
   } else {
+    if (s->scan_pending) flush_scan(s);
     if (int rc = select_lb(s, act, d_nact, 0, s->act[nb], act_count(s, nb), slot, seq)) return rc;
   }
   if (s->detail) record(s, 4);
@@ -1977,7 +2056,30 @@ static int run_level_pipelined(ghs_solver *s) {
     r.nact_out = hs->nact_out;
     r.edges = hs->edges;
     r.err = hs->err;
+    r.nact_in = hs->nact_in;
+    r.pending = hs->pending;
     if (r.err) return fail_counters(s, r.err, ("in round " + std::to_string(round0 + checked + 1)).c_str());
+    if (checked == 0 && s->open_async) {  // the level's counts, from its first round
+      const uint64_t S = r.live_out;  // round 0 does not compact: its live edges are the level's
+      s->open_async = false;
+      s->arcs_known = true;
+      s->cur_arcs = S;
+      s->level_arcs = S;
+      s->rem_total = r.pending;
+      s->level_nact = r.nact_in;
+      live_prev = S;
+      nact_prev = r.nact_in;
+      if (s->level == 0) s->select_out = S;
+      else if (s->filter_run && !s->filter_out) s->filter_out = S + s->rem_total;
+      if (s->debug) {
+        uint32_t g[2] = {0, 0};
+        (void)hipMemcpy(g, s->giant, 8, hipMemcpyDeviceToHost);
+        fprintf(stderr, "[ghs] level %u open: level_edges=%llu active=%llu pending_after=%llu giant=%u (%u/2048 sampled)\n",
+                s->level, (unsigned long long)S, (unsigned long long)r.nact_in, (unsigned long long)s->rem_total,
+                s->level ? g[0] : 0u, s->level ? g[1] : 0u);
+      }
+      if (r.nact_in == 0) break;  // no edge in this level: its rounds were no-ops (checked stays 0)
+    }
     push_stats(s, checked, live_prev, nact_prev, r.edges);
     // the live edges of round k + 1: round 0 does not compact (its input is read again)
     live_prev = checked == 0 ? live_prev : r.live_out;
@@ -2257,12 +2359,8 @@ int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *
         s->phase = 2;
         break;
       }
-      rc = open_level(s);
+      rc = open_level(s, /*async_open=*/true);  // no host sync: the counts come with round 0
       if (rc) break;
-      if (!s->level_open) {
-        s->level += 1;  // skipped (no edges)
-        continue;
-      }
     }
     rc = run_level_pipelined(s);
   }
