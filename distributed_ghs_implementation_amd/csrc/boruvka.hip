@@ -976,6 +976,7 @@ GHS_STREAM_KERNEL void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, const 
 GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__restrict__ eu,
                                 const uint32_t *__restrict__ ev, const uint32_t *__restrict__ ew, uint64_t w_lo,
                                 uint64_t w_hi, const uint64_t *__restrict__ giant_bits,
+                                const uint32_t *__restrict__ giant_ptr,
                                 const uint32_t *__restrict__ lab, uint32_t *__restrict__ lsrc,
                                 uint32_t *__restrict__ ldst, uint64_t *__restrict__ lkey,
                                 uint64_t *__restrict__ lstart, uint64_t *__restrict__ lcount,
@@ -997,6 +998,7 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
   const uint32_t lane_off = threadIdx.x * 16u;
   const uint4 *bits4 = reinterpret_cast<const uint4 *>(giant_bits);
   const uint32_t *bits32 = reinterpret_cast<const uint32_t *>(giant_bits);
+  const uint32_t giant = giant_ptr[0];
   uint64_t nlev = 0, nrem = 0;
   uint4 ca = ld_b128(ru, lane_off), cb = ld_b128(rv, lane_off), cw = ld_b128(rw, lane_off);
   for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
@@ -1026,6 +1028,7 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
     ca = ld_b128(ru, noff);
     cb = ld_b128(rv, noff);
     cw = ld_b128(rw, noff);
+    uint32_t ga[4], gb[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t blk = a[j] >> 7, wsel = (a[j] >> 5) & 3;
@@ -1033,11 +1036,12 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
       const bool odd = wsel & 1;  // two-level select (an == chain becomes a branch tree)
       const uint32_t lo = odd ? q.y : q.x, hi = odd ? q.w : q.z;
       const uint32_t word = (wsel & 2) ? hi : lo;
-      const uint32_t ga = ((blk == A0) | (blk == A3)) ? (word >> (a[j] & 31)) & 1u : 0u;
-      const uint32_t gb = (gbw[j] >> (b[j] & 31)) & 1u;
-      out[j] = out[j] & ((ga & gb) == 0u);  // bitwise (no && : keeps the probes unsunk)
+      ga[j] = ((blk == A0) | (blk == A3)) ? (word >> (a[j] & 31)) & 1u : 0u;
+      gb[j] = (gbw[j] >> (b[j] & 31)) & 1u;
+      out[j] = out[j] & ((ga[j] & gb[j]) == 0u);  // bitwise (no && : keeps the probes unsunk)
     }
-    // level-1 split: labels only for this level's edges
+    // level-1 split: labels only for this level's edges, and only for ends outside the giant
+    // (a set bit IS lab[x] == giant: the bitmap was built from the same labels)
     bool lev[4], rem[4];
     uint32_t la[4], lb[4];
     uint64_t key[4];
@@ -1045,8 +1049,10 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
     for (int j = 0; j < 4; ++j) {
       lev[j] = out[j] & ((uint64_t)w[j] < w_hi);
       rem[j] = out[j] & !lev[j];
-      la[j] = lab[lev[j] ? a[j] : 0u];
-      lb[j] = lab[lev[j] ? b[j] : 0u];
+      la[j] = lab[(lev[j] & (ga[j] == 0u)) ? a[j] : 0u];
+      lb[j] = lab[(lev[j] & (gb[j] == 0u)) ? b[j] : 0u];
+      la[j] = ga[j] ? giant : la[j];
+      lb[j] = gb[j] ? giant : lb[j];
       key[j] = ((uint64_t)w[j] << 32) | (uint32_t)(e0 + j);
     }
     uint32_t lmask = 0, rmask = 0;
@@ -1101,6 +1107,7 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
 GHS_STREAM_KERNEL void k_level_pass(const uint32_t *__restrict__ ru, const uint32_t *__restrict__ rv,
                                     const uint64_t *__restrict__ rkey, SegView in, uint64_t w_hi,
                                     const uint32_t *__restrict__ lab, const uint64_t *__restrict__ giant_bits,
+                                    const uint32_t *__restrict__ giant_ptr,
                                     uint32_t *__restrict__ lsrc, uint32_t *__restrict__ ldst,
                                     uint64_t *__restrict__ lkey, uint64_t *__restrict__ lstart,
                                     uint64_t *__restrict__ lcount, uint32_t *__restrict__ ou, uint32_t *__restrict__ ov, uint64_t *__restrict__ okey,
@@ -1129,6 +1136,7 @@ GHS_STREAM_KERNEL void k_level_pass(const uint32_t *__restrict__ ru, const uint3
   };
   const uint4 *bits4 = reinterpret_cast<const uint4 *>(giant_bits);
   const uint32_t *bits32 = reinterpret_cast<const uint32_t *>(giant_bits);
+  const uint32_t giant = giant_ptr[0];
   uint64_t nlev = 0, nrem = 0;
   uint64_t i0 = tile_index(vb + (uint64_t)threadIdx.x * 4);
   uint4 ca = *reinterpret_cast<const uint4 *>(ru + i0), cb = *reinterpret_cast<const uint4 *>(rv + i0);
@@ -1159,6 +1167,7 @@ GHS_STREAM_KERNEL void k_level_pass(const uint32_t *__restrict__ ru, const uint3
     ck01 = *reinterpret_cast<const ulonglong2 *>(rkey + i0);
     ck23 = *reinterpret_cast<const ulonglong2 *>(rkey + i0 + 2);
     // REJECT a whole class at once: both ends in the giant fragment
+    uint32_t ga[4], gb[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t blk = a[j] >> 7, wsel = (a[j] >> 5) & 3;
@@ -1166,9 +1175,9 @@ GHS_STREAM_KERNEL void k_level_pass(const uint32_t *__restrict__ ru, const uint3
       const bool odd = wsel & 1;
       const uint32_t lo = odd ? q.y : q.x, hi = odd ? q.w : q.z;
       const uint32_t word = (wsel & 2) ? hi : lo;
-      const uint32_t ga = ((blk == A0) | (blk == A3)) ? (word >> (a[j] & 31)) & 1u : 0u;
-      const uint32_t gb = (gbw[j] >> (b[j] & 31)) & 1u;
-      live[j] = live[j] & ((ga & gb) == 0u);
+      ga[j] = ((blk == A0) | (blk == A3)) ? (word >> (a[j] & 31)) & 1u : 0u;
+      gb[j] = (gbw[j] >> (b[j] & 31)) & 1u;
+      live[j] = live[j] & ((ga[j] & gb[j]) == 0u);
     }
     // level/remaining split; labels are gathered only for this level's edges (they become arcs
     // and need the fragment test) — heavier edges are carried forward raw, the bitmap of the
@@ -1179,8 +1188,10 @@ GHS_STREAM_KERNEL void k_level_pass(const uint32_t *__restrict__ ru, const uint3
       const bool in_level = (k[j] >> 32) < w_hi;
       lev[j] = live[j] & in_level;
       rem[j] = live[j] & !in_level;
-      la[j] = lab[lev[j] ? a[j] : 0u];
-      lb[j] = lab[lev[j] ? b[j] : 0u];
+      la[j] = lab[(lev[j] & (ga[j] == 0u)) ? a[j] : 0u];  // ends in the giant: no gather
+      lb[j] = lab[(lev[j] & (gb[j] == 0u)) ? b[j] : 0u];
+      la[j] = ga[j] ? giant : la[j];
+      lb[j] = gb[j] ? giant : lb[j];
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) lev[j] = lev[j] & (la[j] != lb[j]);
@@ -1800,7 +1811,7 @@ static int open_level(ghs_solver *s, bool async_open = false) {
       G = grid_for(TC, ARCS_PER_BLOCK, s->seg_g);
       if (TC) {
         GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[2], st));
-        k_filter<<<G, BLOCK, 0, st>>>(s->e_lo, s->e_hi, s->eu, s->ev, s->ew, s->thresholds[lv], w_hi, s->bits, s->lab,
+        k_filter<<<G, BLOCK, 0, st>>>(s->e_lo, s->e_hi, s->eu, s->ev, s->ew, s->thresholds[lv], w_hi, s->bits, s->giant, s->lab,
                                       Y.src, Y.dst, Y.key, Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key,
                                       RO.seg_start, RO.seg_count, mark);
         GHS_HIP_CHECK(hipGetLastError());
@@ -1821,7 +1832,7 @@ static int open_level(ghs_solver *s, bool async_open = false) {
       // heavier survivors -> RO regions. Fixed grid: block b owns 1/seg_g of the virtual range.
       G = s->seg_g;
       SegView in{RI.seg_start, RI.seg_prefix, s->rem_nseg};
-      k_level_pass<<<G, BLOCK, 0, st>>>(RI.src, RI.dst, RI.key, in, w_hi, s->lab, s->bits, Y.src, Y.dst, Y.key,
+      k_level_pass<<<G, BLOCK, 0, st>>>(RI.src, RI.dst, RI.key, in, w_hi, s->lab, s->bits, s->giant, Y.src, Y.dst, Y.key,
                                         Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key, RO.seg_start, RO.seg_count,
                                         mark);
       GHS_HIP_CHECK(hipGetLastError());
