@@ -999,6 +999,7 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
   const uint4 *bits4 = reinterpret_cast<const uint4 *>(giant_bits);
   const uint32_t *bits32 = reinterpret_cast<const uint32_t *>(giant_bits);
   const uint32_t giant = giant_ptr[0];
+  bool touch_giant = false;  // a level edge of this block has an end in the giant
   uint64_t nlev = 0, nrem = 0;
   uint4 ca = ld_b128(ru, lane_off), cb = ld_b128(rv, lane_off), cw = ld_b128(rw, lane_off);
   for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
@@ -1061,9 +1062,10 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
       lev[j] = lev[j] & (la[j] != lb[j]);
       lmask |= lev[j] ? (1u << j) : 0u;
       rmask |= rem[j] ? (1u << j) : 0u;
-      if (lev[j] && mark) {  // active fragments of the level
-        mark[la[j]] = 1;
-        mark[lb[j]] = 1;
+      if (lev[j] && mark) {  // active fragments of the level; the giant's flag once per block
+        if (!ga[j]) mark[la[j]] = 1;
+        if (!gb[j]) mark[lb[j]] = 1;
+        touch_giant |= (ga[j] | gb[j]) != 0u;
       }
     }
     uint32_t le, wb, wc, tlev, trem;
@@ -1074,6 +1076,7 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
     nlev += tlev;
     nrem += trem;
   }
+  if (__syncthreads_or(touch_giant ? 1 : 0) && threadIdx.x == 0 && mark) mark[giant] = 1;
   // both outputs padded to a multiple of 4 with dead entries (a = LABEL_NONE)
   const uint64_t padded = (nrem + 3) & ~3ull, lpadded = (nlev + 3) & ~3ull;
   if (threadIdx.x < padded - nrem) {
@@ -1137,6 +1140,7 @@ GHS_STREAM_KERNEL void k_level_pass(const uint32_t *__restrict__ ru, const uint3
   const uint4 *bits4 = reinterpret_cast<const uint4 *>(giant_bits);
   const uint32_t *bits32 = reinterpret_cast<const uint32_t *>(giant_bits);
   const uint32_t giant = giant_ptr[0];
+  bool touch_giant = false;  // a level edge of this block has an end in the giant
   uint64_t nlev = 0, nrem = 0;
   uint64_t i0 = tile_index(vb + (uint64_t)threadIdx.x * 4);
   uint4 ca = *reinterpret_cast<const uint4 *>(ru + i0), cb = *reinterpret_cast<const uint4 *>(rv + i0);
@@ -1206,9 +1210,10 @@ GHS_STREAM_KERNEL void k_level_pass(const uint32_t *__restrict__ ru, const uint3
     for (int j = 0; j < 4; ++j) {
       lmask |= lev[j] ? (1u << j) : 0u;
       rmask |= rem[j] ? (1u << j) : 0u;
-      if (lev[j] && mark) {  // active fragments of the level
-        mark[la[j]] = 1;
-        mark[lb[j]] = 1;
+      if (lev[j] && mark) {  // active fragments of the level; the giant's flag once per block
+        if (!ga[j]) mark[la[j]] = 1;
+        if (!gb[j]) mark[lb[j]] = 1;
+        touch_giant |= (ga[j] | gb[j]) != 0u;
       }
     }
     uint32_t le, wb, wc, tlev, trem;
@@ -1219,6 +1224,7 @@ GHS_STREAM_KERNEL void k_level_pass(const uint32_t *__restrict__ ru, const uint3
     nlev += tlev;
     nrem += trem;
   }
+  if (__syncthreads_or(touch_giant ? 1 : 0) && threadIdx.x == 0 && mark) mark[giant] = 1;
   // both outputs padded to a multiple of 4 with dead entries (a = LABEL_NONE)
   const uint64_t padded = (nrem + 3) & ~3ull, lpadded = (nlev + 3) & ~3ull;
   if (threadIdx.x < padded - nrem) {
