@@ -1587,6 +1587,7 @@ struct ghs_solver {
   bool open_async = false;      // the open level's counts arrive with its first round's report
   bool scan_pending = false;    // the last compaction's region counts are not scanned yet
   const ArcBuf *scan_buf = nullptr;
+  bool open_ident = false;      // the open level's first round runs over the identity list (level 0, one rank)
   bool arcs_known = true;       // cur_arcs holds the exact live edge count (else: unknown, grids sized for the bound)
   uint32_t lookahead = LOOKAHEAD;  // rounds in flight ahead of the termination check (GHS_LOOKAHEAD)
   std::chrono::steady_clock::time_point t0;
@@ -1789,8 +1790,14 @@ static int open_level(ghs_solver *s, bool async_open = false) {
 
   // 1. this level's edges -> regions of Y (level edges: a, b labels + key, canonical order).
   //    The pass also flags both ends of every level edge (the level's active fragments).
-  uint8_t *mark = s->flags;
-  GHS_HIP_CHECK(hipMemsetAsync(s->flags, 0, s->n, st));
+  // Single rank, level 0, async open: no active flags at all. Round 0 runs over the identity
+  // list of all n vertices (k_win needs no list; k_jump keeps only the roots that found an
+  // outgoing edge), which costs a sequential pass over par/best instead of 2 random flag stores
+  // per level-0 edge inside k_select plus the select.
+  const bool ident0 = first && single && async_open;
+  uint8_t *mark = ident0 ? nullptr : s->flags;
+  if (!ident0) GHS_HIP_CHECK(hipMemsetAsync(s->flags, 0, s->n, st));
+  s->open_ident = ident0;
   unsigned G = 1;
   const uint64_t TC = s->e_hi > s->e_lo ? s->e_hi - (s->e_lo & ~3ull) : 0;  // canonical passes stream [e_lo & ~3, e_hi)
   if (first) {
@@ -1908,8 +1915,12 @@ static int open_level_finish(ghs_solver *s) {
 // that round's report (run_level_pipelined). Until then the grids are sized for the bounds
 // (n fragments, the streaming grid for the edges). An empty level runs one no-op round.
 static int open_level_async(ghs_solver *s) {
-  if (int rc = select_lb(s, nullptr, s->cnt + C_N, s->n, s->act[0], s->cnt + C_ACT)) return rc;
-  s->act_ident = false;
+  if (s->open_ident) {
+    s->act_ident = true;  // every vertex (count C_N); see open_level
+  } else {
+    if (int rc = select_lb(s, nullptr, s->cnt + C_N, s->n, s->act[0], s->cnt + C_ACT)) return rc;
+    s->act_ident = false;
+  }
   s->act_cur = 0;
   s->nact = s->n;  // bound
   s->level_nact = s->n;
