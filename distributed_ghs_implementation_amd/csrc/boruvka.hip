@@ -67,6 +67,7 @@ static thread_local std::string g_err;
 void set_error(const std::string &msg) { g_err = msg; }
 
 constexpr uint32_t SEG_G = 2048;   // blocks of a compacting kernel (8 per CU) = output segments
+constexpr uint32_t SEG_MAX = SEG_G * 4;  // segments of a wave-private output (one per wave)
 constexpr int FIND_LAB_MAX_HOPS = 256;
 constexpr uint32_t JUMP_MAX_STEPS = 1u << 26;
 
@@ -281,6 +282,84 @@ __device__ __forceinline__ void stage_write_rs(WaveStage &ws, const uint32_t a[4
 }
 
 // ------------------------------------------------------------------------------------------
+// Wave-private sparse output. A streaming kernel whose waves each own a contiguous slice of the
+// input also owns the same slice of the output (one segment per wave). Survivors of each
+// 256-edge wave tile are appended to the wave's LDS buffer (WaveStage, 256 entries); the
+// buffer goes to the output only when the next tile might not fit: full 64-lane stores, every
+// ~30 tiles at level-0 selectivity instead of a block-wide offset computation (two barriers)
+// and a staging round per tile. Measured: the per-tile staging was ~19% of k_select.
+// ------------------------------------------------------------------------------------------
+struct WaveOut {
+  uint32_t cnt = 0;   // entries in the LDS buffer (wave-uniform)
+  uint64_t pos = 0;   // next output index of the wave's slice
+};
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t *total) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  uint32_t incl = x;
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const uint32_t o = __shfl_up(incl, d);
+    if (lane >= d) incl += o;
+  }
+  *total = __shfl(incl, WAVE - 1);
+  return incl - x;
+}
+
+__device__ __forceinline__ void wave_flush(WaveStage &ws, WaveOut &wo, uint32_t *__restrict__ oa, uint32_t *__restrict__ ob,
+                                           uint64_t *__restrict__ ok) {
+  wave_sync_lds();
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  for (uint32_t i = lane; i < wo.cnt; i += WAVE) {
+    oa[wo.pos + i] = ws.a[i];
+    ob[wo.pos + i] = ws.b[i];
+    ok[wo.pos + i] = ws.k[i];
+  }
+  wave_sync_lds();  // the buffer is refilled next
+  wo.pos += wo.cnt;
+  wo.cnt = 0;
+}
+
+__device__ __forceinline__ void wave_append(WaveStage &ws, WaveOut &wo, const uint32_t a[4], const uint32_t b[4],
+                                            const uint64_t k[4], uint32_t mask, uint32_t *__restrict__ oa,
+                                            uint32_t *__restrict__ ob, uint64_t *__restrict__ ok) {
+  uint32_t tile;
+  const uint32_t ex = wave_excl_scan((uint32_t)__popc(mask), &tile);
+  if (tile == 0) return;
+  if (wo.cnt + tile > WAVE * 4) wave_flush(ws, wo, oa, ob, ok);
+  uint32_t p = wo.cnt + ex;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (mask & (1u << j)) {
+      ws.a[p] = a[j];
+      ws.b[p] = b[j];
+      ws.k[p] = k[j];
+      ++p;
+    }
+  }
+  wo.cnt += tile;
+}
+
+// the wave's last flush, padding to a multiple of 4 with dead entries, and its segment entry
+__device__ __forceinline__ void wave_finish(WaveStage &ws, WaveOut &wo, uint32_t *__restrict__ oa,
+                                            uint32_t *__restrict__ ob, uint64_t *__restrict__ ok, uint64_t seg_begin,
+                                            bool has_range, uint64_t *__restrict__ ostart, uint64_t *__restrict__ ocount,
+                                            uint32_t seg) {
+  if (wo.cnt) wave_flush(ws, wo, oa, ob, ok);
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t n = wo.pos - seg_begin, padded = (n + 3) & ~3ull;
+  if (lane < padded - n) {
+    oa[wo.pos + lane] = LABEL_NONE;
+    ob[wo.pos + lane] = 0;
+    ok[wo.pos + lane] = KEY_NONE;
+  }
+  if (lane == 0) {
+    ostart[seg] = seg_begin;
+    ocount[seg] = has_range ? padded : 0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Segmented input: virtual index v in [0, total) lives in segment s with
 // prefix[s] <= v < prefix[s+1], physical index start[s] + (v - prefix[s]).
 // ------------------------------------------------------------------------------------------
@@ -339,7 +418,7 @@ __device__ __forceinline__ void tile_load(EdgeTile &t, const uint32_t *__restric
 // region (padded to a multiple of 4 with dead entries).
 // ------------------------------------------------------------------------------------------
 template <bool IDENT, bool COMPACT>
-GHS_STREAM_KERNEL void k_minedge(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
+GHS_STREAM_KERNEL_6 void k_minedge(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
                                  const uint64_t *__restrict__ key, SegView in, const uint32_t *__restrict__ lab,
                                  uint64_t *__restrict__ best, uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
                                  uint64_t *__restrict__ okey, uint64_t *__restrict__ oseg_start,
@@ -471,7 +550,7 @@ GHS_STREAM_KERNEL void k_minedge(const uint32_t *__restrict__ src, const uint32_
   hot_flush(s_hl, s_hk, best);
   if (COMPACT) {
     // pad to a multiple of 4 with dead entries; stays inside [vb, vb + Q) and below the capacity
-    // (the workspace reserves 4 * SEG_G spare entries)
+    // (the workspace reserves 4 * SEG_MAX spare entries)
     const uint64_t padded = (out_n + 3) & ~3ull;
     if (threadIdx.x < padded - out_n) {
       const uint64_t pos = vb + out_n + threadIdx.x;
@@ -629,7 +708,7 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
 // to the other end o unless the pair is mutual and c < o (the smaller label stays root, as in
 // k_hook). par[c] == c holds for every active root, so only hooking fragments are written.
 // ------------------------------------------------------------------------------------------
-GHS_STREAM_KERNEL void k_win(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
+GHS_STREAM_KERNEL_6 void k_win(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
                              const uint64_t *__restrict__ key, SegView in, const uint64_t *__restrict__ best,
                              uint32_t *__restrict__ par, uint8_t *__restrict__ in_mst,
                              unsigned long long *__restrict__ acc /* [0] weight, [1] edges */) {
@@ -859,45 +938,47 @@ __global__ void k_sample_weights(uint64_t cnt, const uint32_t *__restrict__ w, u
 // heavier edges stay where they are until k_filter. Block-private output regions: deterministic,
 // no atomics; the next tile's loads are issued before the current one is compacted.
 // ------------------------------------------------------------------------------------------
-GHS_STREAM_KERNEL void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, const uint32_t *__restrict__ eu,
+GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, const uint32_t *__restrict__ eu,
                                 const uint32_t *__restrict__ ev, const uint32_t *__restrict__ ew, uint64_t w_hi,
                                 uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst, uint64_t *__restrict__ okey,
                                 uint64_t *__restrict__ ostart, uint64_t *__restrict__ ocount,
                                 uint8_t *__restrict__ mark, unsigned long long *__restrict__ err) {
-  __shared__ uint32_t s_wcnt[BLOCK / WAVE];
   __shared__ WaveStage s_stage[BLOCK / WAVE];
+  // the wave index through readfirstlane: uniform in an SGPR, so every value derived from it
+  // (the slice, its buffer descriptors) is scalar — a VGPR descriptor makes hipcc wrap each
+  // buffer load in a waterfall loop
+  const uint32_t lane = threadIdx.x & (WAVE - 1), wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+  const uint32_t gw = blockIdx.x * (BLOCK / WAVE) + wid;  // this wave's slice (and output segment)
+  const uint64_t W = (uint64_t)gridDim.x * (BLOCK / WAVE);
   const uint64_t E0 = e_lo & ~3ull;
   const uint64_t T = e_hi - E0;
-  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
-  const uint64_t vb = Q * blockIdx.x;
+  const uint64_t Q = ((T + W - 1) / W + 3) & ~3ull;
+  const uint64_t vb = Q * gw;
   const uint64_t ve = (vb + Q < T) ? vb + Q : T;
-  const uint64_t eb = E0 + vb;  // first edge of this block
+  const uint64_t eb = E0 + vb;  // first edge of this wave
   const uint64_t nbytes = ve > vb ? (ve - vb) * 4 : 0;
   const __amdgpu_buffer_rsrc_t ru = make_rsrc(eu + eb, nbytes);
   const __amdgpu_buffer_rsrc_t rv = make_rsrc(ev + eb, nbytes);
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(ew + eb, nbytes);
-  // the edge before each lane's tile; offset -4 (the block's first tile) is out of range of the
-  // descriptor and is replaced by the block's predecessor edge, loaded once
-  // output region [vb, vb + Q) of each array
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc_u32(osrc + vb, Q * 4), rb = make_rsrc_u32(odst + vb, Q * 4);
-  const __amdgpu_buffer_rsrc_t rk = make_rsrc_u32(okey + vb, Q * 8);
+  // the edge before each lane's tile; offset -4 (the wave's first tile) is out of range of the
+  // descriptor and is replaced by the wave's predecessor edge, loaded once
   uint32_t bpa = 0, bpb = 0;
   if (eb > 0 && ve > vb) {
     bpa = eu[eb - 1];
     bpb = ev[eb - 1];
   }
-  const uint32_t lane_off = threadIdx.x * 16u;  // byte offset of the lane's tile in an iteration
-  uint64_t nout = 0;
+  const uint32_t lane_off = lane * 16u;  // byte offset of the lane's tile in an iteration
+  WaveOut wo;
+  wo.pos = vb;
   bool bad = false;
   uint4 ca = ld_b128(ru, lane_off), cb = ld_b128(rv, lane_off), cw = ld_b128(rw, lane_off);
   uint32_t cpa = ld_b32(ru, lane_off - 4), cpb = ld_b32(rv, lane_off - 4);
-  // Every tile's loads are consumed at the END of the iteration that issued them (the empty
-  // asm "uses" below): the wait then sits behind a fixed number of stores and stays counted,
-  // and the loop header receives no pending load from either edge (a pending prologue load
-  // merged into the header made hipcc drain the stores there on every iteration).
+  // Every tile's loads are consumed at the END of the iteration that issued them (the empty asm
+  // "uses"): the loop header then receives no pending load from either edge and never drains
+  // the (rare, variable) flush stores there.
   asm volatile("" ::"v"(ca.x), "v"(cb.x), "v"(cw.x), "v"(cpa), "v"(cpb));
-  for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
-    const uint64_t v = v0 + (uint64_t)threadIdx.x * 4;
+  for (uint64_t v0 = vb; v0 < ve; v0 += WAVE * 4) {
+    const uint64_t v = v0 + (uint64_t)lane * 4;
     const uint64_t e0 = E0 + v;
     const uint32_t a[4] = {ca.x, ca.y, ca.z, ca.w}, b[4] = {cb.x, cb.y, cb.z, cb.w}, w[4] = {cw.x, cw.y, cw.z, cw.w};
     // lane mask of the tile: edges in [e_lo, ve) (32-bit arithmetic, no branches)
@@ -907,7 +988,7 @@ GHS_STREAM_KERNEL void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, const 
 #pragma unroll
     for (int j = 0; j < 4; ++j) live[j] = ((uint32_t)j < nv) & ((uint32_t)j >= nskip);
     // next tile (out-of-range offsets read 0)
-    const uint32_t noff = (uint32_t)(v0 + ARCS_PER_BLOCK - vb) * 4u + lane_off;
+    const uint32_t noff = (uint32_t)(v0 + WAVE * 4 - vb) * 4u + lane_off;
     ca = ld_b128(ru, noff);
     cb = ld_b128(rv, noff);
     cw = ld_b128(rw, noff);
@@ -934,30 +1015,16 @@ GHS_STREAM_KERNEL void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, const 
     for (int j = 0; j < 4; ++j) {
       omask |= out[j] ? (1u << j) : 0u;
       key[j] = ((uint64_t)w[j] << 32) | (uint32_t)(e0 + j);
-      if (mark && out[j]) {  // active fragments of the level (~3% of the edges: branched, measured
-        mark[a[j]] = 1;  // faster than 8 unconditional dropped-lane stores per tile)
+      if (mark && out[j]) {  // active fragments of the level (~3% of the edges)
+        mark[a[j]] = 1;
         mark[b[j]] = 1;
       }
     }
-    uint32_t le, wb, wc, tot;
-    block_offsets_w((uint32_t)__popc(omask), s_wcnt, &le, &wb, &wc, &tot);
-    stage_write_rs(s_stage[threadIdx.x / WAVE], a, b, key, omask, le, wc, ra, rb, rk, (uint32_t)(nout + wb));
-    nout += tot;
+    wave_append(s_stage[wid], wo, a, b, key, omask, osrc, odst, okey);
     asm volatile("" ::"v"(ca.x), "v"(cb.x), "v"(cw.x), "v"(cpa), "v"(cpb));  // next tile landed (see above)
   }
   if (bad) atomicOr(err, 8ull);
-  // output regions are padded to a multiple of 4 with dead entries (a = LABEL_NONE)
-  const uint64_t padded = (nout + 3) & ~3ull;
-  if (threadIdx.x < padded - nout) {
-    const uint64_t pos = vb + nout + threadIdx.x;
-    osrc[pos] = LABEL_NONE;
-    odst[pos] = 0;
-    okey[pos] = KEY_NONE;
-  }
-  if (threadIdx.x == 0) {
-    ostart[blockIdx.x] = vb;
-    ocount[blockIdx.x] = (vb < T) ? padded : 0;
-  }
+  wave_finish(s_stage[wid], wo, osrc, odst, okey, vb, vb < T, ostart, ocount, gw);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1107,7 +1174,7 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
 // dropped for good (cycle property). lab is fully resolved (one hop); the giant-fragment bitmap
 // rejects most heavy edges without a label gather. Block-private regions, no atomics.
 // ------------------------------------------------------------------------------------------
-GHS_STREAM_KERNEL void k_level_pass(const uint32_t *__restrict__ ru, const uint32_t *__restrict__ rv,
+GHS_STREAM_KERNEL_6 void k_level_pass(const uint32_t *__restrict__ ru, const uint32_t *__restrict__ rv,
                                     const uint64_t *__restrict__ rkey, SegView in, uint64_t w_hi,
                                     const uint32_t *__restrict__ lab, const uint64_t *__restrict__ giant_bits,
                                     const uint32_t *__restrict__ giant_ptr,
@@ -1624,7 +1691,7 @@ static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, 
     return p;
   };
   const size_t N = (size_t)n;
-  const uint64_t cap = local_edges + 4 * SEG_G;  // a level's edges (+ padding of the regions)
+  const uint64_t cap = local_edges + 4 * SEG_MAX;  // a level's edges (+ padding of the regions)
   char *p;
   p = carve(N * 4); if (s) s->lab = (uint32_t *)p;
   p = carve(N * 4); if (s) s->par = (uint32_t *)p;
@@ -1640,17 +1707,17 @@ static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, 
     p = carve(cap * 4); if (s) s->buf[b].src = (uint32_t *)p;
     p = carve(cap * 4); if (s) s->buf[b].dst = (uint32_t *)p;
     p = carve(cap * 8); if (s) s->buf[b].key = (uint64_t *)p;
-    p = carve(SEG_G * 8); if (s) s->buf[b].seg_start = (uint64_t *)p;
-    p = carve(SEG_G * 8); if (s) s->buf[b].seg_count = (uint64_t *)p;
-    p = carve((SEG_G + 1) * 8); if (s) s->buf[b].seg_prefix = (uint64_t *)p;
+    p = carve(SEG_MAX * 8); if (s) s->buf[b].seg_start = (uint64_t *)p;
+    p = carve(SEG_MAX * 8); if (s) s->buf[b].seg_count = (uint64_t *)p;
+    p = carve((SEG_MAX + 1) * 8); if (s) s->buf[b].seg_prefix = (uint64_t *)p;
   }
   for (int b = 0; b < 2; ++b) {
     p = carve(cap * 4); if (s) s->rem[b].src = (uint32_t *)p;
     p = carve(cap * 4); if (s) s->rem[b].dst = (uint32_t *)p;
     p = carve(cap * 8); if (s) s->rem[b].key = (uint64_t *)p;
-    p = carve(SEG_G * 8); if (s) s->rem[b].seg_start = (uint64_t *)p;
-    p = carve(SEG_G * 8); if (s) s->rem[b].seg_count = (uint64_t *)p;
-    p = carve((SEG_G + 1) * 8); if (s) s->rem[b].seg_prefix = (uint64_t *)p;
+    p = carve(SEG_MAX * 8); if (s) s->rem[b].seg_start = (uint64_t *)p;
+    p = carve(SEG_MAX * 8); if (s) s->rem[b].seg_count = (uint64_t *)p;
+    p = carve((SEG_MAX + 1) * 8); if (s) s->rem[b].seg_prefix = (uint64_t *)p;
   }
   if (s) s->cap_arcs = cap;
   p = carve(C_COUNT * sizeof(unsigned long long)); if (s) s->cnt = (unsigned long long *)p;
@@ -1809,6 +1876,7 @@ static int open_level(ghs_solver *s, bool async_open = false) {
                                     Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR);
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[1], st));
       GHS_HIP_CHECK(hipGetLastError());
+      G *= BLOCK / WAVE;  // one output segment per wave
       k_scan_counts<<<1, 1024, 0, st>>>(Y.seg_count, G, Y.seg_prefix, s->cnt + C_LIVE);
     } else {
       GHS_HIP_CHECK(hipMemsetAsync(Y.seg_prefix, 0, 16, st));

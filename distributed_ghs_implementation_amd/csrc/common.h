@@ -31,6 +31,13 @@ void set_error(const std::string &msg);
 #endif
 #define GHS_STREAM_KERNEL \
   __global__ __launch_bounds__(BLOCK, GHS_STREAM_WAVES) __attribute__((amdgpu_num_sgpr(72)))
+// Streaming kernels whose VGPR count (> 64) already limits them to 6 waves per SIMD: no SGPR cap
+// (6 waves leave ~128 SGPRs each) but a 6-wave bound (<= 80 VGPRs). An SGPR cap there only
+// spills SGPRs into VGPR lanes — k_filter's loop spent 112 of its 432 VALU instructions on
+// v_readlane/v_writelane under a cap of 72 — and without the wave bound the freed SGPRs turn
+// into VGPRs (k_filter 83, k_level_pass 91: 5 waves, measured slower). k_filter itself stays
+// under the cap: uncapped (106 SGPRs, 75 VGPRs, 20 spills instead of 44) it measured ~3% slower.
+#define GHS_STREAM_KERNEL_6 __global__ __launch_bounds__(BLOCK, 6)
 
 // bijective 32-bit mixer (xorshift-multiply; every step is invertible on u32)
 __host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
