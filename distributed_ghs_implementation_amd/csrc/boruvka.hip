@@ -818,76 +818,47 @@ __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act
 }
 
 // ------------------------------------------------------------------------------------------
-// Between levels: compress every vertex to its root (lab[v] = find(v)) and flag the roots.
+// Between levels. k_giant first: the giant fragment = the most frequent root among NSAMPLE
+// evenly spaced vertices (ties: the smaller label), each sample resolved by its own walk and
+// counted in an LDS hash table — one workgroup, no host round trip. Then k_resolve compresses
+// every vertex to its root (lab[v] = find(v)) and writes the giant-membership bitmap in the same
+// pass (bit v = lab[v] == giant, one ballot word per wave).
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BLOCK) void k_resolve(uint32_t n, uint32_t *lab, uint8_t *__restrict__ root_flag,
-                                                   unsigned long long *__restrict__ err) {
-  for (uint64_t v = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; v < n; v += (uint64_t)gridDim.x * BLOCK) {
-    const uint32_t r = find_lab(lab, (uint32_t)v, err);
-    lab[v] = r;
-    if (root_flag) root_flag[v] = (r == (uint32_t)v) ? 1 : 0;
-  }
-}
-
-// The giant fragment = the most frequent label among NSAMPLE evenly spaced vertices (ties: the
-// smaller label). One workgroup: bitonic sort of the sample in LDS, then an argmax over the run
-// lengths. No host round trip.
 constexpr uint32_t NSAMPLE = 2048;  // the giant holds >= ~10% of the vertices: 2048 samples find it
-__global__ __launch_bounds__(1024) void k_giant(uint32_t n, const uint32_t *__restrict__ lab, uint32_t *__restrict__ giant) {
-  __shared__ uint32_t x[NSAMPLE];
+constexpr uint32_t GIANT_SLOTS = 4096;
+__global__ __launch_bounds__(1024) void k_giant(uint32_t n, const uint32_t *lab, uint32_t *__restrict__ giant,
+                                                unsigned long long *__restrict__ err) {
+  __shared__ uint32_t s_lab[GIANT_SLOTS];
+  __shared__ uint32_t s_cnt[GIANT_SLOTS];
   __shared__ unsigned long long s_best[1024 / WAVE];
-  const uint32_t ns = n < NSAMPLE ? n : NSAMPLE;
-  for (uint32_t i = threadIdx.x; i < NSAMPLE; i += 1024) {
-    const uint64_t v = ((uint64_t)i * n) / ns;
-    x[i] = i < ns ? lab[v] : 0xffffffffu;  // padding sorts last and is never counted
+  for (uint32_t i = threadIdx.x; i < GIANT_SLOTS; i += 1024) {
+    s_lab[i] = LABEL_NONE;
+    s_cnt[i] = 0;
   }
   __syncthreads();
-  for (uint32_t k = 2; k <= NSAMPLE; k <<= 1) {
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = threadIdx.x; i < NSAMPLE; i += 1024) {
-        const uint32_t p = i ^ j;
-        if (p > i) {
-          const uint32_t a = x[i], b = x[p];
-          const bool up = (i & k) == 0;
-          if ((a > b) == up) {
-            x[i] = b;
-            x[p] = a;
-          }
-        }
+  const uint32_t ns = n < NSAMPLE ? n : NSAMPLE;
+  for (uint32_t i = threadIdx.x; i < ns; i += 1024) {
+    const uint32_t r = find_lab(lab, (uint32_t)(((uint64_t)i * n) / ns), err);
+    uint32_t h = (r * 0x9E3779B1u) >> (32 - 12);
+    for (;;) {  // linear probing: 4096 slots for <= 2048 keys always end
+      uint32_t cur = s_lab[h];
+      if (cur == LABEL_NONE) {
+        cur = atomicCAS(&s_lab[h], LABEL_NONE, r);
+        if (cur == LABEL_NONE) cur = r;
       }
-      __syncthreads();
+      if (cur == r) {
+        atomicAdd(&s_cnt[h], 1u);
+        break;
+      }
+      h = (h + 1) & (GIANT_SLOTS - 1);
     }
   }
-  // run starts by an inclusive max-scan of head positions (8 per thread, then across threads);
-  // at the last element of a run, length = i - start + 1. Pack (length, ~label) for a max.
-  constexpr uint32_t PER = NSAMPLE / 1024;
-  uint32_t rs[PER];
-  uint32_t run_start = 0;
-  const uint32_t b0 = threadIdx.x * PER;
-#pragma unroll
-  for (uint32_t q = 0; q < PER; ++q) {
-    const uint32_t i = b0 + q;
-    if (i == 0 || x[i] != x[i - 1]) run_start = i;
-    rs[q] = run_start;
-  }
-  __shared__ uint32_t s_scan[1024];
-  s_scan[threadIdx.x] = rs[PER - 1];
   __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {
-    const uint32_t o = threadIdx.x >= d ? s_scan[threadIdx.x - d] : 0u;
-    __syncthreads();
-    s_scan[threadIdx.x] = s_scan[threadIdx.x] > o ? s_scan[threadIdx.x] : o;
-    __syncthreads();
-  }
-  const uint32_t carry = threadIdx.x ? s_scan[threadIdx.x - 1] : 0u;  // run start entering this chunk
+  // pack (count, ~label) for a max: most frequent, then the smaller label
   unsigned long long best = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < PER; ++q) {
-    const uint32_t i = b0 + q;
-    const uint32_t start = rs[q] > carry ? rs[q] : carry;
-    const bool last = (i + 1 >= ns) || (x[i + 1] != x[i]);
-    if (i < ns && last) {
-      const unsigned long long c = ((unsigned long long)(i - start + 1) << 32) | (0xffffffffu - x[i]);
+  for (uint32_t i = threadIdx.x; i < GIANT_SLOTS; i += 1024) {
+    if (s_lab[i] != LABEL_NONE) {
+      const unsigned long long c = ((unsigned long long)s_cnt[i] << 32) | (0xffffffffu - s_lab[i]);
       best = c > best ? c : best;
     }
   }
@@ -906,14 +877,18 @@ __global__ __launch_bounds__(1024) void k_giant(uint32_t n, const uint32_t *__re
   }
 }
 
-// giant-fragment membership bitmap: bit v = (lab[v] == giant); one u64 word per wave
-__global__ __launch_bounds__(BLOCK) void k_bitmap(uint32_t n, const uint32_t *__restrict__ lab,
-                                                  const uint32_t *__restrict__ giant_ptr, uint64_t *__restrict__ bits) {
-  const uint64_t words = ((uint64_t)n + 63) / 64;
+__global__ __launch_bounds__(BLOCK) void k_resolve(uint32_t n, uint32_t *lab, const uint32_t *__restrict__ giant_ptr,
+                                                   uint64_t *__restrict__ bits, unsigned long long *__restrict__ err) {
   const uint32_t giant = giant_ptr[0];
+  const uint64_t words = ((uint64_t)n + 63) / 64;
   for (uint64_t base = blockIdx.x * (uint64_t)BLOCK; base < (uint64_t)n; base += (uint64_t)gridDim.x * BLOCK) {
     const uint64_t v = base + threadIdx.x;
-    const bool in = v < n && lab[v] == giant;
+    bool in = false;
+    if (v < n) {
+      const uint32_t r = find_lab(lab, (uint32_t)v, err);
+      lab[v] = r;
+      in = r == giant;
+    }
     const uint64_t b = __ballot(in);
     if ((threadIdx.x & (WAVE - 1)) == 0 && (v >> 6) < words) bits[v >> 6] = b;
   }
@@ -1848,10 +1823,9 @@ static int open_level(ghs_solver *s, bool async_open = false) {
   ArcBuf &Y = s->buf[1];
 
   if (!first) {
-    // compress labels, find the giant fragment from a sample, build its bitmap (all on device)
-    k_resolve<<<grid_for(s->n, BLOCK, 16384), BLOCK, 0, st>>>(s->n, s->lab, nullptr, s->cnt + C_ERR);
-    k_giant<<<1, 1024, 0, st>>>(s->n, s->lab, s->giant);
-    k_bitmap<<<grid_for(s->n, BLOCK, 16384), BLOCK, 0, st>>>(s->n, s->lab, s->giant, s->bits);
+    // find the giant fragment from a sample, compress labels and build its bitmap (on device)
+    k_giant<<<1, 1024, 0, st>>>(s->n, s->lab, s->giant, s->cnt + C_ERR);
+    k_resolve<<<grid_for(s->n, BLOCK, 16384), BLOCK, 0, st>>>(s->n, s->lab, s->giant, s->bits, s->cnt + C_ERR);
     GHS_HIP_CHECK(hipGetLastError());
   }
 
