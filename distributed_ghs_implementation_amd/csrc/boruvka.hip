@@ -1322,7 +1322,7 @@ struct RoundSlot {
   unsigned long long seq;
   unsigned long long nact_in;  // active fragments this round started from (a level's first round: the level's)
   unsigned long long pending;  // pending edges after the level's pass (counter C_PENDING)
-  unsigned long long pad;
+  unsigned long long weight;   // MSF weight so far (counter C_WEIGHT)
 };
 
 __device__ __forceinline__ void write_report(RoundSlot *slot, unsigned long long seq, const unsigned long long *cnt,
@@ -1332,6 +1332,7 @@ __device__ __forceinline__ void write_report(RoundSlot *slot, unsigned long long
   const unsigned long long edges = __hip_atomic_load(cnt + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned long long err = __hip_atomic_load(cnt + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned long long pending = __hip_atomic_load(cnt + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long weight = __hip_atomic_load(cnt + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // The slot is coherent (uncached) host memory: its stores bypass the L2, so draining them
   // (vmcnt(0)) before the seq store orders them for the host's acquire load of seq. No
   // __threadfence_system(): its L2 write-back of every dirty line held the next round's first
@@ -1342,6 +1343,7 @@ __device__ __forceinline__ void write_report(RoundSlot *slot, unsigned long long
   slot->err = err;                // error bits
   slot->nact_in = nact_in;
   slot->pending = pending;
+  slot->weight = weight;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(&slot->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1512,7 +1514,7 @@ enum : int {
   C_ACT = 8,      // [8], [9]: lengths of the active lists act[0], act[1]
   C_COUNT = 16
 };
-static_assert(C_ERR == 4 && C_PENDING == 5, "write_report reads the counters by index");
+static_assert(C_WEIGHT == 2 && C_EDGES == 3 && C_ERR == 4 && C_PENDING == 5, "write_report reads the counters by index");
 
 constexpr int SLOT_RING = 8;
 // rounds enqueued ahead of the host's termination check (GHS_LOOKAHEAD: 0..4). R-MAT s24: 1 ->
@@ -1628,6 +1630,8 @@ struct ghs_solver {
   uint32_t seg_g = SEG_G;       // blocks of the streaming kernels (GHS_SEG_G, 256..SEG_G)
   bool open_async = false;      // the open level's counts arrive with its first round's report
   bool scan_pending = false;    // the last compaction's region counts are not scanned yet
+  bool report_final = false;    // the last round report read holds the final weight / edge count
+  unsigned long long rep_weight = 0, rep_edges = 0;
   const ArcBuf *scan_buf = nullptr;
   bool open_ident = false;      // the open level's first round runs over the identity list (level 0, one rank)
   bool arcs_known = true;       // cur_arcs holds the exact live edge count (else: unknown, grids sized for the bound)
@@ -1815,6 +1819,7 @@ static int open_level_finish(ghs_solver *s);
 static int open_level_async(ghs_solver *s);
 
 static int open_level(ghs_solver *s, bool async_open = false) {
+  s->report_final = false;
   const uint32_t lv = s->level;
   const uint64_t w_hi = s->thresholds[lv + 1];
   const bool first = (lv == 0);
@@ -2128,6 +2133,10 @@ static int run_level_pipelined(ghs_solver *s) {
     r.err = hs->err;
     r.nact_in = hs->nact_in;
     r.pending = hs->pending;
+    r.weight = hs->weight;
+    s->rep_weight = r.weight;
+    s->rep_edges = r.edges;
+    s->report_final = true;
     if (r.err) return fail_counters(s, r.err, ("in round " + std::to_string(round0 + checked + 1)).c_str());
     if (checked == 0 && s->open_async) {  // the level's counts, from its first round
       const uint64_t S = r.live_out;  // round 0 does not compact: its live edges are the level's
@@ -2343,6 +2352,7 @@ int ghs_solver_contract(ghs_solver_t *s, int *done) {
     return GHS_OK;
   }
   if (s->phase != 1) GHS_FAIL(GHS_E_STATE, "contract must follow minedge");
+  s->report_final = false;
   const uint64_t live_in = s->level_round <= 1 ? s->cur_arcs : s->h_cnt[C_LIVE];
   const uint64_t nact_in = s->nact;
   if (int rc = enqueue_contract(s)) return rc;
@@ -2365,8 +2375,15 @@ int ghs_solver_contract(ghs_solver_t *s, int *done) {
 int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *stats) {
   if (!s) GHS_FAIL(GHS_E_ARG, "solver is NULL");
   if (s->phase != 2) GHS_FAIL(GHS_E_STATE, "finish before the loop terminated");
-  GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, C_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
-  GHS_HIP_CHECK(hipStreamSynchronize(s->stream));
+  if (s->report_final) {
+    // the pipelined loop's last report already holds the final totals: no copy, no sync (a
+    // trailing no-op lookahead round may still run on the stream; it changes no counter)
+    s->h_cnt[C_WEIGHT] = s->rep_weight;
+    s->h_cnt[C_EDGES] = s->rep_edges;
+  } else {
+    GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, C_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
+    GHS_HIP_CHECK(hipStreamSynchronize(s->stream));
+  }
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s->t0).count();
   const uint32_t ns = (uint32_t)std::min<size_t>(s->stats.size(), GHS_MAX_ROUND_STATS);
   for (uint32_t r = 0; r < ns; ++r) {

@@ -105,19 +105,20 @@ int ghs_mst_host(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t *v, c
                  uint8_t *in_mst, ghs_result_t *result, ghs_round_stats_t *stats);
 
 /* ---- device-resident API -----------------------------------------------------------------
- * Input: the canonical edge list in HBM (d_u, d_v, d_w: m uint32 each, 16-byte aligned). Each
- * weight level is turned into a symmetric ARC list on the device — every selected edge as
- * u->v and v->u, grouped by source: the device form of the reference's per-node neighbour
- * files node_<id>.json (create_graph_files.py:56-74) — with key = w<<32 | eid. */
+ * Input: the canonical edge list in HBM (d_u, d_v, d_w: m uint32 each, 16-byte aligned) — the
+ * device form of the reference's per-node neighbour files node_<id>.json
+ * (create_graph_files.py:56-74), each edge once, key = w<<32 | eid. Each weight level's edges
+ * are streamed out of it (edge-centric: every edge is a candidate for both of its fragments). */
 void ghs_default_config(ghs_config_t *cfg);
 
 /* workspace bytes for ghs_mst_device / a solver handle owning local_edges canonical edges */
 size_t ghs_workspace_bytes(uint32_t n, uint64_t m, uint64_t local_edges);
 
 /* Whole MST on one device: canonical edges -> d_in_mst (m bytes, 1 = in the MSF) + totals.
- * cfg may be NULL (defaults). Blocks the calling thread until done (one host sync per round
- * for the termination test, one per level for the plan). Reference: GHSAlgorithm.run,
- * ghs_implementation.py:442-490. */
+ * cfg may be NULL (defaults). Returns once *result is final (the host polls the rounds'
+ * reports; one sync for the level plan). d_in_mst is written by work enqueued on `stream`:
+ * complete once the stream is synchronized (a trailing no-op round may still run on return).
+ * Reference: GHSAlgorithm.run, ghs_implementation.py:442-490. */
 int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
                    const ghs_config_t *cfg, void *d_workspace, size_t workspace_bytes, uint8_t *d_in_mst,
                    void *stream, ghs_result_t *result, ghs_round_stats_t *stats);
