@@ -902,6 +902,78 @@ __global__ void k_sample_weights(uint64_t cnt, const uint32_t *__restrict__ w, u
   }
 }
 
+// Level plan on the device (no host round trip before the first pass): thresholds = order
+// statistics of the weight sample, the same arithmetic as a host plan would do (target =
+// level1 * n edges, x growth per level, double precision; the q-th smallest by a 4-pass radix
+// select over the sample in LDS; equal thresholds merged). thr[0..count), thr[PLAN_MAX] = count.
+constexpr uint32_t NSAMPLE_W = 16384;  // weights sampled for the level plan
+constexpr uint32_t PLAN_MAX = 33;      // 0, up to 31 interior thresholds, 2^32
+__global__ __launch_bounds__(1024) void k_plan(const uint32_t *__restrict__ sample, uint32_t ns, uint32_t n, uint64_t m,
+                                               uint32_t L, double l1, double growth, uint64_t *__restrict__ thr) {
+  __shared__ uint32_t s_w[NSAMPLE_W];
+  __shared__ uint32_t s_hist[256];
+  __shared__ uint32_t s_sel[2];
+  for (uint32_t i = threadIdx.x; i < ns; i += 1024) s_w[i] = sample[i];
+  __syncthreads();
+  uint32_t cnt = 1;
+  uint64_t last = 0;
+  double target = l1 * (double)n;
+  for (uint32_t lev = 1; lev < L && ns > 0; ++lev) {  // uniform across the block
+    const double frac = target / (double)m;
+    if (frac >= 1.0) break;
+    const uint32_t q = (uint32_t)(frac * ns);  // non-decreasing: target grows every level
+    target *= fmax(1.01, growth);
+    if (q == 0) continue;
+    uint32_t prefix = 0, pmask = 0, k = q;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      for (uint32_t i = threadIdx.x; i < 256; i += 1024) s_hist[i] = 0;
+      __syncthreads();
+      for (uint32_t i = threadIdx.x; i < ns; i += 1024) {
+        const uint32_t x = s_w[i];
+        if ((x & pmask) == prefix) atomicAdd(&s_hist[(x >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      if (threadIdx.x < WAVE) {  // one wave finds the digit: lane t owns bins 4t..4t+3
+        const uint32_t t = threadIdx.x;
+        const uint32_t c[4] = {s_hist[4 * t], s_hist[4 * t + 1], s_hist[4 * t + 2], s_hist[4 * t + 3]};
+        const uint32_t sum = c[0] + c[1] + c[2] + c[3];
+        uint32_t incl = sum;
+#pragma unroll
+        for (int d = 1; d < WAVE; d <<= 1) {
+          const uint32_t o = __shfl_up(incl, d);
+          if ((int)t >= d) incl += o;
+        }
+        const uint32_t excl = incl - sum;
+        if (excl <= k && incl > k) {  // exactly one lane: the candidates number more than k
+          uint32_t acc = excl, d = 4 * t;
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            if (acc + c[j] > k) break;
+            acc += c[j];
+            ++d;
+          }
+          s_sel[0] = prefix | (d << shift);
+          s_sel[1] = k - acc;
+        }
+      }
+      __syncthreads();
+      prefix = s_sel[0];
+      k = s_sel[1];
+      pmask |= 255u << shift;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0 && (uint64_t)prefix > last) {
+      thr[cnt++] = prefix;
+      last = prefix;
+    }
+  }
+  if (threadIdx.x == 0) {
+    thr[0] = 0;
+    thr[cnt++] = 1ull << 32;
+    thr[PLAN_MAX] = cnt;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // SELECT (opens level 0): the first full stream over the caller's canonical list [e_lo, e_hi)
 // (u, v, w: 12 B per edge; key = w << 32 | eid built here). The stream runs over the aligned
@@ -914,10 +986,12 @@ __global__ void k_sample_weights(uint64_t cnt, const uint32_t *__restrict__ w, u
 // no atomics; the next tile's loads are issued before the current one is compacted.
 // ------------------------------------------------------------------------------------------
 GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, const uint32_t *__restrict__ eu,
-                                const uint32_t *__restrict__ ev, const uint32_t *__restrict__ ew, uint64_t w_hi,
+                                const uint32_t *__restrict__ ev, const uint32_t *__restrict__ ew,
+                                const uint64_t *__restrict__ w_hi_p,
                                 uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst, uint64_t *__restrict__ okey,
                                 uint64_t *__restrict__ ostart, uint64_t *__restrict__ ocount,
                                 uint8_t *__restrict__ mark, unsigned long long *__restrict__ err) {
+  const uint64_t w_hi = *w_hi_p;  // the level plan lives on the device (k_plan)
   __shared__ WaveStage s_stage[BLOCK / WAVE];
   // the wave index through readfirstlane: uniform in an SGPR, so every value derived from it
   // (the slice, its buffer descriptors) is scalar — a VGPR descriptor makes hipcc wrap each
@@ -1016,8 +1090,9 @@ GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, cons
 // edges.
 // ------------------------------------------------------------------------------------------
 GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__restrict__ eu,
-                                const uint32_t *__restrict__ ev, const uint32_t *__restrict__ ew, uint64_t w_lo,
-                                uint64_t w_hi, const uint64_t *__restrict__ giant_bits,
+                                const uint32_t *__restrict__ ev, const uint32_t *__restrict__ ew,
+                                const uint64_t *__restrict__ w_range /* [w_lo, w_hi] */,
+                                const uint64_t *__restrict__ giant_bits,
                                 const uint32_t *__restrict__ giant_ptr,
                                 const uint32_t *__restrict__ lab, uint32_t *__restrict__ lsrc,
                                 uint32_t *__restrict__ ldst, uint64_t *__restrict__ lkey,
@@ -1025,6 +1100,7 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
                                 uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
                                 uint64_t *__restrict__ okey, uint64_t *__restrict__ ostart,
                                 uint64_t *__restrict__ ocount, uint8_t *__restrict__ mark) {
+  const uint64_t w_lo = w_range[0], w_hi = w_range[1];  // the level plan (k_plan)
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
   __shared__ WaveStage s_stage[BLOCK / WAVE];
   const uint64_t E0 = e_lo & ~3ull;
@@ -1150,7 +1226,7 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
 // rejects most heavy edges without a label gather. Block-private regions, no atomics.
 // ------------------------------------------------------------------------------------------
 GHS_STREAM_KERNEL_6 void k_level_pass(const uint32_t *__restrict__ ru, const uint32_t *__restrict__ rv,
-                                    const uint64_t *__restrict__ rkey, SegView in, uint64_t w_hi,
+                                    const uint64_t *__restrict__ rkey, SegView in, const uint64_t *__restrict__ w_hi_p,
                                     const uint32_t *__restrict__ lab, const uint64_t *__restrict__ giant_bits,
                                     const uint32_t *__restrict__ giant_ptr,
                                     uint32_t *__restrict__ lsrc, uint32_t *__restrict__ ldst,
@@ -1158,6 +1234,7 @@ GHS_STREAM_KERNEL_6 void k_level_pass(const uint32_t *__restrict__ ru, const uin
                                     uint64_t *__restrict__ lcount, uint32_t *__restrict__ ou, uint32_t *__restrict__ ov, uint64_t *__restrict__ okey,
                                     uint64_t *__restrict__ ostart, uint64_t *__restrict__ ocount,
                                     uint8_t *__restrict__ mark) {
+  const uint64_t w_hi = *w_hi_p;  // the level plan (k_plan)
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
   __shared__ uint32_t s_seg[2];
   __shared__ WaveStage s_stage[BLOCK / WAVE];
@@ -1598,9 +1675,12 @@ struct ghs_solver {
   RoundSlot *h_slot = nullptr;          // = res->h_slot
   RoundSlot *d_slot = nullptr;          // = res->d_slot
   uint32_t *h_sample = nullptr;         // = res->h_sample
+  uint64_t *h_thr = nullptr;            // the plan's host copy (in the pinned sample buffer)
 
   // level plan (identical on every rank: computed from the global canonical list)
-  std::vector<uint64_t> thresholds;  // level i: [thr[i], thr[i+1])
+  std::vector<uint64_t> thresholds;  // level i: [thr[i], thr[i+1]) — host copy, once plan_known
+  uint64_t *d_thr = nullptr;          // the plan on the device (k_plan), read by the passes
+  bool plan_known = false;
   uint32_t level = 0;                // index of the level being processed
   bool level_open = false;
   uint64_t level_arcs = 0;           // edges of the current level (incl. padding; stats)
@@ -1659,7 +1739,6 @@ static HostRes *pooled_res(int *rc) {
   return r;
 }
 
-static constexpr uint32_t NSAMPLE_W = 16384; // weights sampled for the level plan
 static constexpr uint32_t NSAMPLE_MAX = NSAMPLE_W;
 
 static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, char *base) {
@@ -1680,6 +1759,7 @@ static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, 
   p = carve(N ? N : 1); if (s) s->flags = (uint8_t *)p;
   p = carve(((N + 127) / 128) * 16 + 16); if (s) s->bits = (uint64_t *)p;
   p = carve(NSAMPLE_MAX * 4); if (s) s->sample = (uint32_t *)p;
+  p = carve((PLAN_MAX + 1) * 8); if (s) s->d_thr = (uint64_t *)p;
   p = carve(16); if (s) s->giant = (uint32_t *)p;
   p = carve(LB_MAX_TILES * 8); if (s) s->lb_state = (unsigned long long *)p;  // select tile granules
   for (int b = 0; b < 2; ++b) {
@@ -1761,48 +1841,42 @@ static void default_config(ghs_config_t *c) {
 }
 
 // ---- level planning: thresholds from a sample of the GLOBAL canonical weights ----------------
-// Split so the host's quantile selection overlaps the solver's init kernels: the sample and its
-// copy are enqueued first (plan_levels_enqueue), the host waits for them alone (plan_ev) while
-// the GPU clears its arrays, then picks the thresholds (plan_levels_finish).
+// On the device (k_sample_weights -> k_plan -> d_thr, read by the passes), so the first pass
+// starts without a host round trip; the host's copy (pinned, behind plan_ev) is read only when
+// it needs the number of levels — at the end of level 0 at the earliest.
 static uint32_t plan_levels_count(const ghs_solver *s) {
   return std::max<uint32_t>(1, std::min<uint32_t>(s->cfg.max_levels, 32));
 }
 
 static int plan_levels_enqueue(ghs_solver *s) {
-  if (plan_levels_count(s) > 1 && s->m > 0) {
-    const uint32_t ns = (uint32_t)std::min<uint64_t>(NSAMPLE_W, s->m);
-    k_sample_weights<<<grid_for(ns, 256, 256), 256, 0, s->stream>>>(s->m, s->ew, ns, s->sample);
-    GHS_HIP_CHECK(hipGetLastError());
-    GHS_HIP_CHECK(hipMemcpyAsync(s->h_sample, s->sample, ns * 4, hipMemcpyDeviceToHost, s->stream));
-    GHS_HIP_CHECK(hipEventRecord(s->res->plan_ev, s->stream));
-  }
+  const uint32_t L = plan_levels_count(s);
+  const uint32_t ns = (L > 1 && s->m > 0) ? (uint32_t)std::min<uint64_t>(NSAMPLE_W, s->m) : 0u;
+  if (ns) k_sample_weights<<<grid_for(ns, 256, 256), 256, 0, s->stream>>>(s->m, s->ew, ns, s->sample);
+  k_plan<<<1, 1024, 0, s->stream>>>(s->sample, ns, s->n, s->m, L, s->cfg.level1_edges_per_vertex, s->cfg.level_growth,
+                                    s->d_thr);
+  GHS_HIP_CHECK(hipGetLastError());
+  GHS_HIP_CHECK(hipMemcpyAsync(s->h_thr, s->d_thr, (PLAN_MAX + 1) * 8, hipMemcpyDeviceToHost, s->stream));
+  GHS_HIP_CHECK(hipEventRecord(s->res->plan_ev, s->stream));
+  s->plan_known = false;
   return GHS_OK;
 }
 
-static int plan_levels_finish(ghs_solver *s) {
-  s->thresholds.clear();
-  s->thresholds.push_back(0);
-  const uint32_t L = plan_levels_count(s);
-  if (L > 1 && s->m > 0) {
-    const uint32_t ns = (uint32_t)std::min<uint64_t>(NSAMPLE_W, s->m);
-    GHS_HIP_CHECK(hipEventSynchronize(s->res->plan_ev));
-    std::vector<uint32_t> w(s->h_sample, s->h_sample + ns);
-    double target = s->cfg.level1_edges_per_vertex * (double)s->n;
-    size_t lo = 0;  // quantiles ascend: each selection works on the part above the last one
-    for (uint32_t i = 1; i < L; ++i) {
-      const double frac = target / (double)s->m;
-      if (frac >= 1.0) break;
-      const size_t q = (size_t)(frac * ns);
-      target *= std::max(1.01, s->cfg.level_growth);
-      if (q == 0 || q < lo) continue;
-      std::nth_element(w.begin() + lo, w.begin() + q, w.end());
-      lo = q;
-      const uint64_t thr = (uint64_t)w[q];
-      if (thr > s->thresholds.back()) s->thresholds.push_back(thr);
-    }
-  }
-  s->thresholds.push_back(1ull << 32);
+// the host copy of the plan (waits for it the first time)
+static int plan_sync(ghs_solver *s) {
+  if (s->plan_known) return GHS_OK;
+  GHS_HIP_CHECK(hipEventSynchronize(s->res->plan_ev));
+  const uint64_t cnt = s->h_thr[PLAN_MAX];
+  if (cnt < 2 || cnt > PLAN_MAX) GHS_FAIL(GHS_E_STATE, "bad level plan");
+  s->thresholds.assign(s->h_thr, s->h_thr + cnt);
+  s->plan_known = true;
   return GHS_OK;
+}
+
+// every level done? (level 0 always exists: no wait for the plan before it)
+static bool levels_done(ghs_solver *s) {
+  if (s->level == 0 && !s->plan_known) return false;
+  if (plan_sync(s)) return true;
+  return s->level + 1 >= s->thresholds.size();
 }
 
 static int fail_counters(ghs_solver *s, unsigned long long err, const char *where) {
@@ -1821,7 +1895,7 @@ static int open_level_async(ghs_solver *s);
 static int open_level(ghs_solver *s, bool async_open = false) {
   s->report_final = false;
   const uint32_t lv = s->level;
-  const uint64_t w_hi = s->thresholds[lv + 1];
+  const uint64_t *d_range = s->d_thr + lv;  // this level's [w_lo, w_hi] on the device
   const bool first = (lv == 0);
   const bool single = s->cfg.num_ranks <= 1;
   hipStream_t st = s->stream;
@@ -1851,7 +1925,7 @@ static int open_level(ghs_solver *s, bool async_open = false) {
     G = grid_for(TC, ARCS_PER_BLOCK, s->seg_g);
     if (TC) {
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[0], st));
-      k_select<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, w_hi, Y.src, Y.dst, Y.key,
+      k_select<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range + 1, Y.src, Y.dst, Y.key,
                                     Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR);
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[1], st));
       GHS_HIP_CHECK(hipGetLastError());
@@ -1871,7 +1945,7 @@ static int open_level(ghs_solver *s, bool async_open = false) {
       G = grid_for(TC, ARCS_PER_BLOCK, s->seg_g);
       if (TC) {
         GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[2], st));
-        k_filter<<<G, BLOCK, 0, st>>>(s->e_lo, s->e_hi, s->eu, s->ev, s->ew, s->thresholds[lv], w_hi, s->bits, s->giant, s->lab,
+        k_filter<<<G, BLOCK, 0, st>>>(s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range, s->bits, s->giant, s->lab,
                                       Y.src, Y.dst, Y.key, Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key,
                                       RO.seg_start, RO.seg_count, mark);
         GHS_HIP_CHECK(hipGetLastError());
@@ -1892,7 +1966,7 @@ static int open_level(ghs_solver *s, bool async_open = false) {
       // heavier survivors -> RO regions. Fixed grid: block b owns 1/seg_g of the virtual range.
       G = s->seg_g;
       SegView in{RI.seg_start, RI.seg_prefix, s->rem_nseg};
-      k_level_pass<<<G, BLOCK, 0, st>>>(RI.src, RI.dst, RI.key, in, w_hi, s->lab, s->bits, s->giant, Y.src, Y.dst, Y.key,
+      k_level_pass<<<G, BLOCK, 0, st>>>(RI.src, RI.dst, RI.key, in, d_range + 1, s->lab, s->bits, s->giant, Y.src, Y.dst, Y.key,
                                         Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key, RO.seg_start, RO.seg_count,
                                         mark);
       GHS_HIP_CHECK(hipGetLastError());
@@ -1921,6 +1995,7 @@ static int open_level_finish(ghs_solver *s) {
   hipStream_t st = s->stream;
   const uint32_t lv = s->level;
   const bool first = (lv == 0);
+  if (int rc = plan_sync(s)) return rc;
   const uint64_t w_hi = s->thresholds[lv + 1];
   const unsigned G = s->open_G;
   s->pending_exchange = false;
@@ -2099,6 +2174,7 @@ static void push_stats(ghs_solver *s, uint32_t level_round, uint64_t live_in, ui
 static void close_level(ghs_solver *s) {
   s->level_open = false;
   s->level += 1;
+  (void)plan_sync(s);  // on failure thresholds stay empty: no further level
   const bool no_more =
       (s->level + 1 >= s->thresholds.size()) || (s->cfg.num_ranks <= 1 && s->pending_built && s->rem_total == 0);
   s->phase = no_more ? 2 : 0;
@@ -2253,6 +2329,7 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   s->h_slot = s->res->h_slot;
   s->d_slot = s->res->d_slot;
   s->h_sample = s->res->h_sample;
+  s->h_thr = reinterpret_cast<uint64_t *>(s->res->h_sample);
   s->t0 = std::chrono::steady_clock::now();
   int rc = plan_levels_enqueue(s);
   if (rc) {
@@ -2268,11 +2345,6 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   if ((e = hipMemsetAsync(s->lb_state, 0, LB_MAX_TILES * 8, s->stream)) != hipSuccess) return fail(e, "memset select state");
   k_init_counters<<<1, 64, 0, s->stream>>>(s->cnt, n);
   if ((e = hipGetLastError()) != hipSuccess) return fail(e, "init kernels");
-  rc = plan_levels_finish(s);  // waits for the weight sample only
-  if (rc) {
-    ghs_solver_destroy(s);
-    return rc;
-  }
   s->level = 0;
   s->level_open = false;
   s->phase = n ? 0 : 2;
@@ -2295,7 +2367,7 @@ int ghs_solver_minedge(ghs_solver_t *s, uint64_t *num_active) {
       if (!s->level_open) s->level += 1;  // no edge of this level on any rank
       continue;
     }
-    if (s->level + 1 >= s->thresholds.size()) {  // every level done
+    if (levels_done(s)) {  // every level done
       s->phase = 2;
       if (num_active) *num_active = 0;
       return GHS_OK;
@@ -2405,7 +2477,7 @@ int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *
     result->total_weight = s->n ? s->h_cnt[C_WEIGHT] : 0;
     result->rounds = s->round;
     result->num_stats = ns;
-    result->levels = (uint32_t)(s->thresholds.size() - 1);
+    result->levels = (plan_sync(s) == GHS_OK) ? (uint32_t)(s->thresholds.size() - 1) : 0u;
     result->ms_total = ms;
     float t = 0;
     result->ms_select = (s->e_hi > s->e_lo && hipEventElapsedTime(&t, s->res->pass_ev[0], s->res->pass_ev[1]) == hipSuccess) ? t : 0.f;
@@ -2442,7 +2514,7 @@ int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *
   if (rc) return rc;
   while (!rc && s->phase != 2) {
     if (!s->level_open) {
-      if (s->level + 1 >= s->thresholds.size()) {
+      if (levels_done(s)) {
         s->phase = 2;
         break;
       }

@@ -234,3 +234,49 @@ def test_rmat_s20_oracle_and_determinism(torch_cuda):
     g = e.to_host()
     ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
     assert np.array_equal(f1, ref_in.astype(bool))
+
+
+def _host_plan(w, n, m, max_levels=8, l1=0.5, growth=8.0, nsample=16384):
+    """The level plan's formula (boruvka.hip k_plan) restated: order statistics of an evenly
+    spaced weight sample."""
+    L = max(1, min(max_levels, 32))
+    thr = [0]
+    if L > 1 and m > 0:
+        ns = min(nsample, m)
+        idx = (np.arange(ns, dtype=np.uint64) * np.uint64(m)) // np.uint64(ns)
+        smp = np.sort(w[idx.astype(np.int64)].astype(np.uint64))
+        target = l1 * float(n)
+        for _ in range(1, L):
+            frac = target / float(m)
+            if frac >= 1.0:
+                break
+            q = int(frac * ns)
+            target *= max(1.01, growth)
+            if q == 0:
+                continue
+            t = int(smp[q])
+            if t > thr[-1]:
+                thr.append(t)
+    thr.append(1 << 32)
+    return thr
+
+
+@pytest.mark.parametrize("scale,cfg", [(16, {}), (18, dict(max_levels=6, level1_edges_per_vertex=0.25, level_growth=2.0))])
+def test_device_level_plan_matches_formula(scale, cfg, torch_cuda):
+    """k_plan (device radix select) gives the thresholds of the formula: same level count, and
+    level 0 holds exactly the edges below the first threshold (+ <= 3 padding entries per
+    output region)."""
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import DeviceMST, generate_rmat
+    e = generate_rmat(scale, 16, seed=7, wseed=8)
+    g = e.to_host()
+    kw = dict(max_levels=8, l1=0.5, growth=8.0)
+    kw.update({"max_levels": cfg.get("max_levels", 8), "l1": cfg.get("level1_edges_per_vertex", 0.5),
+               "growth": cfg.get("level_growth", 8.0)})
+    thr = _host_plan(g.w, g.n, g.m, **kw)
+    eng = DeviceMST(e, config=_native.make_config(**cfg))
+    res, stats = eng.run()
+    assert res.levels == len(thr) - 1
+    below = int((g.w.astype(np.uint64) < np.uint64(thr[1])).sum())
+    lvl0 = stats[0]["level_arcs"]
+    assert below <= lvl0 <= below + 3 * 4 * 2048

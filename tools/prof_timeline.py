@@ -26,6 +26,8 @@ def main():
     e = idx[occ + 1] if occ + 1 < 0 else len(rows)  # up to the next step's marker
     rows = rows[:e]
     t0 = rows[s][1]
+    if s > 0:
+        print(f"gap before the step's first kernel: {(rows[s][1] - rows[s - 1][2]) / 1e3:.1f} us (after {short(rows[s - 1][0])})")
     prev = t0
     busy = 0
     for r in rows[s:]:
