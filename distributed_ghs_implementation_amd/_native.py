@@ -5,6 +5,7 @@ library. There is no CPU fallback — if the library is missing or no GPU is vis
 compute entry point raises. (The CPU restatement used to CHECK results lives in oracle/, which
 this package never imports.)
 """
+import collections.abc
 import ctypes
 import os
 import threading
@@ -66,6 +67,29 @@ class RoundStats(ctypes.Structure):
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+
+
+class RoundStatsList(collections.abc.Sequence):
+    """The per-round stats of one solve as a read-only sequence of dicts, converted on access
+    (a solve returns up to 64 rounds; building every dict eagerly cost ~27 us per solve)."""
+
+    def __init__(self, arr, n):
+        self._arr, self._n = arr, int(n)
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(self._n))]
+        if i < 0:
+            i += self._n
+        if not 0 <= i < self._n:
+            raise IndexError(i)
+        return self._arr[i].as_dict()
+
+    def __repr__(self):
+        return repr(list(self))
 
 
 ABI_VERSION = 2  # include/ghs_mst.h GHS_MST_ABI_VERSION

@@ -810,7 +810,7 @@ __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act
         break;
       }
     }
-    lab[c] = x;
+    if (x != c) lab[c] = x;  // a root's label is already itself (k_resolve, then only hooks move it)
     const bool keep = root && best[c] != KEY_NONE;
     if (keep) best[c] = KEY_NONE;
     flags[i] = keep ? 1 : 0;

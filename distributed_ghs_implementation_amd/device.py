@@ -118,7 +118,7 @@ class DeviceMST:
         _native.check(self.L.ghs_mst_device(e.n, e.m, _ptr(e.u), _ptr(e.v), _ptr(e.w), ctypes.byref(self.config),
                                             _ptr(self.ws), self.ws_bytes, _ptr(self.in_mst), _stream(),
                                             ctypes.byref(res), stats))
-        return res, [stats[i].as_dict() for i in range(res.num_stats)]
+        return res, _native.RoundStatsList(stats, res.num_stats)
 
     def in_mst_host(self):
         return self.in_mst[: self.edges.m].cpu().numpy().astype(bool)

@@ -74,7 +74,7 @@ class HipStepper:
         res = _native.Result()
         stats = (_native.RoundStats * _native.GHS_MAX_ROUND_STATS)()
         _native.check(self.L.ghs_solver_finish(self.h, ctypes.byref(res), stats))
-        return res, [stats[i].as_dict() for i in range(res.num_stats)]
+        return res, _native.RoundStatsList(stats, res.num_stats)
 
     def close(self):
         if self.h:
