@@ -68,6 +68,10 @@ void set_error(const std::string &msg) { g_err = msg; }
 
 constexpr uint32_t SEG_G = 2048;   // blocks of a compacting kernel (8 per CU) = output segments
 constexpr uint32_t SEG_MAX = SEG_G * 4;  // segments of a wave-private output (one per wave)
+// The compacting min-edge runs 6 blocks per CU (79 VGPRs): a grid of exactly 6 x 256 measured ~5%
+// faster than 2048 (R-MAT s24: 1.75 vs 1.67 TB/s); the canonical passes keep 2048 (k_filter is
+// fastest there).
+constexpr uint32_t CMP_G = 1536;
 constexpr int FIND_LAB_MAX_HOPS = 256;
 constexpr uint32_t JUMP_MAX_STEPS = 1u << 26;
 
@@ -1708,6 +1712,7 @@ struct ghs_solver {
   bool detail = false;          // GHS_DETAIL=1: time every stage (adds ~5.7 us per event)
   bool time_rounds = false;     // GHS_TIME_ROUNDS=1: time the compacting min-edge launches (bench)
   uint32_t seg_g = SEG_G;       // blocks of the streaming kernels (GHS_SEG_G, 256..SEG_G)
+  uint32_t cmp_g = CMP_G;       // blocks (= output regions) of the compacting min-edge (GHS_MINEDGE_G)
   bool open_async = false;      // the open level's counts arrive with its first round's report
   bool scan_pending = false;    // the last compaction's region counts are not scanned yet
   bool report_final = false;    // the last round report read holds the final weight / edge count
@@ -2063,7 +2068,7 @@ static inline const unsigned long long *cur_act_count(ghs_solver *s) {
 
 // the pending region scan as its own launch (when no hook kernel follows to carry it)
 static void flush_scan(ghs_solver *s) {
-  k_scan_counts<<<1, 1024, 0, s->stream>>>(s->scan_buf->seg_count, s->seg_g, s->scan_buf->seg_prefix, s->cnt + C_LIVE);
+  k_scan_counts<<<1, 1024, 0, s->stream>>>(s->scan_buf->seg_count, s->cmp_g, s->scan_buf->seg_prefix, s->cnt + C_LIVE);
   s->scan_pending = false;
 }
 
@@ -2080,7 +2085,7 @@ static int enqueue_minedge(ghs_solver *s) {
           I.src, I.dst, I.key, in, s->lab, s->best, nullptr, nullptr, nullptr, nullptr, nullptr);
   } else {
     // fixed grid: every one of the seg_g blocks writes its region's count
-    k_minedge<false, true><<<s->seg_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, O.src, O.dst,
+    k_minedge<false, true><<<s->cmp_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, O.src, O.dst,
                                                           O.key, O.seg_start, O.seg_count);
     // the regions' prefix scan is left to the round's hook kernel (or a scan launch before the
     // next consumer): s->scan_pending
@@ -2114,7 +2119,7 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
     } else {
       const ArcBuf *sb = s->scan_pending ? s->scan_buf : nullptr;
       k_hook<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
-                                         s->cnt + C_WEIGHT, s->cnt + C_ERR, sb ? sb->seg_count : nullptr, s->seg_g,
+                                         s->cnt + C_WEIGHT, s->cnt + C_ERR, sb ? sb->seg_count : nullptr, s->cmp_g,
                                          sb ? sb->seg_prefix : nullptr, s->cnt + C_LIVE);
       s->scan_pending = false;
     }
@@ -2152,7 +2157,7 @@ static int wait_slot(ghs_solver *s, const RoundSlot *hs, unsigned long long seq)
 static void advance_round(ghs_solver *s) {
   if (s->level_round >= 1) {  // this round's min-edge kernel compacted into the other buffer
     s->cur ^= 1;
-    s->cur_nseg = s->seg_g;
+    s->cur_nseg = s->cmp_g;
   }
   s->act_cur = s->act_ident ? 0 : (s->act_cur ^ 1);
   s->act_ident = false;
@@ -2303,6 +2308,10 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   if (const char *la = getenv("GHS_LOOKAHEAD")) {  // A/B tests: rounds in flight ahead of the check
     const long v = strtol(la, nullptr, 10);
     s->lookahead = (uint32_t)(v < 0 ? 0 : (v > 4 ? 4 : v));
+  }
+  if (const char *g = getenv("GHS_MINEDGE_G")) {  // A/B tests: blocks of the compacting min-edge
+    const long v = strtol(g, nullptr, 10);
+    s->cmp_g = (uint32_t)(v < 256 ? 256 : (v > (long)SEG_G ? SEG_G : v));
   }
   if (const char *g = getenv("GHS_SEG_G")) {  // A/B tests: blocks of the streaming kernels
     const long v = strtol(g, nullptr, 10);
