@@ -1713,6 +1713,9 @@ struct ghs_solver {
   bool time_rounds = false;     // GHS_TIME_ROUNDS=1: time the compacting min-edge launches (bench)
   uint32_t seg_g = SEG_G;       // blocks of the streaming kernels (GHS_SEG_G, 256..SEG_G)
   uint32_t cmp_g = CMP_G;       // blocks (= output regions) of the compacting min-edge (GHS_MINEDGE_G)
+  uint32_t ident_g = SEG_G;     // grid caps: round-0 min-edge (GHS_IDENT_G), k_win (GHS_WIN_G: 6
+  uint32_t win_g = CMP_G;       // blocks/CU like the compaction, measured ~1% faster per step),
+  uint32_t lp_g = SEG_G;        // the level pass (GHS_LP_G)
   bool open_async = false;      // the open level's counts arrive with its first round's report
   bool scan_pending = false;    // the last compaction's region counts are not scanned yet
   bool report_final = false;    // the last round report read holds the final weight / edge count
@@ -1969,7 +1972,7 @@ static int open_level(ghs_solver *s, bool async_open = false) {
     } else {
       // split the pending edges (total on the device): this level's inter-fragment edges -> Y;
       // heavier survivors -> RO regions. Fixed grid: block b owns 1/seg_g of the virtual range.
-      G = s->seg_g;
+      G = s->lp_g;
       SegView in{RI.seg_start, RI.seg_prefix, s->rem_nseg};
       k_level_pass<<<G, BLOCK, 0, st>>>(RI.src, RI.dst, RI.key, in, d_range + 1, s->lab, s->bits, s->giant, Y.src, Y.dst, Y.key,
                                         Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key, RO.seg_start, RO.seg_count,
@@ -2081,7 +2084,7 @@ static int enqueue_minedge(ghs_solver *s) {
   SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
   if (s->level_round == 0) {
     if (s->cur_arcs || !s->arcs_known)
-      k_minedge<true, false><<<s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->seg_g) : s->seg_g, BLOCK, 0, s->stream>>>(
+      k_minedge<true, false><<<s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->ident_g) : s->ident_g, BLOCK, 0, s->stream>>>(
           I.src, I.dst, I.key, in, s->lab, s->best, nullptr, nullptr, nullptr, nullptr, nullptr);
   } else {
     // fixed grid: every one of the seg_g blocks writes its region's count
@@ -2114,7 +2117,7 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
     if (edge_form) {
       const ArcBuf &I = s->buf[s->cur];
       SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
-      k_win<<<s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->seg_g) : s->seg_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->best,
+      k_win<<<s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->win_g) : s->win_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->best,
                                                                                    s->par, s->in_mst, s->cnt + C_WEIGHT);
     } else {
       const ArcBuf *sb = s->scan_pending ? s->scan_buf : nullptr;
@@ -2309,10 +2312,16 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
     const long v = strtol(la, nullptr, 10);
     s->lookahead = (uint32_t)(v < 0 ? 0 : (v > 4 ? 4 : v));
   }
-  if (const char *g = getenv("GHS_MINEDGE_G")) {  // A/B tests: blocks of the compacting min-edge
-    const long v = strtol(g, nullptr, 10);
-    s->cmp_g = (uint32_t)(v < 256 ? 256 : (v > (long)SEG_G ? SEG_G : v));
-  }
+  auto grid_env = [](const char *name, uint32_t *dst) {  // A/B tests: per-kernel grids
+    if (const char *g = getenv(name)) {
+      const long v = strtol(g, nullptr, 10);
+      *dst = (uint32_t)(v < 256 ? 256 : (v > (long)SEG_G ? SEG_G : v));
+    }
+  };
+  grid_env("GHS_MINEDGE_G", &s->cmp_g);
+  grid_env("GHS_IDENT_G", &s->ident_g);
+  grid_env("GHS_WIN_G", &s->win_g);
+  grid_env("GHS_LP_G", &s->lp_g);
   if (const char *g = getenv("GHS_SEG_G")) {  // A/B tests: blocks of the streaming kernels
     const long v = strtol(g, nullptr, 10);
     s->seg_g = (uint32_t)(v < 256 ? 256 : (v > (long)SEG_G ? SEG_G : v));
