@@ -800,6 +800,10 @@ __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act
   const uint64_t nact = *d_nact;
   for (uint64_t i = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; i < nact; i += (uint64_t)gridDim.x * BLOCK) {
     const uint32_t c = act ? act[i] : (uint32_t)i;
+    if (!act && lab[c] != c) {  // identity list: not a root when the level opened, never a label
+      flags[i] = 0;
+      continue;
+    }
     uint32_t x = c;
     uint32_t px = par[x];
     const bool root = px == c;
@@ -1918,11 +1922,12 @@ static int open_level(ghs_solver *s, bool async_open = false) {
 
   // 1. this level's edges -> regions of Y (level edges: a, b labels + key, canonical order).
   //    The pass also flags both ends of every level edge (the level's active fragments).
-  // Single rank, level 0, async open: no active flags at all. Round 0 runs over the identity
-  // list of all n vertices (k_win needs no list; k_jump keeps only the roots that found an
-  // outgoing edge), which costs a sequential pass over par/best instead of 2 random flag stores
-  // per level-0 edge inside k_select plus the select.
-  const bool ident0 = first && single && async_open;
+  // Single rank, async open: no active flags at all. Round 0 runs over the identity list of all
+  // n vertices (k_win needs no list; k_jump skips the vertices that were not roots when the level
+  // opened and keeps the roots that found an outgoing edge), which costs a sequential pass over
+  // lab/par/best instead of 2 random flag stores per level edge inside the pass (their line
+  // write-backs were ~0.25 GB per k_filter launch) plus the select.
+  const bool ident0 = single && async_open;
   uint8_t *mark = ident0 ? nullptr : s->flags;
   if (!ident0) GHS_HIP_CHECK(hipMemsetAsync(s->flags, 0, s->n, st));
   s->open_ident = ident0;
