@@ -825,6 +825,67 @@ __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act
   }
 }
 
+// Stage 3 over the identity list (a single-rank level's first round): every vertex, 4 per lane
+// per step with 16-byte loads of lab, par and best — a stream, where the generic k_jump issues
+// 4-byte loads. A vertex that was not a root when the level opened (lab[c] != c) is never a label
+// and is skipped; a root that did not hook only tests its best slot; a root that hooked walks.
+__global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par, uint32_t *__restrict__ lab,
+                                                      uint64_t *__restrict__ best, uint8_t *__restrict__ flags,
+                                                      unsigned long long *__restrict__ err) {
+  const uint64_t n4 = (uint64_t)n & ~3ull;
+  for (uint64_t i0 = (blockIdx.x * (uint64_t)BLOCK + threadIdx.x) * 4; i0 < n; i0 += (uint64_t)gridDim.x * BLOCK * 4) {
+    uint32_t lc[4], pc[4];
+    uint64_t bc[4];
+    if (i0 < n4) {
+      const uint4 l4 = *reinterpret_cast<const uint4 *>(lab + i0);
+      const uint4 p4 = *reinterpret_cast<const uint4 *>(par + i0);
+      const ulonglong2 b01 = *reinterpret_cast<const ulonglong2 *>(best + i0);
+      const ulonglong2 b23 = *reinterpret_cast<const ulonglong2 *>(best + i0 + 2);
+      lc[0] = l4.x; lc[1] = l4.y; lc[2] = l4.z; lc[3] = l4.w;
+      pc[0] = p4.x; pc[1] = p4.y; pc[2] = p4.z; pc[3] = p4.w;
+      bc[0] = b01.x; bc[1] = b01.y; bc[2] = b23.x; bc[3] = b23.y;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool in = i0 + k < n;
+        lc[k] = in ? lab[i0 + k] : LABEL_NONE;
+        pc[k] = in ? par[i0 + k] : 0u;
+        bc[k] = in ? best[i0 + k] : KEY_NONE;
+      }
+    }
+    uint32_t kb = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t c = (uint32_t)(i0 + k);
+      if (lc[k] != c) continue;  // not a root at the level's open (or past n)
+      if (pc[k] == c) {          // still a root: kept iff it had an outgoing edge
+        if (bc[k] != KEY_NONE) {
+          best[c] = KEY_NONE;
+          kb |= 1u << (8 * k);
+        }
+        continue;
+      }
+      uint32_t x = c, px = pc[k];  // hooked: walk to the root (path splitting)
+      uint32_t steps = 0;
+      while (px != x) {
+        const uint32_t ppx = par[px];
+        if (ppx != px) par[x] = ppx;
+        x = px;
+        px = ppx;
+        if (++steps > JUMP_MAX_STEPS) {
+          atomicOr(err, 4ull);
+          break;
+        }
+      }
+      lab[c] = x;
+    }
+    if (i0 < n4) *reinterpret_cast<uint32_t *>(flags + i0) = kb;
+    else
+      for (int k = 0; k < 4; ++k)
+        if (i0 + k < n) flags[i0 + k] = (uint8_t)(kb >> (8 * k));
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Between levels. k_giant first: the giant fragment = the most frequent root among NSAMPLE
 // evenly spaced vertices (ties: the smaller label), each sample resolved by its own walk and
@@ -2134,7 +2195,11 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
     GHS_HIP_CHECK(hipGetLastError());
     if (s->detail) record(s, 2);
     // Stage 3, then the next active list (one launch each)
-    k_jump<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->par, s->lab, s->best, s->flags, s->cnt + C_ERR);
+    if (s->act_ident && s->cfg.num_ranks <= 1)
+      k_jump_ident<<<grid_for(((uint64_t)s->n + 3) / 4, BLOCK, 16384), BLOCK, 0, s->stream>>>(s->n, s->par, s->lab, s->best,
+                                                                                          s->flags, s->cnt + C_ERR);
+    else
+      k_jump<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->par, s->lab, s->best, s->flags, s->cnt + C_ERR);
     GHS_HIP_CHECK(hipGetLastError());
     if (s->detail) record(s, 3);
     if (int rc = select_lb(s, act, d_nact, bound, s->act[nb], act_count(s, nb), slot, seq)) return rc;
