@@ -1688,13 +1688,17 @@ struct HostRes {
   unsigned long long seq = 0;           // round reports issued through h_slot (monotonic across solves)
 };
 
+// Timing-only events: no system-scope fence when they are recorded (they are read only through
+// hipEventElapsedTime after the stream is synchronized).
+constexpr unsigned TIMING_EVENT_FLAGS = hipEventDisableSystemFence;
+
 static int hostres_init(HostRes *r) {
   GHS_HIP_CHECK(hipHostMalloc((void **)&r->h_cnt, C_COUNT * sizeof(unsigned long long), hipHostMallocDefault));
   // round slots: written by the round's last kernel, read by the host after seq has landed
   GHS_HIP_CHECK(hipHostMalloc((void **)&r->h_slot, SLOT_RING * sizeof(RoundSlot), hipHostMallocMapped | hipHostMallocCoherent));
   GHS_HIP_CHECK(hipHostGetDevicePointer((void **)&r->d_slot, r->h_slot, 0));
   GHS_HIP_CHECK(hipHostMalloc((void **)&r->h_sample, 16384 * 4, hipHostMallocDefault));
-  for (int i = 0; i < 4; ++i) GHS_HIP_CHECK(hipEventCreate(&r->pass_ev[i]));
+  for (int i = 0; i < 4; ++i) GHS_HIP_CHECK(hipEventCreateWithFlags(&r->pass_ev[i], TIMING_EVENT_FLAGS));
   GHS_HIP_CHECK(hipEventCreateWithFlags(&r->plan_ev, hipEventDisableTiming));
   memset(r->h_slot, 0, SLOT_RING * sizeof(RoundSlot));
   return GHS_OK;
@@ -1862,7 +1866,7 @@ static hipEvent_t round_event(ghs_solver *s, uint32_t round, int k) {
   std::vector<hipEvent_t> &pool = s->res->ev_pool;
   while (pool.size() <= idx) {
     hipEvent_t ev = nullptr;
-    if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&ev, TIMING_EVENT_FLAGS) != hipSuccess) return nullptr;
     pool.push_back(ev);
   }
   return pool[idx];
@@ -2212,11 +2216,19 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
 }
 
 // spin until the round report with this seq has landed in the pinned slot (the stream keeps
-// running); a failed or drained stream without the report is an error, never a hang
+// running); a failed or drained stream without the report is an error, never a hang. The stream
+// is queried only after SLOT_QUIET_MS of waiting: hipStreamQuery enqueues a marker behind the
+// last launch, and its system-scope release idled the GPU ~5.6 us before every round >= 2.
+constexpr int SLOT_QUIET_MS = 20;
 static int wait_slot(ghs_solver *s, const RoundSlot *hs, unsigned long long seq) {
+  if (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) == seq) return GHS_OK;
+  const auto t0 = std::chrono::steady_clock::now();
   unsigned spins = 0;
+  bool quiet = true;
   while (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) != seq) {
-    if ((++spins & 255) == 0) {
+    if ((++spins & 255) == 0 && quiet)
+      quiet = std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(SLOT_QUIET_MS);
+    if (!quiet && (spins & 255) == 0) {
       const hipError_t q = hipStreamQuery(s->stream);
       if (q != hipSuccess && q != hipErrorNotReady) GHS_HIP_CHECK(q);
       if (q == hipSuccess && __atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) != seq)
