@@ -1913,8 +1913,19 @@ static int select_lb(ghs_solver *s, const uint32_t *act, const unsigned long lon
 static void default_config(ghs_config_t *c) {
   c->max_levels = 8;
   c->num_ranks = 1;
-  c->level1_edges_per_vertex = 0.5;
+  c->level1_edges_per_vertex = 0.0;  // auto: level1_auto()
   c->level_growth = 8.0;  // R-MAT s24 sweep (tools/sweep_levels.py): 3 levels, 0.5n / 4n / rest
+}
+
+// level1_edges_per_vertex <= 0 picks the first level's size from the density. The first level
+// should just reach the point where a giant fragment forms (the filter of the later levels drops
+// the edges inside it) without paying for an extra level of n-sized passes: 0.5n edges for dense
+// random-like graphs (R-MAT s24: 6.18 ms vs 6.98 at 1.0n), n edges for sparse lattice-like ones
+// (bond percolation of the square lattice at half the edges; 16384^2 grid: 56 ms vs 72 at 0.5n;
+// profiles/r01/sweep_levels_*.jsonl).
+static double level1_auto(const ghs_config_t &c, uint32_t n, uint64_t m) {
+  if (c.level1_edges_per_vertex > 0) return c.level1_edges_per_vertex;
+  return (m >= 4ull * n) ? 0.5 : 1.0;
 }
 
 // ---- level planning: thresholds from a sample of the GLOBAL canonical weights ----------------
@@ -1929,7 +1940,7 @@ static int plan_levels_enqueue(ghs_solver *s) {
   const uint32_t L = plan_levels_count(s);
   const uint32_t ns = (L > 1 && s->m > 0) ? (uint32_t)std::min<uint64_t>(NSAMPLE_W, s->m) : 0u;
   if (ns) k_sample_weights<<<grid_for(ns, 256, 256), 256, 0, s->stream>>>(s->m, s->ew, ns, s->sample);
-  k_plan<<<1, 1024, 0, s->stream>>>(s->sample, ns, s->n, s->m, L, s->cfg.level1_edges_per_vertex, s->cfg.level_growth,
+  k_plan<<<1, 1024, 0, s->stream>>>(s->sample, ns, s->n, s->m, L, level1_auto(s->cfg, s->n, s->m), s->cfg.level_growth,
                                     s->d_thr);
   GHS_HIP_CHECK(hipGetLastError());
   GHS_HIP_CHECK(hipMemcpyAsync(s->h_thr, s->d_thr, (PLAN_MAX + 1) * 8, hipMemcpyDeviceToHost, s->stream));

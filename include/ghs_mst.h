@@ -80,7 +80,8 @@ typedef struct ghs_result {
  * level1_edges_per_vertex * n lightest edges, each further level level_growth times more, the
  * last level the rest; max_levels = 1 runs plain Boruvka over every edge at once. Thresholds
  * are weight quantiles of a fixed sample of the canonical list, so every rank plans the same
- * levels. Results do not depend on the plan (only speed does). */
+ * levels. level1_edges_per_vertex <= 0 (the default) = auto: 0.5 when m >= 4n, else 1.0.
+ * Results do not depend on the plan (only speed does). */
 typedef struct ghs_config {
   uint32_t max_levels;
   uint32_t num_ranks;         /* ranks sharing the solve (1 = single GPU; >1: identical rounds on
