@@ -1794,6 +1794,7 @@ struct ghs_solver {
   bool arcs_known = true;       // cur_arcs holds the exact live edge count (else: unknown, grids sized for the bound)
   uint32_t lookahead = LOOKAHEAD;  // rounds in flight ahead of the termination check (GHS_LOOKAHEAD)
   std::chrono::steady_clock::time_point t0;
+  char *ws_base = nullptr;      // the caller's workspace (carved by workspace_layout)
 };
 
 static std::mutex g_mutex;  // the one-shot entry points are serialised per process
@@ -2377,6 +2378,33 @@ size_t ghs_workspace_bytes(uint32_t n, uint64_t m, uint64_t local_edges) {
   return workspace_layout(n, local_edges, nullptr, nullptr);
 }
 
+// The per-solve start of a solver: plan, state arrays, counters (create, and reset between solves).
+static int solver_begin(ghs_solver *s) {
+  hipError_t e;
+  const uint32_t n = s->n;
+  const uint64_t m = s->m;
+  s->h_cnt = s->res->h_cnt;
+  s->h_slot = s->res->h_slot;
+  s->d_slot = s->res->d_slot;
+  s->h_sample = s->res->h_sample;
+  s->h_thr = reinterpret_cast<uint64_t *>(s->res->h_sample);
+  s->t0 = std::chrono::steady_clock::now();
+  if (int rc = plan_levels_enqueue(s)) return rc;
+  if (n) {
+    if ((e = hipMemsetAsync(s->best, 0xff, (size_t)n * 8, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset best: ") + hipGetErrorString(e));
+    k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->lab, n);
+    k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->par, n);  // every root: par[r] == r
+  }
+  if (m && (e = hipMemsetAsync(s->in_mst, 0, m, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset in_mst: ") + hipGetErrorString(e));
+  if ((e = hipMemsetAsync(s->lb_state, 0, LB_MAX_TILES * 8, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset select state: ") + hipGetErrorString(e));
+  k_init_counters<<<1, 64, 0, s->stream>>>(s->cnt, n);
+  if ((e = hipGetLastError()) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("init kernels: ") + hipGetErrorString(e));
+  s->level = 0;
+  s->level_open = false;
+  s->phase = n ? 0 : 2;
+  return GHS_OK;
+}
+
 int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
                       uint64_t e_lo, uint64_t e_hi, const ghs_config_t *cfg, void *d_workspace,
                       size_t workspace_bytes, uint8_t *d_in_mst, void *stream, ghs_solver_t **out) {
@@ -2420,13 +2448,9 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
     s->seg_g = (uint32_t)(v < 256 ? 256 : (v > (long)SEG_G ? SEG_G : v));
   }
   if (cfg) s->cfg = *cfg; else default_config(&s->cfg);
-  workspace_layout(n, e_hi - e_lo, s, (char *)d_workspace);
-  hipError_t e;
-  auto fail = [&](hipError_t err, const char *what) {
-    set_error(std::string(what) + ": " + hipGetErrorString(err));
-    ghs_solver_destroy(s);
-    return GHS_E_HIP;
-  };
+  s->ws_base = (char *)d_workspace;
+  workspace_layout(n, e_hi - e_lo, s, s->ws_base);
+
   if (g_create_pool) {
     s->res = g_create_pool;
   } else {
@@ -2436,29 +2460,10 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
       return rc;
     }
   }
-  s->h_cnt = s->res->h_cnt;
-  s->h_slot = s->res->h_slot;
-  s->d_slot = s->res->d_slot;
-  s->h_sample = s->res->h_sample;
-  s->h_thr = reinterpret_cast<uint64_t *>(s->res->h_sample);
-  s->t0 = std::chrono::steady_clock::now();
-  int rc = plan_levels_enqueue(s);
-  if (rc) {
+  if (int rc = solver_begin(s)) {
     ghs_solver_destroy(s);
     return rc;
   }
-  if (n) {
-    if ((e = hipMemsetAsync(s->best, 0xff, (size_t)n * 8, s->stream)) != hipSuccess) return fail(e, "memset best");
-    k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->lab, n);
-    k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->par, n);  // every root: par[r] == r
-  }
-  if (m && (e = hipMemsetAsync(s->in_mst, 0, m, s->stream)) != hipSuccess) return fail(e, "memset in_mst");
-  if ((e = hipMemsetAsync(s->lb_state, 0, LB_MAX_TILES * 8, s->stream)) != hipSuccess) return fail(e, "memset select state");
-  k_init_counters<<<1, 64, 0, s->stream>>>(s->cnt, n);
-  if ((e = hipGetLastError()) != hipSuccess) return fail(e, "init kernels");
-  s->level = 0;
-  s->level_open = false;
-  s->phase = n ? 0 : 2;
   *out = s;
   return GHS_OK;
 }
@@ -2599,6 +2604,28 @@ int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *
     result->filter_out = s->filter_out;
   }
   return GHS_OK;
+}
+
+int ghs_solver_reset(ghs_solver_t *s) {
+  if (!s) GHS_FAIL(GHS_E_ARG, "solver is NULL");
+  // a fresh round state over the same inputs, workspace, knobs and host resources
+  ghs_solver t;
+  t.n = s->n; t.m = s->m; t.e_lo = s->e_lo; t.e_hi = s->e_hi;
+  t.eu = s->eu; t.ev = s->ev; t.ew = s->ew;
+  t.in_mst = s->in_mst; t.stream = s->stream; t.cfg = s->cfg;
+  t.debug = s->debug; t.lookahead = s->lookahead;
+  { const char *det = getenv("GHS_DETAIL"); t.detail = det && det[0] == '1'; }
+  { const char *tr = getenv("GHS_TIME_ROUNDS"); t.time_rounds = tr && tr[0] == '1'; }
+  t.seg_g = s->seg_g; t.cmp_g = s->cmp_g; t.ident_g = s->ident_g; t.win_g = s->win_g; t.lp_g = s->lp_g;
+  t.ws_base = s->ws_base;
+  workspace_layout(t.n, t.e_hi - t.e_lo, &t, t.ws_base);
+  const bool owned = s->res == &s->own;
+  HostRes *pool = s->res;
+  t.own = std::move(s->own);
+  s->own = HostRes();
+  *s = std::move(t);
+  s->res = owned ? &s->own : pool;
+  return solver_begin(s);
 }
 
 int ghs_solver_destroy(ghs_solver_t *s) {

@@ -76,6 +76,10 @@ class HipStepper:
         _native.check(self.L.ghs_solver_finish(self.h, ctypes.byref(res), stats))
         return res, _native.RoundStatsList(stats, res.num_stats)
 
+    def reset(self):
+        """Start the next solve on the same handle (no new host resources)."""
+        _native.check(self.L.ghs_solver_reset(self.h))
+
     def close(self):
         if self.h:
             self.L.ghs_solver_destroy(self.h)
@@ -150,15 +154,26 @@ class DistributedMST:
         config.num_ranks = self.world
         self.engine = DeviceMST(edges, lo, hi, config)
         self.edges = edges
+        self.stepper = None
 
     def run(self):
-        """The level/round loop over the owned edge range. Returns (Result, stats)."""
-        st = HipStepper(self.engine)
+        """The level/round loop over the owned edge range. Returns (Result, stats). The solver
+        handle is created once and reset for every later solve."""
+        if self.stepper is None:
+            self.stepper = HipStepper(self.engine)
+        else:
+            self.stepper.reset()
         try:
-            run_rounds(st, torch_allreduce_min(self.group))
-            return st.finish()
-        finally:
-            st.close()
+            run_rounds(self.stepper, torch_allreduce_min(self.group))
+            return self.stepper.finish()
+        except BaseException:
+            self.close()
+            raise
+
+    def close(self):
+        if self.stepper is not None:
+            self.stepper.close()
+            self.stepper = None
 
     def in_mst_host(self):
         return self.engine.in_mst_host()

@@ -168,6 +168,9 @@ int ghs_solver_unpack_best(ghs_solver_t *h, const int64_t *d_dense);
 /* hook + jump + next list; *done = 1 when every level is complete */
 int ghs_solver_contract(ghs_solver_t *h, int *done);
 int ghs_solver_finish(ghs_solver_t *h, ghs_result_t *result, ghs_round_stats_t *stats);
+/* start the next solve of the same inputs on the same handle (keeps the workspace layout and the
+ * pinned host resources: a multi-GPU caller's per-solve create/destroy becomes one reset) */
+int ghs_solver_reset(ghs_solver_t *h);
 int ghs_solver_destroy(ghs_solver_t *h);
 
 /* ---- synthetic graph generators (device; BASELINE.json configs 3-5) ----------------------

@@ -143,9 +143,16 @@ def test_stepwise_solver_equals_monolithic(torch_cuda):
     st = HipStepper(b)
     run_rounds(st, lambda t: None)
     rb, _ = st.finish()
-    st.close()
     assert np.array_equal(a.in_mst_host(), b.in_mst_host())
     assert ra.total_weight == rb.total_weight and ra.rounds == rb.rounds
+    # the same handle again after ghs_solver_reset (what DistributedMST does per solve)
+    b.in_mst.fill_(7)
+    st.reset()
+    run_rounds(st, lambda t: None)
+    rc, _ = st.finish()
+    st.close()
+    assert np.array_equal(a.in_mst_host(), b.in_mst_host())
+    assert rc.total_weight == ra.total_weight and rc.rounds == ra.rounds
 
 
 @pytest.mark.parametrize("world", [2, 3])

@@ -1,0 +1,120 @@
+"""Per-rank cost of the multi-GPU decomposition, emulated on ONE GPU (no RCCL).
+
+N edge-range engines (one per emulated rank) step through the level/round loop in one process;
+the collectives are emulated with torch.maximum / torch.minimum and are NOT timed. Each rank's
+library calls are bracketed by torch.cuda.synchronize(), so per round we get every rank's own
+GPU+host time; the projected step time of a real N-GPU run is
+    sum over rounds of max over ranks (compute)  +  collectives (payload bytes listed per round)
+The result must equal the single-GPU MSF (asserted).
+
+    python tools/dist_emulate.py --scale 26 --world 8
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=int, default=24)
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--reps", type=int, default=2)
+    args = ap.parse_args()
+    import torch
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import DeviceMST, edge_range, generate_rmat
+    from distributed_ghs_implementation_amd.distributed import HipStepper
+
+    e = generate_rmat(args.scale, 16, seed=1, wseed=2)
+    ref = DeviceMST(e)
+    rres, _ = ref.run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ref.run()
+    torch.cuda.synchronize()
+    one_ms = (time.perf_counter() - t0) * 1e3
+    ref_flags = ref.in_mst[: e.m].clone()
+    del ref
+    torch.cuda.empty_cache()
+
+    W = args.world
+    cfg = _native.make_config(num_ranks=W)
+    engines = [DeviceMST(e, *edge_range(e.m, r, W), config=cfg) for r in range(W)]
+    steppers = [HipStepper(x) for x in engines]
+
+    def timed(r, fn):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        out = fn()
+        torch.cuda.synchronize()
+        return out, (time.perf_counter() - t) * 1e3
+
+    for rep in range(args.reps):
+        if rep:
+            for s in steppers:
+                s.reset()
+        rounds = []
+        done = False
+        while not done:
+            ms = [0.0] * W
+            coll = []
+            counts = []
+            for r, s in enumerate(steppers):
+                c, t = timed(r, s.minedge)
+                counts.append(c)
+                ms[r] += t
+            while counts[0] is None:
+                bufs = [s.exchange_buffer() for s in steppers]
+                red = bufs[0].clone()
+                for b in bufs[1:]:
+                    red = torch.maximum(red, b)
+                for b in bufs:
+                    b.copy_(red)
+                coll.append(("allreduce_max_u8", int(red.numel())))
+                counts = []
+                for r, s in enumerate(steppers):
+                    c, t = timed(r, s.minedge)
+                    counts.append(c)
+                    ms[r] += t
+            assert len(set(counts)) == 1
+            if counts[0]:
+                dense = []
+                for r, s in enumerate(steppers):
+                    d, t = timed(r, lambda: s.pack(counts[0]).clone())
+                    dense.append(d)
+                    ms[r] += t
+                red = dense[0]
+                for d in dense[1:]:
+                    red = torch.minimum(red, d)
+                coll.append(("allreduce_min_i64", int(red.numel()) * 8))
+                for r, s in enumerate(steppers):
+                    _, t = timed(r, lambda: s.unpack(red))
+                    ms[r] += t
+            dones = []
+            for r, s in enumerate(steppers):
+                d, t = timed(r, s.contract)
+                dones.append(d)
+                ms[r] += t
+            assert len(set(dones)) == 1
+            done = dones[0]
+            rounds.append({"max_rank_ms": round(max(ms), 4), "min_rank_ms": round(min(ms), 4), "collectives": coll})
+        res = [s.finish()[0] for s in steppers]
+        for x in engines:
+            assert torch.equal(x.in_mst[: e.m], ref_flags), "emulated ranks differ from the single-GPU MSF"
+        assert all(r.total_weight == rres.total_weight for r in res)
+        compute = sum(r["max_rank_ms"] for r in rounds)
+        payload = sum(b for r in rounds for _, b in r["collectives"])
+        print(json.dumps({"scale": args.scale, "world": W, "rep": rep, "m": e.m, "n": e.n,
+                          "single_gpu_ms": round(one_ms, 3), "rounds": len(rounds),
+                          "sum_max_rank_compute_ms": round(compute, 3), "collective_bytes": payload,
+                          "per_round": rounds}), flush=True)
+    for s in steppers:
+        s.close()
+
+
+if __name__ == "__main__":
+    main()
