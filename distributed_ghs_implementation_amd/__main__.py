@@ -8,6 +8,10 @@
     --mpi-compat   also write <graph-dir>/mst_result_mpi.json (same content)
     --graph FILE   read an .mstbin binary graph instead of a directory
     --output FILE  result path (default <graph-dir>/ghs_mst.json)
+    --check        verify the result after the run (verify.py: forest, spans every component,
+                   weight vs NetworkX when available — the reference's check_mst.py)
+    --check-result FILE
+                   verify an existing result JSON against the graph; no GPU, no solve
 
 Multi-GPU (one process per GPU):
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
@@ -26,6 +30,8 @@ def main(argv=None):
     ap.add_argument("--output", type=str, default=None)
     ap.add_argument("--mpi-compat", action="store_true")
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--check", action="store_true", help="verify the result (check_mst.py)")
+    ap.add_argument("--check-result", type=str, default=None, help="verify an existing result JSON only")
     args = ap.parse_args(argv)
 
     from . import graph as G
@@ -33,6 +39,16 @@ def main(argv=None):
     t0 = time.perf_counter()
     g = G.read_mstbin(args.graph) if args.graph else G.read_graph_dir(args.graph_dir)
     t_read = time.perf_counter() - t0
+
+    if args.check_result:
+        import json
+
+        from .verify import format_report, verify_forest
+        with open(args.check_result) as f:
+            triples = [tuple(e) for e in json.load(f)["mst_edges"]]
+        rep = verify_forest(g, triples)
+        print(format_report(rep, triples))
+        return 0 if rep["ok"] else 1
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -75,6 +91,11 @@ def main(argv=None):
         else:
             print(f"Spanning forest: {g.n - res['num_edges']} components")
         print(f"Results saved to: {out}")
+    if args.check:
+        from .verify import format_report, verify_forest
+        rep = verify_forest(g, triples)
+        print(format_report(rep, triples))
+        return 0 if rep["ok"] else 1
     return 0
 
 

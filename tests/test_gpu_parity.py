@@ -6,6 +6,7 @@ Boruvka (tests/torch_boruvka.py, itself pinned against the oracle on CPU) and ch
 size-independent properties: a connected grid gives n - 1 edges, the flags do not depend on
 the level plan or on the rank partition, and repeated solves are identical.
 """
+import os
 import numpy as np
 import pytest
 
@@ -339,3 +340,18 @@ def test_grid_16k_full_size(mode, torch_cuda):
     res, _ = eng.run()
     assert res.num_mst_edges == k * k - 1
     _full_size_checks(e, eng, res, torch)
+
+
+def test_cli_graph_dir_with_check(tmp_path, torch_cuda):
+    """The reference's CLI flow end to end on the reference's own graph-file directory
+    (create_graph_files.py output): --graph-dir D -> ghs_mst.json, then --check (check_mst.py)."""
+    import json
+    import shutil
+
+    from conftest import GOLDEN
+    from distributed_ghs_implementation_amd.__main__ import main
+    d = tmp_path / "graph_data"
+    shutil.copytree(os.path.join(GOLDEN, "graph_data_n6"), d)
+    assert main(["--graph-dir", str(d), "--check", "--quiet"]) == 0
+    res = json.load(open(d / "ghs_mst.json"))
+    assert res["total_weight"] == 11 and res["num_edges"] == 5  # README_MPI.md:228-235

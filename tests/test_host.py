@@ -86,3 +86,64 @@ def test_result_schema(tmp_path):
     assert set(res) == {"mst_edges", "total_weight", "num_edges", "algorithm"}
     assert res["mst_edges"] == [[0, 2, 2], [0, 3, 1], [3, 5, 2]]
     assert res["total_weight"] == 5 and res["num_edges"] == 3
+
+
+def _fixture_graph_and_result(name):
+    fx = load_fixture(name)
+    g = G.canonicalize(fx["num_nodes"], edges=fx["edges"])
+    return g, [tuple(e) for e in fx["expected_mst_edges"]], fx
+
+
+@pytest.mark.parametrize("name", fixture_names())
+def test_verify_accepts_oracle_msf(name):
+    """verify.py (the check_mst.py equivalent) accepts the pinned canonical MSF of every fixture."""
+    from distributed_ghs_implementation_amd.verify import verify_forest
+    g, exp, fx = _fixture_graph_and_result(name)
+    rep = verify_forest(g, exp)
+    assert rep["ok"], rep
+    assert rep["mst_weight"] == fx["expected_total_weight"]
+    assert rep["mst_edges"] == rep["edges_expected"]
+    if rep["networkx_weight"] is not None:
+        assert rep["weight_matches_networkx"]
+
+
+def test_verify_rejects_broken_results():
+    from distributed_ghs_implementation_amd.verify import verify_forest
+    g, exp, _ = _fixture_graph_and_result("readme6.json")
+    assert verify_forest(g, exp)["ok"]
+    assert not verify_forest(g, exp[:-1])["spans_components"]          # an edge missing
+    extra = [e for e in g.edge_triples() if e not in exp][0]
+    assert not verify_forest(g, exp + [extra])["is_forest"]            # a cycle
+    bad_w = [(exp[0][0], exp[0][1], exp[0][2] + 1)] + exp[1:]
+    assert not verify_forest(g, bad_w)["weights_match_graph"]          # wrong weight
+    assert not verify_forest(g, [(0, 5, 1)] + exp[1:])["edges_in_graph"]  # not a graph edge
+    # a spanning tree that is not minimum: structurally fine, rejected by the NetworkX weight
+    pytest.importorskip("networkx")
+    heavier = [e for e in exp if e != (0, 1, 1)] + [(0, 2, 4)]
+    rep = verify_forest(g, heavier)
+    assert rep["is_forest"] and rep["spans_components"] and not rep["ok"]
+
+
+def test_experiment_record_schema():
+    """ghs_experiments.json entry (ghs_implementation.py:766-776)."""
+    from distributed_ghs_implementation_amd.verify import experiment_record
+    g, exp, fx = _fixture_graph_and_result("readme6.json")
+    rec = experiment_record(1, g, exp)
+    assert list(rec) == ["experiment", "num_nodes", "num_edges", "mst_edges", "mst_weight", "networkx_weight",
+                         "is_correct", "edges_found", "edges_expected"]
+    assert rec["mst_weight"] == 20 and rec["is_correct"] and rec["edges_found"] == rec["edges_expected"] == 5
+
+
+def test_cli_check_result_without_gpu(tmp_path):
+    """`python -m distributed_ghs_implementation_amd --graph-dir D --check-result F`: the
+    check_mst.py flow on the reference's own graph-file directory, no GPU needed."""
+    from distributed_ghs_implementation_amd.__main__ import main
+    g, exp, _ = _fixture_graph_and_result("readme6.json")
+    d = tmp_path / "graph"
+    G.write_graph_dir(g, str(d))
+    good = tmp_path / "good.json"
+    G.write_result(str(good), exp)
+    assert main(["--graph-dir", str(d), "--check-result", str(good)]) == 0
+    bad = tmp_path / "bad.json"
+    G.write_result(str(bad), exp[:-1])
+    assert main(["--graph-dir", str(d), "--check-result", str(bad)]) == 1
