@@ -655,7 +655,8 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
                                                 unsigned long long *__restrict__ acc /* [0] weight, [1] edges */,
                                                 unsigned long long *__restrict__ err,
                                                 const uint64_t *__restrict__ scan_count, uint32_t scan_n,
-                                                uint64_t *__restrict__ scan_prefix, unsigned long long *__restrict__ scan_total) {
+                                                uint64_t *__restrict__ scan_prefix, unsigned long long *__restrict__ scan_total,
+                                                bool resolved) {
   __shared__ unsigned long long s_w[BLOCK / WAVE], s_c[BLOCK / WAVE];
   unsigned long long wsum = 0, cnt = 0;
   const uint64_t nact = *d_nact;
@@ -665,8 +666,9 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
     uint32_t p = c;
     if (k != KEY_NONE) {
       const uint32_t eid = (uint32_t)k;
-      const uint32_t la = find_lab(lab, eu[eid], err);
-      const uint32_t lb = find_lab(lab, ev[eid], err);
+      // a level's first round: k_resolve left every label a root (one read, no walk)
+      const uint32_t la = resolved ? lab[eu[eid]] : find_lab(lab, eu[eid], err);
+      const uint32_t lb = resolved ? lab[ev[eid]] : find_lab(lab, ev[eid], err);
       if (la != c && lb != c) atomicOr(err, 2ull);  // the chosen edge must leave c
       const uint32_t other = (la == c) ? lb : la;
       const bool mutual = best[other] == k;
@@ -2205,7 +2207,7 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
       const ArcBuf *sb = s->scan_pending ? s->scan_buf : nullptr;
       k_hook<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
                                          s->cnt + C_WEIGHT, s->cnt + C_ERR, sb ? sb->seg_count : nullptr, s->cmp_g,
-                                         sb ? sb->seg_prefix : nullptr, s->cnt + C_LIVE);
+                                         sb ? sb->seg_prefix : nullptr, s->cnt + C_LIVE, s->level_round == 0);
       s->scan_pending = false;
     }
     GHS_HIP_CHECK(hipGetLastError());
