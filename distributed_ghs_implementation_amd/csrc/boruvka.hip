@@ -73,6 +73,14 @@ constexpr uint32_t SEG_MAX = SEG_G * 4;  // segments of a wave-private output (o
 // fastest there).
 constexpr uint32_t CMP_G = 1536;
 constexpr int FIND_LAB_MAX_HOPS = 256;
+// Rounds >= 1 of one rank: CONNECT in edge form (k_win over the compacted survivors, which carry
+// the current roots) while live edges < EDGE_HOOK_RATIO x active fragments — lattice-like levels,
+// where most fragments are still small (16384^2 grid: ~1.4 survivors per fragment) and k_hook's
+// per-fragment gathers of the canonical endpoints dominate; fragment form (k_hook) otherwise.
+// Chosen on the device from the exact counts; the host enqueues both only while its bound on the
+// active fragments is at least EDGE_HOOK_MIN_BOUND.
+constexpr uint64_t EDGE_HOOK_RATIO = 4;
+constexpr uint64_t EDGE_HOOK_MIN_BOUND = 1u << 20;
 constexpr uint32_t JUMP_MAX_STEPS = 1u << 26;
 
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
@@ -656,10 +664,11 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
                                                 unsigned long long *__restrict__ err,
                                                 const uint64_t *__restrict__ scan_count, uint32_t scan_n,
                                                 uint64_t *__restrict__ scan_prefix, unsigned long long *__restrict__ scan_total,
-                                                bool resolved) {
+                                                bool resolved, const unsigned long long *__restrict__ guard_live) {
   __shared__ unsigned long long s_w[BLOCK / WAVE], s_c[BLOCK / WAVE];
   unsigned long long wsum = 0, cnt = 0;
   const uint64_t nact = *d_nact;
+  if (guard_live && *guard_live < EDGE_HOOK_RATIO * nact) return;  // k_win of this round hooks
   for (uint64_t i = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; i < nact; i += (uint64_t)gridDim.x * BLOCK) {
     const uint32_t c = act ? act[i] : (uint32_t)i;
     const uint64_t k = best[c];
@@ -717,10 +726,14 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
 GHS_STREAM_KERNEL_6 void k_win(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
                              const uint64_t *__restrict__ key, SegView in, const uint64_t *__restrict__ best,
                              uint32_t *__restrict__ par, uint8_t *__restrict__ in_mst,
-                             unsigned long long *__restrict__ acc /* [0] weight, [1] edges */) {
+                             unsigned long long *__restrict__ acc /* [0] weight, [1] edges */,
+                             const unsigned long long *__restrict__ guard_nact) {
   __shared__ uint32_t s_seg[2];
   __shared__ unsigned long long s_w[BLOCK / WAVE], s_c[BLOCK / WAVE];
   const uint64_t T = in.prefix[in.nseg];
+  // device-side choice of the CONNECT form (rounds >= 1): the edge form only while the live
+  // edges are fewer than EDGE_HOOK_RATIO x the active fragments (k_hook takes the other case)
+  if (guard_nact && T >= EDGE_HOOK_RATIO * *guard_nact) return;
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
   const uint64_t vb = Q * blockIdx.x;
   const uint64_t ve = (vb + Q < T) ? vb + Q : T;
@@ -2198,16 +2211,28 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
     const bool edge_form =
         s->cfg.num_ranks <= 1 && s->level_round == 0 && (!s->arcs_known || s->cur_arcs < 8 * bound);
     if (edge_form && s->scan_pending) flush_scan(s);
+    const bool dual = !edge_form && s->cfg.num_ranks <= 1 && s->level_round >= 1 && bound >= EDGE_HOOK_MIN_BOUND;
     if (edge_form) {
       const ArcBuf &I = s->buf[s->cur];
       SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
       k_win<<<s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->win_g) : s->win_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->best,
-                                                                                   s->par, s->in_mst, s->cnt + C_WEIGHT);
+                                                                                   s->par, s->in_mst, s->cnt + C_WEIGHT, nullptr);
+    } else if (dual) {
+      // this round's compaction output (the survivors, relabelled to the current roots)
+      if (s->scan_pending) flush_scan(s);
+      const ArcBuf &O = s->buf[s->cur ^ 1];
+      SegView in{O.seg_start, O.seg_prefix, s->cmp_g};
+      k_win<<<s->win_g, BLOCK, 0, s->stream>>>(O.src, O.dst, O.key, in, s->best, s->par, s->in_mst, s->cnt + C_WEIGHT,
+                                               d_nact);
+      GHS_HIP_CHECK(hipGetLastError());
+      k_hook<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
+                                         s->cnt + C_WEIGHT, s->cnt + C_ERR, nullptr, 0, nullptr, nullptr, false,
+                                         s->cnt + C_LIVE);
     } else {
       const ArcBuf *sb = s->scan_pending ? s->scan_buf : nullptr;
       k_hook<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
                                          s->cnt + C_WEIGHT, s->cnt + C_ERR, sb ? sb->seg_count : nullptr, s->cmp_g,
-                                         sb ? sb->seg_prefix : nullptr, s->cnt + C_LIVE, s->level_round == 0);
+                                         sb ? sb->seg_prefix : nullptr, s->cnt + C_LIVE, s->level_round == 0, nullptr);
       s->scan_pending = false;
     }
     GHS_HIP_CHECK(hipGetLastError());
