@@ -39,6 +39,7 @@ EXPORTED_SYMBOLS = (
     "ghs_solver_create", "ghs_solver_minedge", "ghs_solver_exchange_buffer", "ghs_solver_pack_best",
     "ghs_solver_unpack_best",
     "ghs_solver_contract", "ghs_solver_finish", "ghs_solver_reset", "ghs_solver_destroy",
+    "ghs_solver_hook_local", "ghs_solver_unpack_hook",
     "ghs_rmat_temp_bytes", "ghs_rmat_generate", "ghs_grid_generate",
 )
 
@@ -180,6 +181,8 @@ def load():
             "ghs_solver_unpack_best": (i32, [vp, vp]),
             "ghs_solver_contract": (i32, [vp, P(i32)]),
             "ghs_solver_finish": (i32, [vp, P(Result), P(RoundStats)]),
+            "ghs_solver_hook_local": (i32, [vp, vp, P(ctypes.c_uint64)]),
+            "ghs_solver_unpack_hook": (i32, [vp, vp]),
             "ghs_solver_reset": (i32, [vp]),
             "ghs_solver_destroy": (i32, [vp]),
             "ghs_rmat_temp_bytes": (sz, [u32, u32]),

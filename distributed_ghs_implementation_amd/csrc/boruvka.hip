@@ -726,7 +726,7 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
 GHS_STREAM_KERNEL_6 void k_win(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
                              const uint64_t *__restrict__ key, SegView in, const uint64_t *__restrict__ best,
                              uint32_t *__restrict__ par, uint8_t *__restrict__ in_mst,
-                             unsigned long long *__restrict__ acc /* [0] weight, [1] edges */,
+                             unsigned long long *__restrict__ acc /* [0] weight, [1] edges; nullptr: par only */,
                              const unsigned long long *__restrict__ guard_nact) {
   __shared__ uint32_t s_seg[2];
   __shared__ unsigned long long s_w[BLOCK / WAVE], s_c[BLOCK / WAVE];
@@ -767,13 +767,71 @@ GHS_STREAM_KERNEL_6 void k_win(const uint32_t *__restrict__ src, const uint32_t 
       const bool hb = wb & !(wa & (B[j] < A[j]));  // b hooks to a
       if (ha) par[A[j]] = B[j];
       if (hb) par[B[j]] = A[j];
-      if (ha | hb) {
+      if (acc && (ha | hb)) {
         in_mst[(uint32_t)K[j]] = 1;
         wsum += K[j] >> 32;
         cnt += 1;
       }
     }
     cur = nxt;
+  }
+#pragma unroll
+  for (int d = WAVE / 2; d > 0; d >>= 1) {
+    wsum += __shfl_xor(wsum, d);
+    cnt += __shfl_xor(cnt, d);
+  }
+  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+  if (lane == 0) {
+    s_w[wid] = wsum;
+    s_c[wid] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && acc) {
+    unsigned long long tw = 0, tc = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / WAVE; ++w) {
+      tw += s_w[w];
+      tc += s_c[w];
+    }
+    if (tc) {
+      atomicAdd(acc + 0, tw);
+      atomicAdd(acc + 1, tc);
+    }
+  }
+}
+
+// Multi-rank CONNECT of a level's first round, owner-computes: every winning edge lives on exactly
+// one rank, whose k_win (acc == nullptr) set par[c] = other for the fragments it holds the winner
+// of. The dense slot of active fragment c carries par[c] ^ c — 0 on every other rank, so a MAX
+// all-reduce yields the hook of every fragment on every rank (4 bytes per slot instead of
+// k_hook's ~5 random gathers per fragment: the canonical endpoints, their labels, best[other]).
+__global__ void k_pack_hook(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
+                            const uint32_t *__restrict__ par, int32_t *__restrict__ dense) {
+  const uint64_t nact = *d_nact;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nact; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = act ? act[i] : (uint32_t)i;
+    dense[i] = (int32_t)(par[c] ^ c);
+  }
+}
+
+// ... and after the all-reduce: par, in_mst (the fragment's best key holds the edge id) and the
+// totals on every rank, exactly what k_hook would have written.
+__global__ void k_unpack_hook(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
+                              const int32_t *__restrict__ dense, const uint64_t *__restrict__ best,
+                              uint32_t *__restrict__ par, uint8_t *__restrict__ in_mst,
+                              unsigned long long *__restrict__ acc /* [0] weight, [1] edges */) {
+  __shared__ unsigned long long s_w[BLOCK / WAVE], s_c[BLOCK / WAVE];
+  unsigned long long wsum = 0, cnt = 0;
+  const uint64_t nact = *d_nact;
+  for (uint64_t i = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; i < nact; i += (uint64_t)gridDim.x * BLOCK) {
+    const uint32_t x = (uint32_t)dense[i];
+    if (x == 0) continue;
+    const uint32_t c = act ? act[i] : (uint32_t)i;
+    const uint64_t k = best[c];
+    par[c] = c ^ x;
+    in_mst[(uint32_t)k] = 1;
+    wsum += k >> 32;
+    cnt += 1;
   }
 #pragma unroll
   for (int d = WAVE / 2; d > 0; d >>= 1) {
@@ -1791,6 +1849,7 @@ struct ghs_solver {
   hipEvent_t pass_ev[4] = {};   // around k_select [0,1] and k_filter [2,3] (from the host pool)
   bool filter_run = false;
   bool pending_exchange = false;  // multi-rank: a level's flags await the caller's OR all-reduce
+  bool hooked = false;            // multi-rank: this round's CONNECT came through the hook exchange
   unsigned open_G = 1;            // regions of the level's edges (between the two halves)
   uint64_t select_out = 0, filter_out = 0;
   bool detail = false;          // GHS_DETAIL=1: time every stage (adds ~5.7 us per event)
@@ -2212,7 +2271,10 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
         s->cfg.num_ranks <= 1 && s->level_round == 0 && (!s->arcs_known || s->cur_arcs < 8 * bound);
     if (edge_form && s->scan_pending) flush_scan(s);
     const bool dual = !edge_form && s->cfg.num_ranks <= 1 && s->level_round >= 1 && bound >= EDGE_HOOK_MIN_BOUND;
-    if (edge_form) {
+    if (s->hooked) {
+      // multi-rank: par / in_mst / totals already written by ghs_solver_unpack_hook
+      if (s->scan_pending) flush_scan(s);
+    } else if (edge_form) {
       const ArcBuf &I = s->buf[s->cur];
       SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
       k_win<<<s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->win_g) : s->win_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->best,
@@ -2560,6 +2622,41 @@ int ghs_solver_unpack_best(ghs_solver_t *s, const int64_t *d_dense) {
   return GHS_OK;
 }
 
+int ghs_solver_hook_local(ghs_solver_t *s, int32_t *d_dense, uint64_t *count) {
+  if (!s || !count) GHS_FAIL(GHS_E_ARG, "solver/count is NULL");
+  *count = 0;
+  if (s->phase != 1) GHS_FAIL(GHS_E_STATE, "hook_local must follow unpack_best");
+  // a level's first round with several ranks (its edges carry the current roots); labels and
+  // fragment ids must fit the int32 MAX exchange
+  if (s->cfg.num_ranks <= 1 || s->level_round != 0 || !s->nact || s->hooked || s->n > (1u << 31)) return GHS_OK;
+  if (!d_dense) GHS_FAIL(GHS_E_ARG, "dense is NULL");
+  const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
+  if (s->cur_arcs || !s->arcs_known) {
+    const ArcBuf &I = s->buf[s->cur];
+    SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
+    k_win<<<s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->win_g) : s->win_g, BLOCK, 0, s->stream>>>(
+        I.src, I.dst, I.key, in, s->best, s->par, s->in_mst, nullptr, nullptr);
+  }
+  k_pack_hook<<<grid_for(s->nact, 256, 16384), 256, 0, s->stream>>>(act, cur_act_count(s), s->par, d_dense);
+  GHS_HIP_CHECK(hipGetLastError());
+  *count = s->nact;
+  return GHS_OK;
+}
+
+int ghs_solver_unpack_hook(ghs_solver_t *s, const int32_t *d_dense) {
+  if (!s || (s->nact && !d_dense)) GHS_FAIL(GHS_E_ARG, "solver/dense is NULL");
+  if (s->phase != 1 || s->cfg.num_ranks <= 1 || s->level_round != 0 || s->hooked)
+    GHS_FAIL(GHS_E_STATE, "unpack_hook must follow hook_local");
+  if (s->nact) {
+    const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
+    k_unpack_hook<<<grid_for(s->nact, BLOCK, 16384), BLOCK, 0, s->stream>>>(act, cur_act_count(s), d_dense, s->best,
+                                                                            s->par, s->in_mst, s->cnt + C_WEIGHT);
+    GHS_HIP_CHECK(hipGetLastError());
+  }
+  s->hooked = true;
+  return GHS_OK;
+}
+
 int ghs_solver_contract(ghs_solver_t *s, int *done) {
   if (!s) GHS_FAIL(GHS_E_ARG, "solver is NULL");
   if (s->phase == 2) {
@@ -2571,6 +2668,7 @@ int ghs_solver_contract(ghs_solver_t *s, int *done) {
   const uint64_t live_in = s->level_round <= 1 ? s->cur_arcs : s->h_cnt[C_LIVE];
   const uint64_t nact_in = s->nact;
   if (int rc = enqueue_contract(s)) return rc;
+  s->hooked = false;
   const int nb = s->act_ident ? 0 : (s->act_cur ^ 1);
   GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, C_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
   GHS_HIP_CHECK(hipStreamSynchronize(s->stream));

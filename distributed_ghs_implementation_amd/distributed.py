@@ -11,6 +11,8 @@ per round:
     the identical active list of every rank;
   * per round: local min-edge over the rank's level edges -> dense best[] slots of the active
     fragments -> all_reduce(MIN) -> identical hook / pointer-jump / next-list on every rank;
+    in a level's first round the hook is owner-computes: each rank hooks the fragments whose
+    winning edge it holds and the int32 parent slots are combined with all_reduce(MAX);
   * result: in_mst is identical on every rank by construction (same inputs, same decisions);
     rank 0 writes the output (the reference gathered BRANCH edges to rank 0,
     ghs_implementation_mpi.py:760-779).
@@ -41,6 +43,7 @@ class HipStepper:
                                           _ptr(engine.in_mst), _stream(), ctypes.byref(h)))
         self.h = h
         self.dense = torch.empty(max(ed.n, 1), dtype=torch.int64, device=ed.device)
+        self.dense_hook = torch.empty(max(ed.n, 1), dtype=torch.int32, device=ed.device)
 
     def minedge(self):
         """Local min-edge of the round; None when a level was opened and its fragment flags must
@@ -64,6 +67,16 @@ class HipStepper:
 
     def unpack(self, dense):
         _native.check(self.L.ghs_solver_unpack_best(self.h, _ptr(dense)))
+
+    def hook_local(self):
+        """Owner-computes CONNECT of a level's first round: the int32 slots to all-reduce with
+        MAX (then unpack_hook), or None when the round hooks inside contract."""
+        c = ctypes.c_uint64(0)
+        _native.check(self.L.ghs_solver_hook_local(self.h, _ptr(self.dense_hook), ctypes.byref(c)))
+        return self.dense_hook[: int(c.value)] if c.value else None
+
+    def unpack_hook(self, dense):
+        _native.check(self.L.ghs_solver_unpack_hook(self.h, _ptr(dense)))
 
     def contract(self):
         d = ctypes.c_int(0)
@@ -94,7 +107,7 @@ class HipStepper:
 
 def run_rounds(stepper, allreduce_min, max_rounds=4096, allreduce_max=None):
     """The level loop shared by every backend: (level open: OR the fragment flags), min-edge,
-    all-reduce MIN, contract.
+    all-reduce MIN, (a level's first round: owner-computes hook, all-reduce MAX), contract.
 
     `allreduce_min(tensor)` / `allreduce_max(tensor)` reduce in place across ranks (identity for
     one rank; allreduce_max defaults to allreduce_min's backend with MAX). Returns the number of
@@ -110,6 +123,11 @@ def run_rounds(stepper, allreduce_min, max_rounds=4096, allreduce_max=None):
             dense = stepper.pack(count)
             allreduce_min(dense)
             stepper.unpack(dense)
+            hook = getattr(stepper, "hook_local", None)
+            hooks = hook() if hook is not None else None
+            if hooks is not None:  # each winning edge lives on one rank: MAX gathers the hooks
+                (allreduce_max or allreduce_min.max)(hooks)
+                stepper.unpack_hook(hooks)
         done = stepper.contract()
         rounds += 1
         if done:

@@ -165,6 +165,14 @@ int ghs_solver_minedge(ghs_solver_t *h, uint64_t *num_active);
 int ghs_solver_exchange_buffer(ghs_solver_t *h, uint8_t **d_flags, uint64_t *bytes);
 int ghs_solver_pack_best(ghs_solver_t *h, int64_t *d_dense);
 int ghs_solver_unpack_best(ghs_solver_t *h, const int64_t *d_dense);
+/* optional, after unpack_best (a level's first round, several ranks): owner-computes CONNECT.
+ * Each rank hooks the fragments whose winning edge it holds and fills *count int32 slots
+ * (par ^ fragment, 0 where another rank owns the winner); the caller all-reduces them with MAX
+ * and hands them to unpack_hook, after which contract skips its own hook. *count = 0: not
+ * applicable this round (contract hooks in fragment form, as without the call). Replaces the
+ * per-fragment gathers of the fragment-form hook with 4 bytes per active fragment on the wire. */
+int ghs_solver_hook_local(ghs_solver_t *h, int32_t *d_dense, uint64_t *count);
+int ghs_solver_unpack_hook(ghs_solver_t *h, const int32_t *d_dense);
 /* hook + jump + next list; *done = 1 when every level is complete */
 int ghs_solver_contract(ghs_solver_t *h, int *done);
 int ghs_solver_finish(ghs_solver_t *h, ghs_result_t *result, ghs_round_stats_t *stats);

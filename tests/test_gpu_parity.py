@@ -191,6 +191,16 @@ def test_partitioned_ranks_emulated_on_one_gpu(world, torch_cuda):
                 red = torch.minimum(red, d)
             for s in steppers:
                 s.unpack(red)
+            hooks = [s.hook_local() for s in steppers]  # owner-computes hook (a level's round 0)
+            assert len(set(h is None for h in hooks)) == 1
+            if hooks[0] is not None:
+                nz = sum((h != 0).to(torch.int64) for h in hooks)
+                assert int(nz.max().item()) <= 1  # one owner per winning edge
+                hmax = hooks[0].clone()
+                for h in hooks[1:]:
+                    hmax = torch.maximum(hmax, h)
+                for s in steppers:
+                    s.unpack_hook(hmax)
         dones = [s.contract() for s in steppers]
         assert len(set(dones)) == 1
         done = dones[0]
