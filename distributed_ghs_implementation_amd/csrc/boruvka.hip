@@ -434,7 +434,7 @@ GHS_STREAM_KERNEL_6 void k_minedge(const uint32_t *__restrict__ src, const uint3
                                  const uint64_t *__restrict__ key, SegView in, const uint32_t *__restrict__ lab,
                                  uint64_t *__restrict__ best, uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
                                  uint64_t *__restrict__ okey, uint64_t *__restrict__ oseg_start,
-                                 uint64_t *__restrict__ oseg_count) {
+                                 uint64_t *__restrict__ oseg_count, bool aside) {
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
   __shared__ uint32_t s_seg[2];
   __shared__ uint32_t s_hl[HOT_SLOTS];
@@ -496,6 +496,7 @@ GHS_STREAM_KERNEL_6 void k_minedge(const uint32_t *__restrict__ src, const uint3
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       if (smask & (1u << j)) hot_min(s_hl, s_hk, best, D[j], V[j]);
+    if (aside) {
     // a-side. Deferred run of the previous iteration (wave-uniform carry): a run that reaches
     // the wave's end is not flushed but carried, and merged into the next run of the same label
     // (min is associative, contiguity is not needed).
@@ -547,6 +548,7 @@ GHS_STREAM_KERNEL_6 void k_minedge(const uint32_t *__restrict__ src, const uint3
     }
     carry_l = __shfl(carry_l, WAVE - 1);
     carry_v = __shfl(carry_v, WAVE - 1);
+    }  // aside
 
     if (COMPACT) {
       uint32_t lane_excl, wave_before, wave_cnt, total;
@@ -577,6 +579,101 @@ GHS_STREAM_KERNEL_6 void k_minedge(const uint32_t *__restrict__ src, const uint3
   }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Level 0, round 0, a-side only (the b-side follows in k_minedge<IDENT> with aside = false).
+// At level 0 a label IS the vertex, and the canonical order holds each vertex's a-edges as ONE
+// run, so a run whose head and tail both lie inside a wave tile (their neighbours valid and
+// different) has a single writer: its minimum goes to best[] with a plain store — no LDS cache,
+// no read, no atomic. A run touching the tile's first or last entry, or a padding entry (a run
+// cut by a region end), may have a second piece elsewhere and takes the atomic path. Every store
+// here lands before the b-side's atomics (next launch). On a 16384^2 grid this removes about half
+// of round 0's global atomics (one a-run per vertex).
+// ------------------------------------------------------------------------------------------
+GHS_STREAM_KERNEL_6 void k_seed_runs(const uint32_t *__restrict__ src, const uint64_t *__restrict__ key, SegView in,
+                                     uint64_t *__restrict__ best) {
+  __shared__ uint32_t s_seg[2];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const uint64_t T = in.prefix[in.nseg];
+  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
+  const uint64_t vb = Q * blockIdx.x;
+  const uint64_t ve = (vb + Q < T) ? vb + Q : T;
+  if (threadIdx.x == 0) {
+    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
+    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
+  }
+  __syncthreads();
+  const uint32_t slo = s_seg[0], shi = s_seg[1];
+  uint64_t ph = tile_phys(in, slo, shi, vb + (uint64_t)threadIdx.x * 4, ve);
+  uint4 ca = *reinterpret_cast<const uint4 *>(src + ph);
+  ulonglong2 c01 = *reinterpret_cast<const ulonglong2 *>(key + ph), c23 = *reinterpret_cast<const ulonglong2 *>(key + ph + 2);
+  for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
+    const uint64_t v = v0 + (uint64_t)threadIdx.x * 4;
+    const bool in_range = v < ve;
+    uint32_t L[4] = {ca.x, ca.y, ca.z, ca.w};
+    const uint64_t K[4] = {c01.x, c01.y, c23.x, c23.y};
+    const uint64_t pn = tile_phys(in, slo, shi, v + ARCS_PER_BLOCK, ve);
+    ca = *reinterpret_cast<const uint4 *>(src + pn);
+    c01 = *reinterpret_cast<const ulonglong2 *>(key + pn);
+    c23 = *reinterpret_cast<const ulonglong2 *>(key + pn + 2);
+    uint64_t X[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!in_range) L[j] = LABEL_NONE;
+      X[j] = (L[j] != LABEL_NONE) ? K[j] : KEY_NONE;
+    }
+    const uint32_t prevL3 = __shfl_up(L[3], 1);
+    const uint32_t nextL0 = __shfl_down(L[0], 1);
+    bool H[4], TH[4], TT[4];
+    H[0] = (lane == 0) || (L[0] != prevL3);
+    TH[0] = (lane != 0) && (L[0] != prevL3) && (prevL3 != LABEL_NONE);
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      H[j] = L[j] != L[j - 1];
+      TH[j] = H[j] && (L[j - 1] != LABEL_NONE);
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) TT[j] = (L[j + 1] != L[j]) && (L[j + 1] != LABEL_NONE);
+    TT[3] = (lane != WAVE - 1) && (nextL0 != L[3]) && (nextL0 != LABEL_NONE);
+    // segmented min over runs (heads reset), carrying "the run's head is untrusted"
+    uint64_t x = KEY_NONE;
+    int f = 0, uu = 1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x = H[j] ? X[j] : umin64(x, X[j]);
+      uu = H[j] ? (TH[j] ? 0 : 1) : uu;
+      f |= H[j] ? 1 : 0;
+    }
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+      const uint64_t xo = __shfl_up(x, d);
+      const int fo = __shfl_up(f, d);
+      const int uo = __shfl_up(uu, d);
+      if (lane >= d && !f) {
+        x = umin64(x, xo);
+        uu = uo;
+      }
+      if (lane >= d) f |= fo;
+    }
+    uint64_t run = __shfl_up(x, 1);
+    int ru = __shfl_up(uu, 1);
+    if (lane == 0) {
+      run = KEY_NONE;
+      ru = 1;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      run = H[j] ? X[j] : umin64(run, X[j]);
+      ru = H[j] ? (TH[j] ? 0 : 1) : ru;
+      // a run continuing into the next lane is finished there (the scan carries its minimum)
+      const bool tail = (j < 3) ? (L[j + 1] != L[j]) : (lane == WAVE - 1 || nextL0 != L[3]);
+      if (tail && run != KEY_NONE && L[j] != LABEL_NONE) {
+        if (!ru && TT[j]) best[L[j]] = run;   // whole run inside the tile: the only writer
+        else flush_min(best, L[j], run);      // a piece of a run: atomic
+      }
+    }
+  }
+}
 
 // exclusive scan of count[0..n) into prefix[0..n]; one block of 1024 threads
 __global__ __launch_bounds__(1024) void k_scan_counts(const uint64_t *__restrict__ count, uint32_t n,
@@ -1869,6 +1966,7 @@ struct ghs_solver {
   uint32_t lookahead = LOOKAHEAD;  // rounds in flight ahead of the termination check (GHS_LOOKAHEAD)
   std::chrono::steady_clock::time_point t0;
   char *ws_base = nullptr;      // the caller's workspace (carved by workspace_layout)
+  bool seed_runs = true;        // level 0 round 0: a-side runs by k_seed_runs (GHS_SEED_RUNS=0: off)
 };
 
 static std::mutex g_mutex;  // the one-shot entry points are serialised per process
@@ -2239,13 +2337,18 @@ static int enqueue_minedge(ghs_solver *s) {
   ArcBuf &O = s->buf[s->cur ^ 1];
   SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
   if (s->level_round == 0) {
-    if (s->cur_arcs || !s->arcs_known)
-      k_minedge<true, false><<<s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->ident_g) : s->ident_g, BLOCK, 0, s->stream>>>(
-          I.src, I.dst, I.key, in, s->lab, s->best, nullptr, nullptr, nullptr, nullptr, nullptr);
+    if (s->cur_arcs || !s->arcs_known) {
+      const unsigned g = s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->ident_g) : s->ident_g;
+      // level 0 (labels are the vertices): a-side runs seeded first, mostly by plain stores
+      const bool seed = s->level == 0 && s->seed_runs;
+      if (seed) k_seed_runs<<<g, BLOCK, 0, s->stream>>>(I.src, I.key, in, s->best);
+      k_minedge<true, false><<<g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, nullptr, nullptr,
+                                                         nullptr, nullptr, nullptr, !seed);
+    }
   } else {
     // fixed grid: every one of the seg_g blocks writes its region's count
     k_minedge<false, true><<<s->cmp_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, O.src, O.dst,
-                                                          O.key, O.seg_start, O.seg_count);
+                                                          O.key, O.seg_start, O.seg_count, true);
     // the regions' prefix scan is left to the round's hook kernel (or a scan launch before the
     // next consumer): s->scan_pending
     s->scan_pending = true;
@@ -2529,6 +2632,7 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
     }
   };
   grid_env("GHS_MINEDGE_G", &s->cmp_g);
+  if (const char *sr = getenv("GHS_SEED_RUNS")) s->seed_runs = sr[0] != '0';
   grid_env("GHS_IDENT_G", &s->ident_g);
   grid_env("GHS_WIN_G", &s->win_g);
   grid_env("GHS_LP_G", &s->lp_g);
@@ -2738,7 +2842,7 @@ int ghs_solver_reset(ghs_solver_t *s) {
   t.n = s->n; t.m = s->m; t.e_lo = s->e_lo; t.e_hi = s->e_hi;
   t.eu = s->eu; t.ev = s->ev; t.ew = s->ew;
   t.in_mst = s->in_mst; t.stream = s->stream; t.cfg = s->cfg;
-  t.debug = s->debug; t.lookahead = s->lookahead;
+  t.debug = s->debug; t.lookahead = s->lookahead; t.seed_runs = s->seed_runs;
   { const char *det = getenv("GHS_DETAIL"); t.detail = det && det[0] == '1'; }
   { const char *tr = getenv("GHS_TIME_ROUNDS"); t.time_rounds = tr && tr[0] == '1'; }
   t.seg_g = s->seg_g; t.cmp_g = s->cmp_g; t.ident_g = s->ident_g; t.win_g = s->win_g; t.lp_g = s->lp_g;
