@@ -21,7 +21,8 @@ timed steps); all three are listed under "kernels". `traffic` comes from the
 committed PMC profile (profiles/**/<workload>_pmc.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes,
 gfx950-corrected, tools/gpu/pmc_traffic.sh) when one exists for this workload, else null.
 `cpu_baseline` = the oracle's C Kruskal (kind "port", 1 thread) on a bounded sample (R-MAT of a
-smaller scale, same generator), rank 0 at N=1 only.
+smaller scale, same generator), rank 0 at N=1 only; `cpu_baseline_networkx` = NetworkX Kruskal
+(the reference's verifier) on an R-MAT s16 sample, beside it.
 """
 import argparse
 import glob
@@ -49,6 +50,7 @@ def parse():
     ap.add_argument("--grid-k", type=int, default=16384)
     ap.add_argument("--cpu-scale", type=int, default=21, help="R-MAT scale of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--nx-scale", type=int, default=16, help="R-MAT scale of the NetworkX baseline sample")
     ap.add_argument("--verify", action="store_true", help="check the result against the oracle (slow at s24)")
     ap.add_argument("--stats", action="store_true", help="print per-round stats to stderr")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -135,6 +137,35 @@ def cpu_baseline(scale, edgefactor):
                       f"{g.m} canonical edges) through oracle/kruskal.c canonical Kruskal, 1 thread, "
                       f"{dt:.2f} s; host os.cpu_count()={os.cpu_count()}",
             "seconds": dt}
+
+
+def networkx_baseline(scale, edgefactor):
+    """NetworkX Kruskal (the reference's own verifier, ghs_implementation.py:746 /
+    check_mst.py:9; 1 core under the GIL) on R-MAT(scale) from the same generator. Times the
+    nx.minimum_spanning_tree call (graph built beforehand, as the GPU timing excludes generation)
+    and checks its weight against the oracle's. None when NetworkX is not importable here."""
+    try:
+        import networkx as nx
+    except ImportError:
+        return None
+    from distributed_ghs_implementation_amd.device import generate_rmat
+    from oracle import oracle
+    e = generate_rmat(scale, edgefactor, seed=1, wseed=2)
+    g = e.to_host()
+    del e
+    G = nx.Graph()
+    G.add_nodes_from(range(g.n))
+    G.add_weighted_edges_from(zip(g.u.tolist(), g.v.tolist(), g.w.tolist()))
+    t0 = time.perf_counter()
+    T = nx.minimum_spanning_tree(G, weight="weight")
+    dt = time.perf_counter() - t0
+    tw = sum(int(d["weight"]) for _, _, d in T.edges(data=True))
+    _, ref_tw, _ = oracle.kruskal_c(g.n, g.u, g.v, g.w)
+    return {"value": g.m / dt, "unit": "edges/s", "cores": 1, "kind": "networkx",
+            "sample": f"R-MAT scale {scale} edgefactor {edgefactor} ({g.m} canonical edges) through "
+                      f"nx.minimum_spanning_tree (networkx {nx.__version__}), graph prebuilt, {dt:.2f} s; "
+                      f"weight {'==' if tw == ref_tw else '!='} oracle",
+            "seconds": dt, "weight_matches_oracle": tw == ref_tw}
 
 
 def main():
@@ -255,14 +286,15 @@ def main():
                            "ms_minedge": round(s["ms_minedge"], 4), "ms_hook": round(s["ms_hook"], 4),
                            "ms_jump": round(s["ms_jump"], 4), "ms_next": round(s["ms_active"], 4)} for s in s0],
         }
-        cpu = None
+        cpu = cpu_nx = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.cpu_scale, args.edgefactor)
+            cpu_nx = networkx_baseline(args.nx_scale, args.edgefactor)
         line = {"metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
                 "data": "synthetic (generated on GPU)", "config": cfg, "roofline": roofline,
-                "cpu_baseline": cpu, "kernels": kernels, "mst": {"total_weight": results[-1][0], "edges": results[-1][1]},
+                "cpu_baseline": cpu, "cpu_baseline_networkx": cpu_nx, "kernels": kernels, "mst": {"total_weight": results[-1][0], "edges": results[-1][1]},
                 "breakdown": breakdown}
         print(json.dumps(line), flush=True)
     if world > 1:

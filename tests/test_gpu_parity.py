@@ -156,15 +156,18 @@ def test_stepwise_solver_equals_monolithic(torch_cuda):
     assert rc.total_weight == ra.total_weight and rc.rounds == ra.rounds
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_partitioned_ranks_emulated_on_one_gpu(world, torch_cuda):
+@pytest.mark.parametrize("world,graph", [(2, "rmat"), (3, "rmat"), (8, "rmat"), (8, "grid"), (5, "grid-gradient")])
+def test_partitioned_ranks_emulated_on_one_gpu(world, graph, torch_cuda):
     """`world` edge-range engines on one GPU, all-reduce emulated with torch.minimum: the
     multi-GPU decomposition gives the single-GPU answer."""
     import torch
-    from distributed_ghs_implementation_amd.device import DeviceMST, edge_range, generate_rmat
+    from distributed_ghs_implementation_amd.device import DeviceMST, edge_range, generate_grid, generate_rmat
     from distributed_ghs_implementation_amd.distributed import HipStepper
     from distributed_ghs_implementation_amd import _native
-    e = generate_rmat(15, 16, seed=3, wseed=4)
+    if graph == "rmat":
+        e = generate_rmat(15, 16, seed=3, wseed=4)
+    else:
+        e = generate_grid(257, 1 if graph == "grid-gradient" else 0)
     ref = DeviceMST(e)
     ref.run()
     cfg = _native.make_config(num_ranks=world)
