@@ -3,11 +3,12 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scale S] [--workload rmat|grid]
 
 A step = one full MST of the device-resident canonical edge list (BASELINE.md "Definitions"):
-symmetric arc build (radix sort by source) + all Boruvka rounds -> in_mst flags + total weight.
+validation, the weight-level plan, every level's pass and all Boruvka rounds -> in_mst flags +
+total weight.
 Inputs are generated on the GPU before the timed region (synthetic R-MAT, Graph500 parameters,
 unique hashed weights — no dataset download). N=1: R-MAT scale 24 (BASELINE config 3).
 N>1 (torch.distributed.run, one rank per GPU, RCCL all-reduce MIN per round): every rank holds
-the replicated canonical list and scans the arcs of its source-vertex range; scale
+the replicated canonical list and streams its contiguous canonical-edge range; scale
 min(26, 24 + log2 N) (config 4: s26 on 8 GPUs).
 
 Rank 0 prints ONE JSON line. `roofline` is for the dominant kernel of the step (largest
@@ -200,7 +201,7 @@ def main():
         cfg = {"workload": tag, "grid_k": k}
     torch.cuda.synchronize()
     n, m = edges.n, edges.m
-    cfg.update({"n": n, "m": m, "partition": f"source-vertex ranges x{world}", "parallelism": f"arcs{world}"})
+    cfg.update({"n": n, "m": m, "partition": f"canonical edge ranges x{world}", "parallelism": f"edges{world}"})
 
     if world > 1:
         eng = DistributedMST(edges, rank, world)
