@@ -236,7 +236,7 @@ def main():
         raise RuntimeError("non-deterministic MST across steps")
     if world > 1 and args.verify_ranks:
         # every rank must hold the same MSF: (weight, edges, checksum of the chosen eids)
-        flags = eng.engine.in_mst[:m]
+        flags = eng.gather_in_mst()
         chk = int((torch.nonzero(flags).flatten().to(torch.int64) % 1000003).sum().item())
         mine = torch.tensor([results[-1][0], results[-1][1], chk], dtype=torch.int64)
         if args.backend == "nccl":

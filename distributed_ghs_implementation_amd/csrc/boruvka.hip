@@ -80,6 +80,7 @@ constexpr int FIND_LAB_MAX_HOPS = 256;
 // Chosen on the device from the exact counts; the host enqueues both only while its bound on the
 // active fragments is at least EDGE_HOOK_MIN_BOUND.
 constexpr uint64_t EDGE_HOOK_RATIO = 4;
+constexpr uint32_t HOOK_G = 2048;  // grid cap of the kernels ending in per-block total atomics
 constexpr uint64_t EDGE_HOOK_MIN_BOUND = 1u << 20;
 constexpr uint32_t JUMP_MAX_STEPS = 1u << 26;
 
@@ -864,8 +865,8 @@ GHS_STREAM_KERNEL_6 void k_win(const uint32_t *__restrict__ src, const uint32_t 
       const bool hb = wb & !(wa & (B[j] < A[j]));  // b hooks to a
       if (ha) par[A[j]] = B[j];
       if (hb) par[B[j]] = A[j];
-      if (acc && (ha | hb)) {
-        in_mst[(uint32_t)K[j]] = 1;
+      if (ha | hb) {
+        in_mst[(uint32_t)K[j]] = 1;  // with acc == nullptr: the owner rank's mark (see k_unpack_hook)
         wsum += K[j] >> 32;
         cnt += 1;
       }
@@ -911,12 +912,14 @@ __global__ void k_pack_hook(const uint32_t *__restrict__ act, const unsigned lon
   }
 }
 
-// ... and after the all-reduce: par, in_mst (the fragment's best key holds the edge id) and the
-// totals on every rank, exactly what k_hook would have written.
+// ... and after the all-reduce: par and the totals on every rank, as k_hook would have written
+// them. in_mst is NOT written here: the owner rank's k_win marked the edge (a random byte store
+// per hook on every rank cost ~0.5 ms per level at s26 / 8 ranks), so after a multi-rank solve
+// each rank holds the flags of the hooks it owned and the OR over the ranks is the MSF
+// (DistributedMST.gather_in_mst).
 __global__ void k_unpack_hook(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
                               const int32_t *__restrict__ dense, const uint64_t *__restrict__ best,
-                              uint32_t *__restrict__ par, uint8_t *__restrict__ in_mst,
-                              unsigned long long *__restrict__ acc /* [0] weight, [1] edges */) {
+                              uint32_t *__restrict__ par, unsigned long long *__restrict__ acc /* [0] weight, [1] edges */) {
   __shared__ unsigned long long s_w[BLOCK / WAVE], s_c[BLOCK / WAVE];
   unsigned long long wsum = 0, cnt = 0;
   const uint64_t nact = *d_nact;
@@ -926,7 +929,6 @@ __global__ void k_unpack_hook(const uint32_t *__restrict__ act, const unsigned l
     const uint32_t c = act ? act[i] : (uint32_t)i;
     const uint64_t k = best[c];
     par[c] = c ^ x;
-    in_mst[(uint32_t)k] = 1;
     wsum += k >> 32;
     cnt += 1;
   }
@@ -2367,6 +2369,9 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
   const int nb = s->act_ident ? 0 : (s->act_cur ^ 1);
   if (bound) {
     const unsigned g = grid_for(bound, BLOCK, 16384);  // grid-stride beyond 4M fragments
+    // the hook kernels end with one pair of same-address atomics per block (the totals), which
+    // serialise at ~12 ns each: at most HOOK_G blocks (16384 blocks cost ~0.4 ms in atomics)
+    const unsigned gh = grid_for(bound, BLOCK, HOOK_G);
     // CONNECT: edge form while fragments are many and small (a level's first round: its edges
     // carry the current roots), fragment form otherwise (and always with several ranks: a
     // fragment's best edge may live on another rank)
@@ -2390,12 +2395,12 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
       k_win<<<s->win_g, BLOCK, 0, s->stream>>>(O.src, O.dst, O.key, in, s->best, s->par, s->in_mst, s->cnt + C_WEIGHT,
                                                d_nact);
       GHS_HIP_CHECK(hipGetLastError());
-      k_hook<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
+      k_hook<<<gh, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
                                          s->cnt + C_WEIGHT, s->cnt + C_ERR, nullptr, 0, nullptr, nullptr, false,
                                          s->cnt + C_LIVE);
     } else {
       const ArcBuf *sb = s->scan_pending ? s->scan_buf : nullptr;
-      k_hook<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
+      k_hook<<<gh, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
                                          s->cnt + C_WEIGHT, s->cnt + C_ERR, sb ? sb->seg_count : nullptr, s->cmp_g,
                                          sb ? sb->seg_prefix : nullptr, s->cnt + C_LIVE, s->level_round == 0, nullptr);
       s->scan_pending = false;
@@ -2753,8 +2758,8 @@ int ghs_solver_unpack_hook(ghs_solver_t *s, const int32_t *d_dense) {
     GHS_FAIL(GHS_E_STATE, "unpack_hook must follow hook_local");
   if (s->nact) {
     const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
-    k_unpack_hook<<<grid_for(s->nact, BLOCK, 16384), BLOCK, 0, s->stream>>>(act, cur_act_count(s), d_dense, s->best,
-                                                                            s->par, s->in_mst, s->cnt + C_WEIGHT);
+    k_unpack_hook<<<grid_for(s->nact, BLOCK, HOOK_G), BLOCK, 0, s->stream>>>(act, cur_act_count(s), d_dense, s->best,
+                                                                            s->par, s->cnt + C_WEIGHT);
     GHS_HIP_CHECK(hipGetLastError());
   }
   s->hooked = true;

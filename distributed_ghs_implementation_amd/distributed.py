@@ -13,8 +13,10 @@ per round:
     fragments -> all_reduce(MIN) -> identical hook / pointer-jump / next-list on every rank;
     in a level's first round the hook is owner-computes: each rank hooks the fragments whose
     winning edge it holds and the int32 parent slots are combined with all_reduce(MAX);
-  * result: in_mst is identical on every rank by construction (same inputs, same decisions);
-    rank 0 writes the output (the reference gathered BRANCH edges to rank 0,
+  * result: the totals are identical on every rank by construction (same inputs, same
+    decisions); an owner-computed hook marks its edge's in_mst flag on the owning rank only, so
+    the flags are combined on demand (`gather_in_mst`: uint8 MAX all-reduce, outside the solve)
+    and rank 0 writes the output (the reference gathered BRANCH edges to rank 0,
     ghs_implementation_mpi.py:760-779).
 
 The round loop (`run_rounds`) is written against a small stepper interface so that the same
@@ -193,5 +195,13 @@ class DistributedMST:
             self.stepper.close()
             self.stepper = None
 
+    def gather_in_mst(self):
+        """OR the ranks' MSF flags (collective: every rank calls it). Returns the device flags."""
+        flags = self.engine.in_mst[: self.edges.m]
+        if dist.is_initialized() and dist.get_world_size(self.group) > 1:
+            dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=self.group)
+        return flags
+
     def in_mst_host(self):
-        return self.engine.in_mst_host()
+        """The MSF flags as a host bool array (collective, see gather_in_mst)."""
+        return self.gather_in_mst().cpu().numpy().astype(bool)

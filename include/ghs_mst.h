@@ -170,7 +170,11 @@ int ghs_solver_unpack_best(ghs_solver_t *h, const int64_t *d_dense);
  * (par ^ fragment, 0 where another rank owns the winner); the caller all-reduces them with MAX
  * and hands them to unpack_hook, after which contract skips its own hook. *count = 0: not
  * applicable this round (contract hooks in fragment form, as without the call). Replaces the
- * per-fragment gathers of the fragment-form hook with 4 bytes per active fragment on the wire. */
+ * per-fragment gathers of the fragment-form hook with 4 bytes per active fragment on the wire.
+ * The MSF flag of such a hook is set only on the rank that owns the edge: after a solve that
+ * used hook_local, d_in_mst of each rank holds a subset and the OR over the ranks (a uint8 MAX
+ * all-reduce of the m flags, or a gather of each rank's [e_lo, e_hi) slice plus the rest) is
+ * the MSF; the totals of ghs_solver_finish are complete on every rank. */
 int ghs_solver_hook_local(ghs_solver_t *h, int32_t *d_dense, uint64_t *count);
 int ghs_solver_unpack_hook(ghs_solver_t *h, const int32_t *d_dense);
 /* hook + jump + next list; *done = 1 when every level is complete */

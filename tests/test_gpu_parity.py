@@ -218,10 +218,18 @@ def test_partitioned_ranks_emulated_on_one_gpu(world, graph, torch_cuda):
         dones = [s.contract() for s in steppers]
         assert len(set(dones)) == 1
         done = dones[0]
-    for s, x in zip(steppers, engines):
-        s.finish()
+    totals = []
+    for s in steppers:
+        res, _ = s.finish()
+        totals.append((res.total_weight, res.num_mst_edges))
         s.close()
-        assert np.array_equal(x.in_mst_host(), ref.in_mst_host())
+    # the MSF flags are the OR over the ranks (an owner-computed hook marks its owner's copy)
+    flags = engines[0].in_mst.clone()
+    for x in engines[1:]:
+        flags = torch.maximum(flags, x.in_mst)
+    assert np.array_equal(flags[: e.m].cpu().numpy().astype(bool), ref.in_mst_host())
+    rr, _ = ref.run()
+    assert set(totals) == {(rr.total_weight, rr.num_mst_edges)}
 
 
 def test_build_arcs_utility(torch_cuda):
