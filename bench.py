@@ -22,8 +22,9 @@ timed steps); all three are listed under "kernels". `traffic` comes from the
 committed PMC profile (profiles/**/<workload>_pmc.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes,
 gfx950-corrected, tools/gpu/pmc_traffic.sh) when one exists for this workload, else null.
 `cpu_baseline` = the oracle's C Kruskal (kind "port", 1 thread) on a bounded sample (R-MAT of a
-smaller scale, same generator), rank 0 at N=1 only; `cpu_baseline_networkx` = NetworkX Kruskal
-(the reference's verifier) on an R-MAT s16 sample, beside it.
+smaller scale, same generator), rank 0 at N=1 only; `cpu_baseline_parallel` = the all-cores
+OpenMP Borůvka (oracle/boruvka_omp.c, OMP_NUM_THREADS threads) on an R-MAT s23 sample;
+`cpu_baseline_networkx` = NetworkX Kruskal (the reference's verifier) on an R-MAT s16 sample.
 """
 import argparse
 import glob
@@ -51,6 +52,7 @@ def parse():
     ap.add_argument("--grid-k", type=int, default=16384)
     ap.add_argument("--cpu-scale", type=int, default=21, help="R-MAT scale of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--omp-scale", type=int, default=23, help="R-MAT scale of the OpenMP Boruvka baseline sample")
     ap.add_argument("--nx-scale", type=int, default=16, help="R-MAT scale of the NetworkX baseline sample")
     ap.add_argument("--verify", action="store_true", help="check the result against the oracle (slow at s24)")
     ap.add_argument("--stats", action="store_true", help="print per-round stats to stderr")
@@ -138,6 +140,32 @@ def cpu_baseline(scale, edgefactor):
                       f"{g.m} canonical edges) through oracle/kruskal.c canonical Kruskal, 1 thread, "
                       f"{dt:.2f} s; host os.cpu_count()={os.cpu_count()}",
             "seconds": dt}
+
+
+def omp_baseline(scale, edgefactor, threads=None):
+    """The all-cores CPU baseline: oracle/boruvka_omp.c, an OpenMP Borůvka
+    over the canonical list (same canonical MSF, parity in tests/test_oracle.py), on R-MAT(scale)
+    from the same generator. threads: OMP_NUM_THREADS (16 on the GPU box), else the process's
+    CPUs capped at 16. Its weight/edge count is checked against one GPU solve of the same graph."""
+    from distributed_ghs_implementation_amd.device import DeviceMST, generate_rmat
+    from oracle import oracle
+    if threads is None:
+        threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, len(os.sched_getaffinity(0)))
+    e = generate_rmat(scale, edgefactor, seed=1, wseed=2)
+    gres, _ = DeviceMST(e).run()
+    g = e.to_host()
+    del e
+    oracle.boruvka_omp_c(min(g.n, 1024), g.u[:0], g.v[:0], g.w[:0], threads=threads)  # load outside the timing
+    t0 = time.perf_counter()
+    _, tw, k, rounds = oracle.boruvka_omp_c(g.n, g.u, g.v, g.w, threads=threads)
+    dt = time.perf_counter() - t0
+    ok = (tw, k) == (gres.total_weight, gres.num_mst_edges)
+    return {"value": g.m / dt, "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": f"R-MAT scale {scale} edgefactor {edgefactor} ({g.m} canonical edges) through "
+                      f"oracle/boruvka_omp.c OpenMP Boruvka, {threads} threads, {rounds} rounds, {dt:.2f} s; "
+                      f"weight/edges {'==' if ok else '!='} the GPU solve of the same graph; "
+                      f"host os.cpu_count()={os.cpu_count()}",
+            "seconds": dt, "matches_gpu": ok}
 
 
 def networkx_baseline(scale, edgefactor):
@@ -287,15 +315,16 @@ def main():
                            "ms_minedge": round(s["ms_minedge"], 4), "ms_hook": round(s["ms_hook"], 4),
                            "ms_jump": round(s["ms_jump"], 4), "ms_next": round(s["ms_active"], 4)} for s in s0],
         }
-        cpu = cpu_nx = None
+        cpu = cpu_nx = cpu_omp = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.cpu_scale, args.edgefactor)
+            cpu_omp = omp_baseline(args.omp_scale, args.edgefactor)
             cpu_nx = networkx_baseline(args.nx_scale, args.edgefactor)
         line = {"metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
                 "data": "synthetic (generated on GPU)", "config": cfg, "roofline": roofline,
-                "cpu_baseline": cpu, "cpu_baseline_networkx": cpu_nx, "kernels": kernels, "mst": {"total_weight": results[-1][0], "edges": results[-1][1]},
+                "cpu_baseline": cpu, "cpu_baseline_parallel": cpu_omp, "cpu_baseline_networkx": cpu_nx, "kernels": kernels, "mst": {"total_weight": results[-1][0], "edges": results[-1][1]},
                 "breakdown": breakdown}
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -5,6 +5,8 @@
                     wins on duplicate pairs, output sorted by (min, max)).
 * `kruskal_c` / `canonicalize_c`  the same in C (oracle/kruskal.c via ctypes), for the large
                     parity cases and the bench's cpu_baseline (kind "port").
+* `boruvka_omp_c`   OpenMP Borůvka on all given cores (oracle/boruvka_omp.c): the same canonical
+                    MSF (unique keys), the bench's all-cores CPU baseline.
 
 Reference anchors: the MST the reference verifies against is NetworkX Kruskal
 (ghs_implementation.py:746, create_graph_files.py:141, check_mst.py:9); the raw-edge semantics
@@ -38,6 +40,9 @@ def lib():
         L.oracle_canonicalize.restype = ctypes.c_int
         L.oracle_check_canonical.argtypes = [ctypes.c_uint32, ctypes.c_uint64, u32p, u32p]
         L.oracle_check_canonical.restype = ctypes.c_int
+        L.oracle_boruvka_omp.argtypes = [ctypes.c_uint32, ctypes.c_uint64, u32p, u32p, u32p, ctypes.c_int,
+                                         u8p, u64p, u64p, u32p]
+        L.oracle_boruvka_omp.restype = ctypes.c_int
         _LIB = L
     return _LIB
 
@@ -115,3 +120,22 @@ def kruskal_c(n, u, v, w):
     if rc != 0:
         raise ValueError(f"oracle_kruskal failed rc={rc}")
     return in_mst[:m], tw.value, k.value
+
+
+def boruvka_omp_c(n, u, v, w, threads=0):
+    """OpenMP Borůvka on canonical arrays -> (in_mst uint8[m], total_weight, num_edges, rounds).
+    threads <= 0: the OpenMP default (OMP_NUM_THREADS)."""
+    u = np.ascontiguousarray(u, dtype=np.uint32)
+    v = np.ascontiguousarray(v, dtype=np.uint32)
+    w = np.ascontiguousarray(w, dtype=np.uint32)
+    m = len(u)
+    in_mst = np.zeros(max(m, 1), np.uint8)
+    tw = ctypes.c_uint64(0)
+    k = ctypes.c_uint64(0)
+    r = ctypes.c_uint32(0)
+    rc = lib().oracle_boruvka_omp(n, m, _p(u, ctypes.c_uint32), _p(v, ctypes.c_uint32), _p(w, ctypes.c_uint32),
+                                  int(threads), _p(in_mst, ctypes.c_uint8), ctypes.byref(tw), ctypes.byref(k),
+                                  ctypes.byref(r))
+    if rc != 0:
+        raise ValueError(f"oracle_boruvka_omp failed rc={rc}")
+    return in_mst[:m], tw.value, k.value, r.value
