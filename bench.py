@@ -21,10 +21,10 @@ instrumented step after them (GHS_TIME_ROUNDS=1; per-round events would add idle
 timed steps); all three are listed under "kernels". `traffic` comes from the
 committed PMC profile (profiles/**/<workload>_pmc.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes,
 gfx950-corrected, tools/gpu/pmc_traffic.sh) when one exists for this workload, else null.
-`cpu_baseline` = the oracle's C Kruskal (kind "port", 1 thread) on a bounded sample (R-MAT of a
-smaller scale, same generator), rank 0 at N=1 only; `cpu_baseline_parallel` = the all-cores
-OpenMP Borůvka (oracle/boruvka_omp.c, OMP_NUM_THREADS threads) on an R-MAT s23 sample;
-`cpu_baseline_networkx` = NetworkX Kruskal (the reference's verifier) on an R-MAT s16 sample.
+CPU baselines on bounded samples (same generator, smaller scale), rank 0 at N=1 only:
+`cpu_baseline` = the all-cores OpenMP Borůvka (oracle/boruvka_omp.c, kind "port",
+OMP_NUM_THREADS threads) on R-MAT s23; `cpu_baseline_serial` = the oracle's C Kruskal (1 thread)
+on R-MAT s21; `cpu_baseline_networkx` = NetworkX Kruskal (the reference's verifier) on R-MAT s16.
 """
 import argparse
 import glob
@@ -324,7 +324,7 @@ def main():
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
                 "data": "synthetic (generated on GPU)", "config": cfg, "roofline": roofline,
-                "cpu_baseline": cpu, "cpu_baseline_parallel": cpu_omp, "cpu_baseline_networkx": cpu_nx, "kernels": kernels, "mst": {"total_weight": results[-1][0], "edges": results[-1][1]},
+                "cpu_baseline": cpu_omp, "cpu_baseline_serial": cpu, "cpu_baseline_networkx": cpu_nx, "kernels": kernels, "mst": {"total_weight": results[-1][0], "edges": results[-1][1]},
                 "breakdown": breakdown}
         print(json.dumps(line), flush=True)
     if world > 1:
