@@ -100,6 +100,11 @@ __device__ __forceinline__ void flush_min(uint64_t *__restrict__ best, uint32_t 
 // block instead of one per run — same-address global operations serialise at the memory side
 // (~12 ns each, MI355X_MICROARCH.md "fanin") and atomics drop the line from L2, so every later
 // plain read of that slot misses too.
+// k_filter: issue the random b-probe only for edges whose a-end is in the giant (1), or for
+// every heavy edge beside the a-probes (0)
+#ifndef GHS_FILTER_GATED
+#define GHS_FILTER_GATED 1
+#endif
 #ifndef GHS_HOT_BITS
 #define GHS_HOT_BITS 8
 #endif
@@ -1384,23 +1389,47 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
     const uint4 q0 = bits4[A0];
     const uint4 q3 = bits4[A3];
     uint32_t gbw[4];
+#if !GHS_FILTER_GATED
 #pragma unroll
     for (int j = 0; j < 4; ++j) gbw[j] = bits32[out[j] ? (b[j] >> 5) : 0u];
+#endif
+    uint32_t ga[4], gb[4];
+#if GHS_FILTER_GATED
+    // gated b-probes: only an edge whose a-end is in the giant can be dropped, so the random
+    // b-probe (one L2 request) is issued for those edges alone, after the a-probes landed (the
+    // sequential a-probes are near-always L2 hits); the next tile's stream loads follow them
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t blk = a[j] >> 7, wsel = (a[j] >> 5) & 3;
+      const uint4 q = (blk == A0) ? q0 : q3;
+      const bool odd = wsel & 1;
+      const uint32_t lo = odd ? q.y : q.x, hi = odd ? q.w : q.z;
+      const uint32_t word = (wsel & 2) ? hi : lo;
+      ga[j] = ((blk == A0) | (blk == A3)) ? (word >> (a[j] & 31)) & 1u : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gbw[j] = bits32[(out[j] & (ga[j] != 0u)) ? (b[j] >> 5) : 0u];
+#endif
     // next tile (out-of-range offsets read 0)
     const uint32_t noff = (uint32_t)(v0 + ARCS_PER_BLOCK - vb) * 4u + lane_off;
     ca = ld_b128(ru, noff);
     cb = ld_b128(rv, noff);
     cw = ld_b128(rw, noff);
-    uint32_t ga[4], gb[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
+#if !GHS_FILTER_GATED
       const uint32_t blk = a[j] >> 7, wsel = (a[j] >> 5) & 3;
       const uint4 q = (blk == A0) ? q0 : q3;
       const bool odd = wsel & 1;  // two-level select (an == chain becomes a branch tree)
       const uint32_t lo = odd ? q.y : q.x, hi = odd ? q.w : q.z;
       const uint32_t word = (wsel & 2) ? hi : lo;
       ga[j] = ((blk == A0) | (blk == A3)) ? (word >> (a[j] & 31)) & 1u : 0u;
+#endif
+#if GHS_FILTER_GATED
+      gb[j] = ga[j] & (gbw[j] >> (b[j] & 31));  // unprobed b: "not known in the giant" (lab gathered)
+#else
       gb[j] = (gbw[j] >> (b[j] & 31)) & 1u;
+#endif
       out[j] = out[j] & ((ga[j] & gb[j]) == 0u);  // bitwise (no && : keeps the probes unsunk)
     }
     // level-1 split: labels only for this level's edges, and only for ends outside the giant
