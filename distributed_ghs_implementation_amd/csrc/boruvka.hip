@@ -102,6 +102,10 @@ __device__ __forceinline__ void flush_min(uint64_t *__restrict__ best, uint32_t 
 // plain read of that slot misses too.
 // k_filter: issue the random b-probe only for edges whose a-end is in the giant (1), or for
 // every heavy edge beside the a-probes (0)
+// k_jump_ident: a lane's 4 pointer walks advance together (1) or one after another (0)
+#ifndef GHS_JUMP_ILP
+#define GHS_JUMP_ILP 1
+#endif
 #ifndef GHS_FILTER_GATED
 #define GHS_FILTER_GATED 1
 #endif
@@ -1034,6 +1038,48 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
       }
     }
     uint32_t kb = 0;
+#if GHS_JUMP_ILP
+    // the lane's (up to) 4 walks advance together: each step issues the par loads of every
+    // unfinished walk before any is used, so a lane keeps 4 dependent chains in flight
+    uint32_t x[4], px[4], walking = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t c = (uint32_t)(i0 + k);
+      x[k] = c;
+      px[k] = pc[k];
+      if (lc[k] != c) continue;  // not a root at the level's open (or past n)
+      if (pc[k] == c) {          // still a root: kept iff it had an outgoing edge
+        if (bc[k] != KEY_NONE) {
+          best[c] = KEY_NONE;
+          kb |= 1u << (8 * k);
+        }
+        continue;
+      }
+      walking |= 1u << k;  // hooked: walk to the root (path splitting)
+    }
+    const uint32_t hooked = walking;
+    uint32_t steps = 0;
+    while (walking) {
+      uint32_t ppx[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ppx[k] = par[(walking >> k) & 1u ? px[k] : 0u];  // finished: a harmless load
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!((walking >> k) & 1u)) continue;
+        if (ppx[k] != px[k]) par[x[k]] = ppx[k];
+        x[k] = px[k];
+        px[k] = ppx[k];
+        if (px[k] == x[k]) walking &= ~(1u << k);
+      }
+      if (++steps > JUMP_MAX_STEPS) {
+        atomicOr(err, 4ull);
+        break;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if ((hooked >> k) & 1u) lab[i0 + k] = x[k];
+#else
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint32_t c = (uint32_t)(i0 + k);
@@ -1059,6 +1105,7 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
       }
       lab[c] = x;
     }
+#endif
     if (i0 < n4) *reinterpret_cast<uint32_t *>(flags + i0) = kb;
     else
       for (int k = 0; k < 4; ++k)
