@@ -106,6 +106,10 @@ __device__ __forceinline__ void flush_min(uint64_t *__restrict__ best, uint32_t 
 #ifndef GHS_JUMP_ILP
 #define GHS_JUMP_ILP 1
 #endif
+// k_resolve: 4 vertices per lane with their label walks interleaved (1), or one per thread (0)
+#ifndef GHS_RESOLVE4
+#define GHS_RESOLVE4 1
+#endif
 #ifndef GHS_FILTER_GATED
 #define GHS_FILTER_GATED 1
 #endif
@@ -1177,6 +1181,58 @@ __global__ __launch_bounds__(BLOCK) void k_resolve(uint32_t n, uint32_t *lab, co
                                                    uint64_t *__restrict__ bits, unsigned long long *__restrict__ err) {
   const uint32_t giant = giant_ptr[0];
   const uint64_t words = ((uint64_t)n + 63) / 64;
+#if GHS_RESOLVE4
+  // 4 vertices per lane (16-B lab load/store), their label walks advanced together; a lane's 4
+  // giant bits are OR-combined over 16 lanes into one 64-bit bitmap word
+  const uint64_t n4 = (uint64_t)n & ~3ull;
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  for (uint64_t i0 = (blockIdx.x * (uint64_t)BLOCK + threadIdx.x) * 4; i0 - lane * 4 < (uint64_t)n;
+       i0 += (uint64_t)gridDim.x * BLOCK * 4) {
+    uint32_t x[4], y[4], walking = 0;
+    if (i0 < n4) {
+      const uint4 l4 = *reinterpret_cast<const uint4 *>(lab + i0);
+      y[0] = l4.x; y[1] = l4.y; y[2] = l4.z; y[3] = l4.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) y[k] = i0 + k < n ? lab[i0 + k] : (uint32_t)(i0 + k);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      x[k] = (uint32_t)(i0 + k);
+      if (i0 + k < n && y[k] != x[k]) walking |= 1u << k;
+    }
+    uint32_t hops = 0;
+    while (walking) {
+      uint32_t ny[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ny[k] = lab[(walking >> k) & 1u ? y[k] : 0u];  // finished: a harmless load
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!((walking >> k) & 1u)) continue;
+        x[k] = y[k];
+        y[k] = ny[k];
+        if (y[k] == x[k]) walking &= ~(1u << k);
+      }
+      if (++hops > FIND_LAB_MAX_HOPS) {
+        atomicOr(err, 1ull);
+        break;
+      }
+    }
+    uint64_t part = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) part |= (uint64_t)((i0 + k < n) & (x[k] == giant)) << (4 * (lane & 15) + k);
+    if (i0 < n4) {
+      *reinterpret_cast<uint4 *>(lab + i0) = make_uint4(x[0], x[1], x[2], x[3]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (i0 + k < n) lab[i0 + k] = x[k];
+    }
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) part |= __shfl_xor(part, d);
+    if ((lane & 15) == 0 && (i0 >> 6) < words) bits[i0 >> 6] = part;
+  }
+#else
   for (uint64_t base = blockIdx.x * (uint64_t)BLOCK; base < (uint64_t)n; base += (uint64_t)gridDim.x * BLOCK) {
     const uint64_t v = base + threadIdx.x;
     bool in = false;
@@ -1188,6 +1244,7 @@ __global__ __launch_bounds__(BLOCK) void k_resolve(uint32_t n, uint32_t *lab, co
     const uint64_t b = __ballot(in);
     if ((threadIdx.x & (WAVE - 1)) == 0 && (v >> 6) < words) bits[v >> 6] = b;
   }
+#endif
 }
 
 
