@@ -102,9 +102,11 @@ __device__ __forceinline__ void flush_min(uint64_t *__restrict__ best, uint32_t 
 // plain read of that slot misses too.
 // k_filter: issue the random b-probe only for edges whose a-end is in the giant (1), or for
 // every heavy edge beside the a-probes (0)
-// k_jump_ident: a lane's 4 pointer walks advance together (1) or one after another (0)
+// k_jump_ident: a lane's 4 pointer walks advance together, from 4 consecutive vertices (1) or
+// from vertices 64 apart (2: walks started together are not chain neighbours, so they do not
+// duplicate each other's path splitting — gradient grid 55.7 -> 40.9 ms), or one after another (0)
 #ifndef GHS_JUMP_ILP
-#define GHS_JUMP_ILP 1
+#define GHS_JUMP_ILP 2
 #endif
 // k_resolve: 4 vertices per lane with their label walks interleaved (1), or one per thread (0)
 #ifndef GHS_RESOLVE4
@@ -1021,9 +1023,26 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
                                                       uint64_t *__restrict__ best, uint8_t *__restrict__ flags,
                                                       unsigned long long *__restrict__ err) {
   const uint64_t n4 = (uint64_t)n & ~3ull;
-  for (uint64_t i0 = (blockIdx.x * (uint64_t)BLOCK + threadIdx.x) * 4; i0 < n; i0 += (uint64_t)gridDim.x * BLOCK * 4) {
+  // every lane of a wave iterates while the wave's first vertex is < n (the strided variant's
+  // lanes own vertices below their own i0)
+  for (uint64_t i0 = (blockIdx.x * (uint64_t)BLOCK + threadIdx.x) * 4; (i0 & ~255ull) < n;
+       i0 += (uint64_t)gridDim.x * BLOCK * 4) {
     uint32_t lc[4], pc[4];
     uint64_t bc[4];
+#if GHS_JUMP_ILP == 2
+    // strided: the lane's 4 vertices lie 64 apart (4 coalesced wave loads per array), so the
+    // walks a lane advances together start from vertices that are not neighbours
+    const uint32_t ln = threadIdx.x & (WAVE - 1);
+    const uint64_t wb = i0 - ln * 4;  // the wave's 256 vertices
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t vv = wb + ln + 64 * k;
+      const bool in = vv < n;
+      lc[k] = in ? lab[vv] : LABEL_NONE;
+      pc[k] = in ? par[vv] : 0u;
+      bc[k] = in ? best[vv] : KEY_NONE;
+    }
+#else
     if (i0 < n4) {
       const uint4 l4 = *reinterpret_cast<const uint4 *>(lab + i0);
       const uint4 p4 = *reinterpret_cast<const uint4 *>(par + i0);
@@ -1041,14 +1060,20 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
         bc[k] = in ? best[i0 + k] : KEY_NONE;
       }
     }
+#endif
     uint32_t kb = 0;
 #if GHS_JUMP_ILP
     // the lane's (up to) 4 walks advance together: each step issues the par loads of every
     // unfinished walk before any is used, so a lane keeps 4 dependent chains in flight
     uint32_t x[4], px[4], walking = 0;
+#if GHS_JUMP_ILP == 2
+#define JV(k) (wb + ln + 64 * (k))
+#else
+#define JV(k) (i0 + (k))
+#endif
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const uint32_t c = (uint32_t)(i0 + k);
+      const uint32_t c = (uint32_t)JV(k);
       x[k] = c;
       px[k] = pc[k];
       if (lc[k] != c) continue;  // not a root at the level's open (or past n)
@@ -1082,7 +1107,14 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      if ((hooked >> k) & 1u) lab[i0 + k] = x[k];
+      if ((hooked >> k) & 1u) lab[JV(k)] = x[k];
+#if GHS_JUMP_ILP == 2
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (JV(k) < n) flags[JV(k)] = (uint8_t)(kb >> (8 * k));
+    continue;
+#endif
+#undef JV
 #else
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
