@@ -102,11 +102,12 @@ __device__ __forceinline__ void flush_min(uint64_t *__restrict__ best, uint32_t 
 // plain read of that slot misses too.
 // k_filter: issue the random b-probe only for edges whose a-end is in the giant (1), or for
 // every heavy edge beside the a-probes (0)
-// k_jump_ident: a lane's 4 pointer walks advance together, from 4 consecutive vertices (1) or
-// from vertices 64 apart (2: walks started together are not chain neighbours, so they do not
-// duplicate each other's path splitting — gradient grid 55.7 -> 40.9 ms), or one after another (0)
+// k_jump_ident: a lane's 4 pointer walks advance together, from 4 consecutive vertices (1), from
+// vertices 64 apart (2) or a whole grid stride apart (3: walks started together are far from each
+// other on a chain, so they do not duplicate each other's path splitting — gradient grid
+// 55.7 (1) -> 38.8 (2) -> 25.8 ms (3)), or one after another (0)
 #ifndef GHS_JUMP_ILP
-#define GHS_JUMP_ILP 2
+#define GHS_JUMP_ILP 3
 #endif
 // k_resolve: 4 vertices per lane with their label walks interleaved (1), or one per thread (0)
 #ifndef GHS_RESOLVE4
@@ -1025,18 +1026,32 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
   const uint64_t n4 = (uint64_t)n & ~3ull;
   // every lane of a wave iterates while the wave's first vertex is < n (the strided variant's
   // lanes own vertices below their own i0)
-  for (uint64_t i0 = (blockIdx.x * (uint64_t)BLOCK + threadIdx.x) * 4; (i0 & ~255ull) < n;
-       i0 += (uint64_t)gridDim.x * BLOCK * 4) {
+  const uint64_t tg = blockIdx.x * (uint64_t)BLOCK + threadIdx.x, S = (uint64_t)gridDim.x * BLOCK;
+  (void)tg;
+  (void)S;
+#if GHS_JUMP_ILP == 3
+  for (uint64_t i0 = tg * 4; i0 - tg * 4 < n; i0 += S * 4) {  // every thread while the chunk starts below n
+#else
+  for (uint64_t i0 = tg * 4; (i0 & ~255ull) < n; i0 += S * 4) {
+#endif
     uint32_t lc[4], pc[4];
     uint64_t bc[4];
 #if GHS_JUMP_ILP == 2
-    // strided: the lane's 4 vertices lie 64 apart (4 coalesced wave loads per array), so the
-    // walks a lane advances together start from vertices that are not neighbours
     const uint32_t ln = threadIdx.x & (WAVE - 1);
     const uint64_t wb = i0 - ln * 4;  // the wave's 256 vertices
+#define JV(k) (wb + ln + 64 * (uint64_t)(k))
+#elif GHS_JUMP_ILP == 3
+    const uint64_t cb = i0 - tg * 4;  // the grid's chunk of 4S vertices
+#define JV(k) (cb + tg + S * (uint64_t)(k))
+#else
+#define JV(k) (i0 + (uint64_t)(k))
+#endif
+#if GHS_JUMP_ILP >= 2
+    // strided: the lane's 4 vertices lie 64 (2) or S (3) apart (coalesced wave loads per
+    // array), so the walks a lane advances together start from vertices that are not neighbours
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const uint64_t vv = wb + ln + 64 * k;
+      const uint64_t vv = JV(k);
       const bool in = vv < n;
       lc[k] = in ? lab[vv] : LABEL_NONE;
       pc[k] = in ? par[vv] : 0u;
@@ -1066,11 +1081,6 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
     // the lane's (up to) 4 walks advance together: each step issues the par loads of every
     // unfinished walk before any is used, so a lane keeps 4 dependent chains in flight
     uint32_t x[4], px[4], walking = 0;
-#if GHS_JUMP_ILP == 2
-#define JV(k) (wb + ln + 64 * (k))
-#else
-#define JV(k) (i0 + (k))
-#endif
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint32_t c = (uint32_t)JV(k);
@@ -1108,13 +1118,12 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if ((hooked >> k) & 1u) lab[JV(k)] = x[k];
-#if GHS_JUMP_ILP == 2
+#if GHS_JUMP_ILP >= 2
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (JV(k) < n) flags[JV(k)] = (uint8_t)(kb >> (8 * k));
     continue;
 #endif
-#undef JV
 #else
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
