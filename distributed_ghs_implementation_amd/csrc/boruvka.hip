@@ -1016,9 +1016,9 @@ __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act
   }
 }
 
-// Stage 3 over the identity list (a single-rank level's first round): every vertex, 4 per lane
-// per step with 16-byte loads of lab, par and best — a stream, where the generic k_jump issues
-// 4-byte loads. A vertex that was not a root when the level opened (lab[c] != c) is never a label
+// Stage 3 over the identity list (a single-rank level's first round): every vertex, 4 per thread
+// per step (a grid stride apart by default, GHS_JUMP_ILP; 16-byte loads of lab, par and best
+// when consecutive) with their walks advanced together. A vertex that was not a root when the level opened (lab[c] != c) is never a label
 // and is skipped; a root that did not hook only tests its best slot; a root that hooked walks.
 __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par, uint32_t *__restrict__ lab,
                                                       uint64_t *__restrict__ best, uint8_t *__restrict__ flags,
