@@ -109,7 +109,8 @@ __device__ __forceinline__ void flush_min(uint64_t *__restrict__ best, uint32_t 
 #ifndef GHS_JUMP_ILP
 #define GHS_JUMP_ILP 3
 #endif
-// k_resolve: 4 vertices per lane with their label walks interleaved (1), or one per thread (0)
+// k_resolve: 4 vertices per lane with their label walks interleaved — consecutive (1) or a grid
+// stride apart (2) — or one per thread (0)
 #ifndef GHS_RESOLVE4
 #define GHS_RESOLVE4 1
 #endif
@@ -1222,7 +1223,46 @@ __global__ __launch_bounds__(BLOCK) void k_resolve(uint32_t n, uint32_t *lab, co
                                                    uint64_t *__restrict__ bits, unsigned long long *__restrict__ err) {
   const uint32_t giant = giant_ptr[0];
   const uint64_t words = ((uint64_t)n + 63) / 64;
-#if GHS_RESOLVE4
+#if GHS_RESOLVE4 == 2
+  // 4 vertices per thread a grid stride S apart (their walks start far apart on a chain, as in
+  // k_jump_ident), advanced together; each of the 4 is a coalesced wave slice of 64 vertices, so
+  // the giant bits of slice k are one ballot = one 64-bit bitmap word (S is a multiple of 64)
+  const uint64_t tg = blockIdx.x * (uint64_t)BLOCK + threadIdx.x, S = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t cb = 0; cb < (uint64_t)n; cb += 4 * S) {
+    uint32_t x[4], y[4], walking = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t vv = cb + tg + S * k;
+      x[k] = (uint32_t)vv;
+      y[k] = vv < n ? lab[vv] : (uint32_t)vv;
+      if (vv < n && y[k] != x[k]) walking |= 1u << k;
+    }
+    uint32_t hops = 0;
+    while (walking) {
+      uint32_t ny[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ny[k] = lab[(walking >> k) & 1u ? y[k] : 0u];  // finished: a harmless load
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!((walking >> k) & 1u)) continue;
+        x[k] = y[k];
+        y[k] = ny[k];
+        if (y[k] == x[k]) walking &= ~(1u << k);
+      }
+      if (++hops > FIND_LAB_MAX_HOPS) {
+        atomicOr(err, 1ull);
+        break;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t vv = cb + tg + S * k;
+      if (vv < n) lab[vv] = x[k];
+      const uint64_t b = __ballot((vv < n) && x[k] == giant);
+      if ((threadIdx.x & (WAVE - 1)) == 0 && (vv >> 6) < words) bits[vv >> 6] = b;
+    }
+  }
+#elif GHS_RESOLVE4
   // 4 vertices per lane (16-B lab load/store), their label walks advanced together; a lane's 4
   // giant bits are OR-combined over 16 lanes into one 64-bit bitmap word
   const uint64_t n4 = (uint64_t)n & ~3ull;
