@@ -34,13 +34,12 @@ _ERR_NAMES = {
 EXPORTED_SYMBOLS = (
     "ghs_abi_version", "ghs_last_error", "ghs_device_count", "ghs_mst_host",
     "ghs_default_config", "ghs_workspace_bytes", "ghs_mst_device",
-    "ghs_build_arcs_temp_bytes", "ghs_count_arcs_range", "ghs_build_arcs_range", "ghs_build_arcs",
     "ghs_check_canonical",
     "ghs_solver_create", "ghs_solver_minedge", "ghs_solver_exchange_buffer", "ghs_solver_pack_best",
     "ghs_solver_unpack_best",
     "ghs_solver_contract", "ghs_solver_finish", "ghs_solver_reset", "ghs_solver_destroy",
     "ghs_solver_hook_local", "ghs_solver_unpack_hook",
-    "ghs_rmat_temp_bytes", "ghs_rmat_generate", "ghs_grid_generate",
+    "ghs_rmat_temp_bytes", "ghs_rmat_generate", "ghs_rmat_tuples", "ghs_grid_generate",
 )
 
 
@@ -93,7 +92,7 @@ class RoundStatsList(collections.abc.Sequence):
         return repr(list(self))
 
 
-ABI_VERSION = 2  # include/ghs_mst.h GHS_MST_ABI_VERSION
+ABI_VERSION = 3  # include/ghs_mst.h GHS_MST_ABI_VERSION
 
 
 class Result(ctypes.Structure):
@@ -168,10 +167,6 @@ def load():
             "ghs_mst_host": (i32, [u32, u64, vp, vp, vp, vp, P(Result), P(RoundStats)]),
             "ghs_default_config": (None, [P(Config)]),
             "ghs_check_canonical": (i32, [u32, u64, vp, vp, vp, P(i32)]),
-            "ghs_build_arcs_temp_bytes": (sz, [u32, u64]),
-            "ghs_count_arcs_range": (i32, [u32, u64, vp, vp, u32, u32, vp, sz, vp, P(u64)]),
-            "ghs_build_arcs_range": (i32, [u32, u64, vp, vp, vp, u32, u32, vp, vp, vp, u64, vp, sz, vp, P(u64)]),
-            "ghs_build_arcs": (i32, [u32, u64, vp, vp, vp, vp, vp, vp, vp, sz, vp]),
             "ghs_workspace_bytes": (sz, [u32, u64, u64]),
             "ghs_mst_device": (i32, [u32, u64, vp, vp, vp, P(Config), vp, sz, vp, vp, P(Result), P(RoundStats)]),
             "ghs_solver_create": (i32, [u32, u64, vp, vp, vp, u64, u64, P(Config), vp, sz, vp, vp, P(vp)]),
@@ -187,6 +182,7 @@ def load():
             "ghs_solver_destroy": (i32, [vp]),
             "ghs_rmat_temp_bytes": (sz, [u32, u32]),
             "ghs_rmat_generate": (i32, [u32, u32, u64, u64, vp, vp, vp, P(u64), vp, sz, vp]),
+            "ghs_rmat_tuples": (i32, [u32, u32, u64, vp, vp]),
             "ghs_grid_generate": (i32, [u32, u32, u64, vp, vp, vp, vp]),
         }
         for name, (res, args) in sigs.items():

@@ -1824,6 +1824,20 @@ GHS_STREAM_KERNEL_6 void k_level_pass(const uint32_t *__restrict__ ru, const uin
   }
 }
 
+// Multi-rank error agreement: a rank's own error bits -> the error byte flags[n] of the level's
+// exchanged flag buffer (2: non-canonical input, 1: another invariant), and after the caller's
+// MAX all-reduce the combined byte -> this rank's error bits, so every rank fails in the same
+// call instead of leaving the others blocked in the next collective.
+__global__ void k_err_to_flag(const unsigned long long *__restrict__ err, uint8_t *__restrict__ flag) {
+  const unsigned long long e = *err;
+  *flag = (e & 8ull) ? 2 : (e ? 1 : 0);
+}
+
+__global__ void k_flag_to_err(const uint8_t *__restrict__ flag, unsigned long long *__restrict__ err) {
+  const uint8_t f = *flag;
+  if (f) atomicOr(err, f >= 2 ? 8ull : 32ull);
+}
+
 __global__ void k_iota(uint32_t *__restrict__ a, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     a[i] = (uint32_t)i;
@@ -2225,7 +2239,7 @@ static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, 
   p = carve(N * 8); if (s) s->best = (uint64_t *)p;
   p = carve(N * 4); if (s) s->act[0] = (uint32_t *)p;
   p = carve(N * 4); if (s) s->act[1] = (uint32_t *)p;
-  p = carve(N ? N : 1); if (s) s->flags = (uint8_t *)p;
+  p = carve(N + 1); if (s) s->flags = (uint8_t *)p;  // + the multi-rank error byte flags[n]
   p = carve(((N + 127) / 128) * 16 + 16); if (s) s->bits = (uint64_t *)p;
   p = carve(NSAMPLE_MAX * 4); if (s) s->sample = (uint32_t *)p;
   p = carve((PLAN_MAX + 1) * 8); if (s) s->d_thr = (uint64_t *)p;
@@ -2362,6 +2376,7 @@ static bool levels_done(ghs_solver *s) {
 static int fail_counters(ghs_solver *s, unsigned long long err, const char *where) {
   s->phase = 2;
   if (err & 8) GHS_FAIL(GHS_E_NONCANON, "edge list is not canonical (need u < v < n, strictly ascending (u, v))");
+  if (err == 32) GHS_FAIL(GHS_E_STATE, std::string("another rank failed ") + where);
   GHS_FAIL(GHS_E_STATE, std::string("internal invariant violated ") + where + " (code " + std::to_string(err) + ")");
 }
 
@@ -2397,7 +2412,7 @@ static int open_level(ghs_solver *s, bool async_open = false) {
   // write-backs were ~0.25 GB per k_filter launch) plus the select.
   const bool ident0 = single && async_open;
   uint8_t *mark = ident0 ? nullptr : s->flags;
-  if (!ident0) GHS_HIP_CHECK(hipMemsetAsync(s->flags, 0, s->n, st));
+  if (!ident0) GHS_HIP_CHECK(hipMemsetAsync(s->flags, 0, (size_t)s->n + 1, st));
   s->open_ident = ident0;
   unsigned G = 1;
   const uint64_t TC = s->e_hi > s->e_lo ? s->e_hi - (s->e_lo & ~3ull) : 0;  // canonical passes stream [e_lo & ~3, e_hi)
@@ -2460,6 +2475,8 @@ static int open_level(ghs_solver *s, bool async_open = false) {
   }
 
   if (!single) {  // the caller OR-combines the flags across ranks, then open_level_finish
+    k_err_to_flag<<<1, 1, 0, st>>>(s->cnt + C_ERR, s->flags + s->n);  // travels with the flags
+    GHS_HIP_CHECK(hipGetLastError());
     s->pending_exchange = true;
     s->open_G = G;
     return GHS_OK;
@@ -2479,6 +2496,10 @@ static int open_level_finish(ghs_solver *s) {
   if (int rc = plan_sync(s)) return rc;
   const uint64_t w_hi = s->thresholds[lv + 1];
   const unsigned G = s->open_G;
+  if (s->pending_exchange) {  // several ranks: the combined error byte (any rank's error)
+    k_flag_to_err<<<1, 1, 0, st>>>(s->flags + s->n, s->cnt + C_ERR);
+    GHS_HIP_CHECK(hipGetLastError());
+  }
   s->pending_exchange = false;
   if (int rc = select_lb(s, nullptr, s->cnt + C_N, s->n, s->act[0], s->cnt + C_ACT)) return rc;
   s->act_ident = false;
@@ -2922,7 +2943,7 @@ int ghs_solver_exchange_buffer(ghs_solver_t *s, uint8_t **d_flags, uint64_t *byt
   if (!s->pending_exchange) GHS_FAIL(GHS_E_STATE, "no exchange pending");
   GHS_HIP_CHECK(hipStreamSynchronize(s->stream));  // the flags are complete before the caller reads them
   *d_flags = s->flags;
-  *bytes = s->n;
+  *bytes = (uint64_t)s->n + 1;  // n fragment flags + the error byte
   return GHS_OK;
 }
 

@@ -22,12 +22,8 @@ extern "C" int ghs_mst_host(uint32_t n, uint64_t m, const uint32_t *u, const uin
   if (m >= (1ull << 31)) GHS_FAIL(GHS_E_ARG, "m must be < 2^31");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) GHS_FAIL(GHS_E_NODEVICE, "no HIP device");
-  // host-side canonical check (cheap, gives a precise error before any device work)
-  for (uint64_t e = 0; e < m; ++e) {
-    bool ok = u[e] < v[e] && v[e] < n;
-    if (ok && e) ok = (u[e - 1] < u[e]) || (u[e - 1] == u[e] && v[e - 1] < v[e]);
-    if (!ok) GHS_FAIL(GHS_E_NONCANON, "edge " + std::to_string(e) + " breaks canonical order (u < v < n, ascending)");
-  }
+  // canonicity is validated on the device by the solve's first pass (k_select, GHS_E_NONCANON
+  // before any id indexes an array): no serial host loop in front of the copy
   const size_t ws = ghs_workspace_bytes(n, m, m);
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t off_u = 0, off_v = off_u + al(m * 4), off_w = off_v + al(m * 4), off_mst = off_w + al(m * 4),

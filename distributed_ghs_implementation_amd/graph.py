@@ -11,9 +11,13 @@ ghs_mst.json), "algorithm": "Boruvka (HIP)", edges sorted ascending.
 Canonical edge list (the contract of include/ghs_mst.h): self-loops dropped, each unordered
 pair once as (min, max) with the LAST weight given for it (nx.Graph.add_edge overwrites, which
 is how every reference entry point builds its graph: ghs_implementation.py:425-426,
-check_mst.py:6-7), sorted ascending by (min, max); eid = position. Weights are non-negative
-integers < 2^32 (the reference draws random.randint(1, 10): create_graph_files.py:38,
-ghs_implementation.py:718).
+check_mst.py:6-7), sorted ascending by (min, max); eid = position. The engine computes on uint32
+weights: integers in [0, 2^32) (the reference draws random.randint(1, 10):
+create_graph_files.py:38, ghs_implementation.py:718) go through unchanged; any other numeric
+weights (negative, float, > 2^32 — nx.Graph, and so the reference's GHSAlgorithm at
+ghs_implementation.py:417-440, accepts any comparable weight) are replaced by their dense rank
+among the distinct values, an order-preserving map that keeps ties tied, so the MSF edge set is
+the same; the original values are kept (`CanonicalGraph.weights`) for the reported weights.
 
 Binary format for large graphs (.mstbin, little endian): 8-byte magic b"MSTBIN1\\0", uint32 n,
 uint32 flags (bit 0 = canonical), uint64 m, then u[m], v[m], w[m] as uint32 arrays.
@@ -29,17 +33,21 @@ _NODE_RE = re.compile(r"^node_(\d+)\.json$")
 
 
 class CanonicalGraph:
-    """n vertices + canonical (u < v, ascending, unique) uint32 arrays u, v, w."""
+    """n vertices + canonical (u < v, ascending, unique) uint32 arrays u, v, w. `weights`: the
+    caller's original weights in canonical order when w holds their ranks (else None)."""
 
-    __slots__ = ("n", "u", "v", "w")
+    __slots__ = ("n", "u", "v", "w", "weights")
 
-    def __init__(self, n, u, v, w):
+    def __init__(self, n, u, v, w, weights=None):
         self.n = int(n)
         self.u = np.ascontiguousarray(u, dtype=np.uint32)
         self.v = np.ascontiguousarray(v, dtype=np.uint32)
         self.w = np.ascontiguousarray(w, dtype=np.uint32)
+        self.weights = None if weights is None else np.asarray(weights)
         if not (len(self.u) == len(self.v) == len(self.w)):
             raise ValueError("u, v, w must have equal length")
+        if self.weights is not None and len(self.weights) != len(self.w):
+            raise ValueError("weights must align with the canonical edges")
 
     @property
     def m(self):
@@ -53,30 +61,57 @@ class CanonicalGraph:
             return self
         if not np.all(u < v) or int(v.max()) >= self.n:
             raise ValueError("canonical edge list needs u < v < n")
-        key = (u << 32) | v
+        key = (self.u.astype(np.uint64) << np.uint64(32)) | self.v.astype(np.uint64)
         if not np.all(key[1:] > key[:-1]):
             raise ValueError("canonical edge list must be strictly ascending in (u, v)")
         return self
 
+    def weight_of(self, i):
+        """The caller's weight of canonical edge i (a Python int or float)."""
+        if self.weights is None:
+            return int(self.w[i])
+        x = self.weights[i]
+        return x.item() if hasattr(x, "item") else x
+
+    def total_weight(self, mask):
+        """Sum of the caller's weights over a mask of canonical edges."""
+        if self.weights is None:
+            return int(self.w[np.asarray(mask, bool)].astype(np.uint64).sum())
+        sel = self.weights[np.asarray(mask, bool)]
+        return sum(x.item() if hasattr(x, "item") else x for x in sel)
+
     def edge_triples(self, mask=None):
         idx = np.arange(self.m) if mask is None else np.flatnonzero(mask)
-        return [(int(self.u[i]), int(self.v[i]), int(self.w[i])) for i in idx]
+        return [(int(self.u[i]), int(self.v[i]), self.weight_of(i)) for i in idx]
 
 
 def _as_weight_array(ws):
+    """Weights -> (uint32 engine weights, the original values or None). Integers in [0, 2^32)
+    pass unchanged; other numeric weights are replaced by their dense rank (order-preserving,
+    ties stay tied)."""
     w = np.asarray(ws)
     if w.size == 0:
-        return np.zeros(0, np.uint32)
-    if w.dtype.kind == "f":
-        if not np.all(np.isfinite(w)) or not np.all(w == np.floor(w)):
-            raise ValueError("weights must be integers (the reference uses random.randint weights)")
+        return np.zeros(0, np.uint32), None
+    if w.dtype.kind == "O":  # Python ints beyond int64, mixed int / float
+        try:
+            w = np.asarray(ws, dtype=np.float64) if any(isinstance(x, float) for x in ws) \
+                else np.asarray([int(x) for x in ws], dtype=object)
+        except (TypeError, ValueError) as exc:
+            raise ValueError("weights must be numbers") from exc
+    if w.dtype.kind == "b":
         w = w.astype(np.int64)
-    elif w.dtype.kind not in "iu":
-        w = np.array([int(x) for x in ws], dtype=np.int64)
-    w = w.astype(np.int64)
-    if np.any(w < 0) or np.any(w >= (1 << 32)):
-        raise ValueError("weights must lie in [0, 2^32)")
-    return w.astype(np.uint32)
+    if w.dtype.kind in "iu" and int(w.min()) >= 0 and int(w.max()) < (1 << 32):
+        return w.astype(np.uint32), None
+    if w.dtype.kind == "f" and np.any(np.isnan(w)):
+        raise ValueError("weights must not be NaN")
+    if w.dtype.kind not in "iufO":
+        raise ValueError("weights must be numbers")
+    if w.dtype.kind == "O":
+        uniq = sorted(set(w.tolist()))
+        rank = {x: i for i, x in enumerate(uniq)}
+        return np.array([rank[x] for x in w.tolist()], dtype=np.uint32), w
+    uniq = np.unique(w)
+    return np.searchsorted(uniq, w).astype(np.uint32), w
 
 
 def canonicalize(num_nodes, edges=None, u=None, v=None, w=None):
@@ -92,14 +127,14 @@ def canonicalize(num_nodes, edges=None, u=None, v=None, w=None):
         if edges:
             arr = np.array([(int(a), int(b)) for a, b, _ in edges], dtype=np.int64).reshape(-1, 2)
             u, v = arr[:, 0], arr[:, 1]
-            w = _as_weight_array([c for _, _, c in edges])
+            w, orig = _as_weight_array([c for _, _, c in edges])
         else:
             u = v = np.zeros(0, np.int64)
-            w = np.zeros(0, np.uint32)
+            w, orig = np.zeros(0, np.uint32), None
     else:
         u = np.asarray(u, dtype=np.int64)
         v = np.asarray(v, dtype=np.int64)
-        w = _as_weight_array(w)
+        w, orig = _as_weight_array(w)
     if len(u):
         if u.min() < 0 or v.min() < 0 or u.max() >= n or v.max() >= n:
             raise ValueError(f"vertex id out of range [0, {n})")
@@ -107,7 +142,9 @@ def canonicalize(num_nodes, edges=None, u=None, v=None, w=None):
     a = np.minimum(u, v)[keep]
     b = np.maximum(u, v)[keep]
     w = w[keep]
-    key = (a << 32) | b
+    if orig is not None:
+        orig = orig[keep]
+    key = (a.astype(np.uint64) << np.uint64(32)) | b.astype(np.uint64)
     # stable sort by key; for repeated keys keep the LAST occurrence (nx add_edge overwrite)
     order = np.argsort(key, kind="stable")
     ks = key[order]
@@ -115,6 +152,9 @@ def canonicalize(num_nodes, edges=None, u=None, v=None, w=None):
     if len(ks) > 1:
         last[:-1] = ks[1:] != ks[:-1]
     sel = order[last]
+    if orig is not None:
+        # ranks were taken over every given value; the canonical list keeps the same order
+        return CanonicalGraph(n, a[sel], b[sel], w[sel], weights=orig[sel])
     return CanonicalGraph(n, a[sel], b[sel], w[sel])
 
 
@@ -175,8 +215,8 @@ def write_graph_dir(graph, graph_dir):
 
 def mst_result_dict(mst_triples, algorithm="Boruvka (HIP)"):
     """The mst_result_mpi.json schema (ghs_implementation_mpi.py:811-816), edges sorted."""
-    edges = sorted([int(a), int(b), int(c)] for a, b, c in mst_triples)
-    return {"mst_edges": edges, "total_weight": int(sum(e[2] for e in edges)),
+    edges = sorted([int(a), int(b), c if isinstance(c, (int, float)) else c.item()] for a, b, c in mst_triples)
+    return {"mst_edges": edges, "total_weight": sum(e[2] for e in edges),
             "num_edges": len(edges), "algorithm": algorithm}
 
 

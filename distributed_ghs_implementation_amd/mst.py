@@ -12,7 +12,10 @@ Deliberate differences from the reference (all documented in DESIGN.md):
   * isolated vertices / disconnected inputs give a spanning forest instead of NetworkXError
     (ghs_implementation.py:433-436);
   * `timeout` is accepted for signature compatibility; the engine terminates by construction
-    (at most ceil(log2 n) + 1 rounds; a hang guard raises GHS_E_ROUNDCAP).
+    (at most ceil(log2 n) + 1 rounds; a hang guard raises GHS_E_ROUNDCAP);
+  * weights: any numbers, as nx.Graph accepts (ghs_implementation.py:417-440). Integers in
+    [0, 2^32) go to the engine as they are; others (negative, float, larger) as their dense rank
+    (order-preserving, ties kept: the same MSF), and results report the caller's values.
 """
 import ctypes
 import time
@@ -29,7 +32,9 @@ class MSTResult:
     def __init__(self, graph, in_mst, total_weight, rounds, stats, ms_total):
         self.graph = graph
         self.in_mst = in_mst.astype(bool)
-        self.total_weight = int(total_weight)
+        # the engine sums uint32 weights; for rank-mapped weights (graph.weights) the caller's
+        # own values are summed over the same edges
+        self.total_weight = int(total_weight) if graph.weights is None else graph.total_weight(self.in_mst)
         self.rounds = int(rounds)
         self.stats = stats
         self.ms_total = float(ms_total)

@@ -37,10 +37,11 @@ def networkx_msf(graph):
     import networkx as nx
     G = nx.Graph()
     G.add_nodes_from(range(graph.n))
-    for a, b, c in zip(graph.u.tolist(), graph.v.tolist(), graph.w.tolist()):
+    gw = graph.w if graph.weights is None else graph.weights
+    for a, b, c in zip(graph.u.tolist(), graph.v.tolist(), gw.tolist()):
         G.add_edge(a, b, weight=c)
     T = nx.minimum_spanning_tree(G, weight="weight")
-    edges = sorted((min(a, b), max(a, b), int(d["weight"])) for a, b, d in T.edges(data=True))
+    edges = sorted((min(a, b), max(a, b), d["weight"]) for a, b, d in T.edges(data=True))
     return edges, sum(e[2] for e in edges)
 
 
@@ -48,19 +49,22 @@ def verify_forest(graph, mst_triples, use_networkx=True, nx_max_edges=NX_MAX_EDG
     """Check `mst_triples` [(u, v, w)] against the canonical `graph`. Returns a report dict;
     report["ok"] is True iff every structural check passes and (when it ran) the NetworkX
     weight matches."""
-    t = np.asarray(list(mst_triples), dtype=np.int64).reshape(-1, 3)
+    triples = list(mst_triples)
+    t = np.asarray([(a, b) for a, b, _ in triples], dtype=np.int64).reshape(-1, 2)
+    tw = [c for _, _, c in triples]  # the caller's weights (ints, or any numbers: graph.weights)
     tu = np.minimum(t[:, 0], t[:, 1])
     tv = np.maximum(t[:, 0], t[:, 1])
     rep = {"num_nodes": graph.n, "num_edges": graph.m, "mst_edges": int(len(t)),
-           "mst_weight": int(t[:, 2].sum()) if len(t) else 0}
+           "mst_weight": sum(tw) if tw else 0}
     # every result edge is a graph edge with the graph's weight (canonical order: searchsorted)
-    gkey = (graph.u.astype(np.int64) << 32) | graph.v.astype(np.int64)
-    tkey = (tu << 32) | tv
+    gkey = (graph.u.astype(np.uint64) << np.uint64(32)) | graph.v.astype(np.uint64)
+    tkey = (tu.astype(np.uint64) << np.uint64(32)) | tv.astype(np.uint64)
     pos = np.searchsorted(gkey, tkey)
     found = (pos < graph.m) & (gkey[np.minimum(pos, max(graph.m - 1, 0))] == tkey) if graph.m else np.zeros(len(t), bool)
     rep["edges_in_graph"] = bool(found.all())
+    gw = graph.w.astype(np.int64) if graph.weights is None else graph.weights
     rep["weights_match_graph"] = bool(rep["edges_in_graph"] and
-                                      np.array_equal(graph.w[pos[found]].astype(np.int64), t[found, 2]))
+                                      all(gw[p] == c for p, c in zip(pos[found].tolist(), np.asarray(tw, dtype=object)[found])))
     rep["duplicate_edges"] = int(len(tkey) - len(np.unique(tkey)))
     cg = _components(graph.n, graph.u, graph.v)
     ct = _components(graph.n, tu, tv)
@@ -81,10 +85,10 @@ def verify_forest(graph, mst_triples, use_networkx=True, nx_max_edges=NX_MAX_EDG
         except ImportError:
             nx_edges = None
         if nx_edges is not None:
-            rep["networkx_weight"] = int(nx_w)
-            rep["weight_matches_networkx"] = int(nx_w) == rep["mst_weight"]
+            rep["networkx_weight"] = nx_w
+            rep["weight_matches_networkx"] = nx_w == rep["mst_weight"]
             # informational under weight ties (the MST edge set is then not unique)
-            rep["edge_set_matches_networkx"] = nx_edges == sorted(map(tuple, t.tolist()))
+            rep["edge_set_matches_networkx"] = [e[:2] for e in nx_edges] == sorted(zip(tu.tolist(), tv.tolist()))
             ok = ok and rep["weight_matches_networkx"]
     rep["ok"] = bool(ok)
     return rep
@@ -93,7 +97,7 @@ def verify_forest(graph, mst_triples, use_networkx=True, nx_max_edges=NX_MAX_EDG
 def experiment_record(experiment, graph, mst_triples, num_input_edges=None, **kw):
     """One ghs_experiments.json entry (ghs_implementation.py:766-776 schema) for a result."""
     rep = verify_forest(graph, mst_triples, **kw)
-    edges = sorted([int(a), int(b), int(c)] for a, b, c in mst_triples)
+    edges = sorted([int(a), int(b), c] for a, b, c in mst_triples)
     correct = rep["ok"] if rep["networkx_weight"] is None else bool(rep["ok"] and rep["weight_matches_networkx"])
     return {"experiment": experiment, "num_nodes": graph.n,
             "num_edges": graph.m if num_input_edges is None else int(num_input_edges),

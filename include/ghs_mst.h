@@ -13,7 +13,9 @@
  *   - all functions return GHS_OK (0) or a negative GHS_E_* code and never abort;
  *     ghs_last_error() returns a thread-local message for the last failure;
  *   - "canonical edge list": u[e] < v[e] < n, strictly ascending (u, v), no duplicates;
- *     eid = e. Ties resolve under the strict key (w, u, v) == (w, eid) — the order in which
+ *     eid = e. Size limits: m < 2^31 (edge ids are 32-bit inside the 64-bit keys and the
+ *     kernels' byte offsets) and n <= 2^32 - 1 (ids < n, so 0xffffffff never names a vertex
+ *     and marks dead entries); every entry point that takes m returns GHS_E_ARG past the cap. Ties resolve under the strict key (w, u, v) == (w, eid) — the order in which
  *     NetworkX Kruskal (the reference's verifier, ghs_implementation.py:746) visits edges on a
  *     canonically built graph. The result is a minimum spanning FOREST.
  *   - d_* pointers are device pointers (HIP / torch device memory) on the current device;
@@ -31,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GHS_MST_ABI_VERSION 2
+#define GHS_MST_ABI_VERSION 3
 
 #define GHS_OK 0
 #define GHS_NEED_EXCHANGE 1   /* ghs_solver_minedge on a multi-rank solver opened a level: OR-combine
@@ -124,18 +126,6 @@ int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *
                    const ghs_config_t *cfg, void *d_workspace, size_t workspace_bytes, uint8_t *d_in_mst,
                    void *stream, ghs_result_t *result, ghs_round_stats_t *stats);
 
-/* Standalone ingest utility (not needed by ghs_mst_device): the full symmetric arc list
- * (asrc/adst u32, akey u64, 2m entries, grouped by source) of a canonical edge list, or only the
- * arcs whose source lies in [src_lo, src_hi). Validates canonicity (GHS_E_NONCANON). */
-size_t ghs_build_arcs_temp_bytes(uint32_t n, uint64_t m);
-int ghs_count_arcs_range(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, uint32_t src_lo,
-                         uint32_t src_hi, void *d_temp, size_t temp_bytes, void *stream, uint64_t *num_arcs);
-int ghs_build_arcs_range(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
-                         uint32_t src_lo, uint32_t src_hi, uint32_t *d_asrc, uint32_t *d_adst, uint64_t *d_akey,
-                         uint64_t arc_capacity, void *d_temp, size_t temp_bytes, void *stream, uint64_t *num_arcs);
-int ghs_build_arcs(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
-                   uint32_t *d_asrc, uint32_t *d_adst, uint64_t *d_akey, void *d_temp, size_t temp_bytes,
-                   void *stream);
 /* device-side canonicity check: *ok = 1 iff u < v < n and (u, v) strictly ascending */
 int ghs_check_canonical(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, void *stream, int *ok);
 
@@ -154,14 +144,21 @@ int ghs_check_canonical(uint32_t n, uint64_t m, const uint32_t *d_u, const uint3
  *         ghs_solver_unpack_best(h, d_dense)
  *         ghs_solver_contract(h, &done)        hook + pointer-jump + next fragment list
  *   ghs_solver_finish(h, result, stats); ghs_solver_destroy(h)
- * Identical inputs on every rank => identical hook decisions => replicated in_mst. */
+ * Identical inputs on every rank => identical hook decisions => identical totals (ghs_solver_finish)
+ * on every rank. The MSF flags are NOT replicated when ghs_solver_hook_local is used (the
+ * default of the Python driver): each rank's d_in_mst then holds the hooks whose winning edge
+ * it owns, and the MSF is the OR over the ranks (see ghs_solver_hook_local).
+ * Errors: a rank that finds its edge range non-canonical records it in the exchanged flag
+ * buffer (its last byte), so after the caller's MAX every rank returns GHS_E_NONCANON from the
+ * same ghs_solver_minedge call — no rank is left waiting in a collective. */
 typedef struct ghs_solver ghs_solver_t;
 int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
                       uint64_t e_lo, uint64_t e_hi, const ghs_config_t *cfg, void *d_workspace,
                       size_t workspace_bytes, uint8_t *d_in_mst, void *stream, ghs_solver_t **out);
 /* runs the min-edge kernel; *num_active = fragments whose best slot must be all-reduced */
 int ghs_solver_minedge(ghs_solver_t *h, uint64_t *num_active);
-/* the n-byte flag array to OR-combine (uint8 MAX all-reduce) after GHS_NEED_EXCHANGE */
+/* the flag array to OR-combine (uint8 MAX all-reduce) after GHS_NEED_EXCHANGE: n fragment flags
+ * + 1 error byte (*bytes = n + 1) */
 int ghs_solver_exchange_buffer(ghs_solver_t *h, uint8_t **d_flags, uint64_t *bytes);
 int ghs_solver_pack_best(ghs_solver_t *h, int64_t *d_dense);
 int ghs_solver_unpack_best(ghs_solver_t *h, const int64_t *d_dense);
@@ -195,6 +192,10 @@ size_t ghs_rmat_temp_bytes(uint32_t scale, uint32_t edgefactor);
 int ghs_rmat_generate(uint32_t scale, uint32_t edgefactor, uint64_t seed, uint64_t wseed,
                       uint32_t *d_u, uint32_t *d_v, uint32_t *d_w, uint64_t *m_out,
                       void *d_temp, size_t temp_bytes, void *stream);
+/* The raw R-MAT tuples of ghs_rmat_generate before its canonical sort/dedupe (generator parity
+ * tests): d_keys[t] = min << scale | max of tuple t, or 2^(2 scale) - 1 for a self-loop;
+ * edgefactor * 2^scale entries. */
+int ghs_rmat_tuples(uint32_t scale, uint32_t edgefactor, uint64_t seed, uint64_t *d_keys, void *stream);
 /* k x k grid, vertex r*k+c, right + down edges (m = 2k(k-1)), canonical order.
  * mode 0: unique hashed weights; mode 1: "road-like" gradient weights w = eid (unique, forces
  * long hook chains). */

@@ -13,6 +13,13 @@ root), pointer-jump to roots, next active list = roots that had an outgoing edge
 list holds at most one fragment. A level starts with the
 fragments that have a level edge on ANY rank: minedge returns None after opening a level, the
 caller OR-combines exchange_buffer() across ranks (all-reduce MAX) and calls minedge again.
+
+Owner-computes CONNECT (ghs_solver_hook_local / ghs_solver_unpack_hook, k_win + k_pack_hook +
+k_unpack_hook in boruvka.hip), several ranks, a level's first round: each rank hooks the
+fragments whose winning edge (best key) is one of ITS level edges and marks that edge's MSF flag
+on its own copy only; slot i of the int32 exchange carries par[c] ^ c for active fragment c (0
+where another rank owns the winner), a MAX all-reduce gathers every hook, and unpack applies
+them (par, totals) identically on every rank. The MSF is then the OR of the ranks' flags.
 """
 import numpy as np
 
@@ -21,7 +28,7 @@ SIGN = np.uint64(0x8000000000000000)
 
 
 class CpuStepper:
-    def __init__(self, n, u, v, w, e_lo, e_hi, thresholds=(0, 1 << 32)):
+    def __init__(self, n, u, v, w, e_lo, e_hi, thresholds=(0, 1 << 32), ranks=1):
         import torch  # only for the dense all-reduce buffer
         self.torch = torch
         self.n = n
@@ -41,6 +48,10 @@ class CpuStepper:
         self.total = 0
         self.count = 0
         self.done = n == 0
+        self.ranks = ranks
+        self.level_round = 0
+        self.hook_par = None  # par of an owner-computed CONNECT (unpack_hook), else None
+        self.hooks_exchanged = 0  # rounds whose CONNECT came through the hook exchange
 
     def _open_level(self):
         lo, hi = self.thr[self.level], self.thr[self.level + 1]
@@ -50,6 +61,8 @@ class CpuStepper:
         cu, cv = self.comp[self.u[e]], self.comp[self.v[e]]
         keep = cu != cv
         e, cu, cv = e[keep], cu[keep], cv[keep]
+        self.level_edges = e  # this rank's edges of the level (their ends carry the current roots)
+        self.level_round = 0
         self.src = np.concatenate([cu, cv])
         self.dst = np.concatenate([cv, cu])
         self.akey = np.concatenate([self.key[e], self.key[e]])
@@ -92,25 +105,61 @@ class CpuStepper:
     def unpack(self, dense):
         self.best[self.active] = dense.numpy().view(np.uint64) ^ SIGN
 
+    def hook_local(self):
+        """Owner-computes CONNECT of a level's first round (several ranks): the int32 slots
+        par[c] ^ c to all-reduce with MAX, or None (the round hooks inside contract)."""
+        if self.ranks <= 1 or self.level_round != 0 or self.done or not len(self.active) \
+                or not self.level_open or self.n > (1 << 31):
+            return None
+        e = self.level_edges
+        ca, cb = self.comp[self.u[e]], self.comp[self.v[e]]
+        k = self.key[e]
+        wa = self.best[ca] == k
+        wb = self.best[cb] == k
+        ha = wa & ~(wb & (ca < cb))  # a hooks to b (mutual pair: the smaller label stays root)
+        hb = wb & ~(wa & (cb < ca))
+        par = np.arange(self.n, dtype=np.int64)
+        par[ca[ha]] = cb[ha]
+        par[cb[hb]] = ca[hb]
+        self.in_mst[e[ha | hb]] = 1  # the owner's mark
+        slots = (par[self.active] ^ self.active).astype(np.int32)
+        return self.torch.from_numpy(slots)
+
+    def unpack_hook(self, dense):
+        x = dense.numpy().astype(np.int64) & 0xFFFFFFFF
+        hooked = x != 0
+        c = self.active[hooked]
+        par = np.arange(self.n, dtype=np.int64)
+        par[c] = c ^ x[hooked]
+        self.total += int((self.best[c] >> np.uint64(32)).sum())
+        self.count += int(hooked.sum())
+        self.hook_par = par
+        self.hooks_exchanged += 1
+
     def contract(self):
         if self.done:
             return True
         act = self.active
-        par = np.arange(self.n, dtype=np.int64)
         k = self.best[act]
         has = k != KEY_NONE
-        c = act[has]
-        kk = k[has]
-        eid = (kk & np.uint64(0xFFFFFFFF)).astype(np.int64)
-        la = self.comp[self.u[eid]]
-        lb = self.comp[self.v[eid]]
-        other = np.where(la == c, lb, la)
-        mutual = self.best[other] == kk
-        hook = ~(mutual & (c < other))
-        par[c[hook]] = other[hook]
-        self.in_mst[eid[hook]] = 1
-        self.total += int((kk[hook] >> np.uint64(32)).sum())
-        self.count += int(hook.sum())
+        if self.hook_par is not None:  # owner-computed CONNECT (unpack_hook) already applied
+            par = self.hook_par
+            self.hook_par = None
+        else:
+            par = np.arange(self.n, dtype=np.int64)
+            c = act[has]
+            kk = k[has]
+            eid = (kk & np.uint64(0xFFFFFFFF)).astype(np.int64)
+            la = self.comp[self.u[eid]]
+            lb = self.comp[self.v[eid]]
+            other = np.where(la == c, lb, la)
+            mutual = self.best[other] == kk
+            hook = ~(mutual & (c < other))
+            par[c[hook]] = other[hook]
+            self.in_mst[eid[hook]] = 1
+            self.total += int((kk[hook] >> np.uint64(32)).sum())
+            self.count += int(hook.sum())
+        self.level_round += 1
         while True:  # pointer jumping to the roots
             nxt = par[par]
             if np.array_equal(nxt, par):

@@ -7,6 +7,9 @@
                     parity cases and the bench's cpu_baseline (kind "port").
 * `boruvka_omp_c`   OpenMP Borůvka on all given cores (oracle/boruvka_omp.c): the same canonical
                     MSF (unique keys), the bench's all-cores CPU baseline.
+* `rmat_pairs_c` / `rmat_canonical` / `grid_canonical`  the synthetic generators restated
+                    (oracle/generators.c, numpy): the GPU generators are checked against them
+                    tuple for tuple (SURVEY §8(d) "reproducible by both CPU oracle and GPU generator").
 
 Reference anchors: the MST the reference verifies against is NetworkX Kruskal
 (ghs_implementation.py:746, create_graph_files.py:141, check_mst.py:9); the raw-edge semantics
@@ -43,6 +46,10 @@ def lib():
         L.oracle_boruvka_omp.argtypes = [ctypes.c_uint32, ctypes.c_uint64, u32p, u32p, u32p, ctypes.c_int,
                                          u8p, u64p, u64p, u32p]
         L.oracle_boruvka_omp.restype = ctypes.c_int
+        L.oracle_rmat_pairs.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, u32p, u32p]
+        L.oracle_rmat_pairs.restype = ctypes.c_int
+        L.oracle_hash_weights.argtypes = [ctypes.c_uint64, ctypes.c_uint64, u32p]
+        L.oracle_hash_weights.restype = None
         _LIB = L
     return _LIB
 
@@ -63,6 +70,19 @@ def canonicalize_py(n, edges):
         last[(min(u, v), max(u, v))] = w
     keys = sorted(last)
     return [(a, b, last[(a, b)]) for a, b in keys]
+
+
+def canonicalize_py_any(n, edges):
+    """canonicalize_py for any comparable weights (kept as given)."""
+    last = {}
+    for u, v, w in edges:
+        u, v = int(u), int(v)
+        if not (0 <= u < n and 0 <= v < n):
+            raise ValueError("vertex out of range")
+        if u == v:
+            continue
+        last[(min(u, v), max(u, v))] = w
+    return [(a, b, last[(a, b)]) for a, b in sorted(last)]
 
 
 def kruskal_py(n, canon_edges):
@@ -139,3 +159,58 @@ def boruvka_omp_c(n, u, v, w, threads=0):
     if rc != 0:
         raise ValueError(f"oracle_boruvka_omp failed rc={rc}")
     return in_mst[:m], tw.value, k.value, r.value
+
+
+def mix32_np(x):
+    """The bijective 32-bit mixer of the weight hash (oracle/generators.c oracle_mix32), numpy."""
+    x = np.asarray(x, dtype=np.uint32).copy()
+    x ^= x >> np.uint32(16)
+    x *= np.uint32(0x7FEB352D)
+    x ^= x >> np.uint32(15)
+    x *= np.uint32(0x846CA68B)
+    x ^= x >> np.uint32(16)
+    return x
+
+
+def rmat_pairs_c(scale, edgefactor, seed):
+    """Raw R-MAT tuples (uu[t], vv[t]) after the vertex permutation (oracle/generators.c)."""
+    T = edgefactor << scale
+    uu = np.empty(max(T, 1), np.uint32)
+    vv = np.empty(max(T, 1), np.uint32)
+    rc = lib().oracle_rmat_pairs(scale, edgefactor, seed, _p(uu, ctypes.c_uint32), _p(vv, ctypes.c_uint32))
+    if rc != 0:
+        raise ValueError("oracle_rmat_pairs failed")
+    return uu[:T], vv[:T]
+
+
+def hash_weights(m, wseed):
+    w = np.empty(max(m, 1), np.uint32)
+    lib().oracle_hash_weights(m, wseed, _p(w, ctypes.c_uint32))
+    return w[:m]
+
+
+def rmat_canonical(scale, edgefactor=16, seed=1, wseed=2):
+    """The canonical R-MAT graph: tuples -> self-loops dropped, pairs deduplicated, sorted by
+    (min, max) (canonicalize_c) -> w[e] = mix32(e ^ wseed). Returns (n, u, v, w)."""
+    n = 1 << scale
+    uu, vv = rmat_pairs_c(scale, edgefactor, seed)
+    cu, cv, _ = canonicalize_c(n, uu, vv, np.zeros(len(uu), np.uint32))
+    return n, cu, cv, hash_weights(len(cu), wseed)
+
+
+def grid_canonical(k, mode=0, wseed=2):
+    """k x k grid, vertex r*k + c, right and down edges in canonical order (for each vertex x: its
+    right edge (x, x+1), then its down edge (x, x+k)); w = eid (mode 1, "road-like" gradient) or
+    mix32(eid ^ wseed). Returns (n, u, v, w)."""
+    n = k * k
+    x = np.arange(n, dtype=np.int64)
+    r, c = x // k, x % k
+    right = np.stack([x, x + 1], 1)[c < k - 1]
+    down = np.stack([x, x + k], 1)[r < k - 1]
+    e = np.concatenate([right, down])
+    order = np.lexsort((e[:, 1], e[:, 0]))
+    e = e[order]
+    m = len(e)
+    eid = np.arange(m, dtype=np.uint32)
+    w = eid.copy() if mode else mix32_np(eid ^ np.uint32(wseed & 0xFFFFFFFF))
+    return n, e[:, 0].astype(np.uint32), e[:, 1].astype(np.uint32), w

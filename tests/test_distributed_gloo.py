@@ -1,7 +1,10 @@
 """The multi-rank orchestration (distributed.run_rounds + edge_range partition + all-reduce
 MIN) on CPU with the gloo backend, world_size 2 and 3, with one and with several weight levels.
 The per-rank compute is the oracle's numpy stepper (oracle/boruvka_steps.py) standing in for the
-HIP stepper; the result must equal canonical Kruskal on every rank."""
+HIP stepper, including the owner-computes CONNECT exchange of a level's first round (hook_local,
+int32 MAX all-reduce, unpack_hook: distributed.run_rounds drives it exactly as for HipStepper).
+The totals must equal canonical Kruskal on every rank and the OR of the ranks' MSF flags must
+equal Kruskal's edge set (an owner-computed hook marks its edge on the owning rank only)."""
 import os
 import socket
 
@@ -20,7 +23,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, u, v, w, thr, out):
+def _worker(rank, world, port, n, u, v, w, thr, out, owner_hooks):
     import torch.distributed as dist
 
     from distributed_ghs_implementation_amd.device import edge_range
@@ -30,7 +33,7 @@ def _worker(rank, world, port, n, u, v, w, thr, out):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     lo, hi = edge_range(len(u), rank, world)
-    st = CpuStepper(n, u, v, w, lo, hi, thr)
+    st = CpuStepper(n, u, v, w, lo, hi, thr, ranks=world if owner_hooks else 1)
 
     def ar(t):
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
@@ -40,21 +43,22 @@ def _worker(rank, world, port, n, u, v, w, thr, out):
 
     rounds = run_rounds(st, ar, allreduce_max=ar_max)
     total, count = st.finish()
-    out[rank] = (st.in_mst.tolist(), total, count, rounds)
+    out[rank] = (st.in_mst.tolist(), total, count, rounds, st.hooks_exchanged)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run(world, n, u, v, w, thr):
+def _run(world, n, u, v, w, thr, owner_hooks=True):
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), n, u, v, w, thr, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), n, u, v, w, thr, out, owner_hooks), nprocs=world, join=True)
     return dict(out)
 
 
-@pytest.mark.parametrize("world,name,levels", [(2, "ties_4.json", 1), (2, "cgf_n1000_p001.json", 3),
-                                               (3, "ties_2.json", 2), (2, "ties_5.json", 3)])
-def test_gloo_ranks_match_kruskal(world, name, levels):
+@pytest.mark.parametrize("world,name,levels,owner_hooks", [(2, "ties_4.json", 1, True), (2, "cgf_n1000_p001.json", 3, True),
+                                                           (3, "ties_2.json", 2, True), (2, "ties_5.json", 3, True),
+                                                           (2, "ties_5.json", 3, False)])
+def test_gloo_ranks_match_kruskal(world, name, levels, owner_hooks):
     from oracle import oracle
     fx = load_fixture(name)
     n = fx["num_nodes"]
@@ -63,11 +67,16 @@ def test_gloo_ranks_match_kruskal(world, name, levels):
     ref_in, ref_tw, ref_k = oracle.kruskal_c(n, u, v, w)
     qs = np.quantile(w, np.linspace(0, 1, levels + 1)[1:-1]).astype(np.int64).tolist() if levels > 1 else []
     thr = [0] + sorted(set(int(q) + 1 for q in qs)) + [1 << 32]
-    out = _run(world, n, u, v, w, thr)
+    out = _run(world, n, u, v, w, thr, owner_hooks)
     assert len(out) == world
+    flags = np.zeros(len(u), np.uint8)
     for rank in range(world):
-        in_mst, total, count, rounds = out[rank]
-        assert np.array_equal(np.array(in_mst, np.uint8), ref_in)
+        in_mst, total, count, rounds, exchanged = out[rank]
+        flags |= np.array(in_mst, np.uint8)
         assert total == ref_tw == fx["expected_total_weight"]
         assert count == ref_k
         assert rounds <= (len(thr) - 1) * (int(np.ceil(np.log2(max(n, 2)))) + 2)
+        assert (exchanged > 0) == owner_hooks  # the int32 MAX hook exchange really ran
+        if not owner_hooks:  # fragment-form hooks on every rank: each rank holds the whole MSF
+            assert np.array_equal(np.array(in_mst, np.uint8), ref_in)
+    assert np.array_equal(flags, ref_in)

@@ -1,0 +1,39 @@
+"""Real multi-process runs of the product's multi-GPU driver on the box's one GPU: 2 and 3 ranks
+(torch.distributed.run, gloo — RCCL needs one GPU per rank, the driver's 8-GPU run is not ours
+to launch), each a separate process through libghs_mst.so, checked against the oracle."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world,scale", [(2, 16), (3, 14)])
+def test_ranks_in_separate_processes_match_oracle(world, scale, tmp_path):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    out = tmp_path / "verdict.json"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "gpu_workers", "dist_ranks.py"), str(out), str(scale)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    v = json.loads(out.read_text())
+    assert v == {"world": world, "m": v["m"], "flags_match_oracle": True, "totals_match_oracle": True,
+                 "ranks_agree": True}

@@ -156,17 +156,74 @@ def test_stepwise_solver_equals_monolithic(torch_cuda):
     assert rc.total_weight == ra.total_weight and rc.rounds == ra.rounds
 
 
+def _emulate_ranks(e, world, cfg=None):
+    """`world` edge-range engines on one GPU stepping in lock step, the collectives emulated with
+    torch.maximum / torch.minimum (exactly what RCCL's MAX / MIN all-reduce compute). Returns the
+    OR of the ranks' MSF flags (an owner-computed hook marks its owner's copy only) and every
+    rank's (total weight, MSF edges)."""
+    import torch
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import DeviceMST, edge_range
+    from distributed_ghs_implementation_amd.distributed import HipStepper
+    cfg = cfg or _native.make_config(num_ranks=world)
+    engines = [DeviceMST(e, *edge_range(e.m, r, world), config=cfg) for r in range(world)]
+    assert sum(x.e_hi - x.e_lo for x in engines) == e.m
+    steppers = [HipStepper(x) for x in engines]
+    try:
+        done = False
+        while not done:
+            counts = [s.minedge() for s in steppers]
+            while counts[0] is None:  # a level opened: OR-combine the fragment flags (emulated MAX)
+                assert all(c is None for c in counts)
+                bufs = [s.exchange_buffer() for s in steppers]
+                red = bufs[0].clone()
+                for b in bufs[1:]:
+                    red = torch.maximum(red, b)
+                for b in bufs:
+                    b.copy_(red)
+                counts = [s.minedge() for s in steppers]
+            assert len(set(counts)) == 1
+            if counts[0]:
+                dense = [s.pack(counts[0]).clone() for s in steppers]
+                red = dense[0]
+                for d in dense[1:]:
+                    red = torch.minimum(red, d)
+                for s in steppers:
+                    s.unpack(red)
+                hooks = [s.hook_local() for s in steppers]  # owner-computes hook (a level's round 0)
+                assert len(set(h is None for h in hooks)) == 1
+                if hooks[0] is not None:
+                    nz = sum((h != 0).to(torch.int64) for h in hooks)
+                    assert int(nz.max().item()) <= 1  # one owner per winning edge
+                    hmax = hooks[0].clone()
+                    for h in hooks[1:]:
+                        hmax = torch.maximum(hmax, h)
+                    for s in steppers:
+                        s.unpack_hook(hmax)
+            dones = [s.contract() for s in steppers]
+            assert len(set(dones)) == 1
+            done = dones[0]
+        totals = []
+        for s in steppers:
+            res, _ = s.finish()
+            totals.append((res.total_weight, res.num_mst_edges))
+        flags = engines[0].in_mst[: e.m].clone()
+        for x in engines[1:]:
+            flags = torch.maximum(flags, x.in_mst[: e.m])
+        return flags, totals
+    finally:
+        for s in steppers:
+            s.close()
+
+
 @pytest.mark.parametrize("world,graph", [(2, "rmat"), (3, "rmat"), (8, "rmat"), (8, "grid"), (5, "grid-gradient"),
                                          (8, "readme"), (4, "ties")])
 def test_partitioned_ranks_emulated_on_one_gpu(world, graph, torch_cuda):
-    """`world` edge-range engines on one GPU, all-reduce emulated with torch.minimum: the
-    multi-GPU decomposition gives the single-GPU answer."""
-    import torch
-    from distributed_ghs_implementation_amd.device import DeviceMST, edge_range, generate_grid, generate_rmat
-    from distributed_ghs_implementation_amd.distributed import HipStepper
-    from distributed_ghs_implementation_amd import _native
+    """`world` edge-range engines on one GPU, all-reduces emulated: the OR of the ranks' flags is
+    canonical Kruskal's MSF (oracle) and every rank reports the oracle's totals."""
     from distributed_ghs_implementation_amd import canonicalize
-    from distributed_ghs_implementation_amd.device import DeviceEdges
+    from distributed_ghs_implementation_amd.device import DeviceEdges, generate_grid, generate_rmat
+    ora = _oracle()
     if graph == "rmat":
         e = generate_rmat(15, 16, seed=3, wseed=4)
     elif graph == "readme":  # 9 edges over 8 ranks: most ranks own no edge at all
@@ -179,87 +236,136 @@ def test_partitioned_ranks_emulated_on_one_gpu(world, graph, torch_cuda):
                                                w=rng.integers(0, 3, m)))
     else:
         e = generate_grid(257, 1 if graph == "grid-gradient" else 0)
-    ref = DeviceMST(e)
-    ref.run()
+    flags, totals = _emulate_ranks(e, world)
+    g = e.to_host()
+    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    assert np.array_equal(flags.cpu().numpy().astype(bool), ref_in.astype(bool))
+    assert set(totals) == {(ref_tw, ref_k)}
+
+
+def test_partitioned_noncanonical_fails_on_every_rank(torch_cuda):
+    """A non-canonical edge in ONE rank's range: every rank returns GHS_E_NONCANON from the same
+    minedge call (the error byte travels with the exchanged flags), so no rank would be left
+    waiting in a collective."""
+    import torch
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import DeviceEdges, DeviceMST, edge_range, generate_rmat
+    from distributed_ghs_implementation_amd.distributed import HipStepper
+    e = generate_rmat(12, 16, seed=1, wseed=2)
+    world = 4
+    lo, hi = edge_range(e.m, 2, world)
+    v = e.v.clone()
+    v[(lo + hi) // 2] = e.u[(lo + hi) // 2]  # u == v inside rank 2's range
+    bad = DeviceEdges(e.n, e.u, v, e.w)
     cfg = _native.make_config(num_ranks=world)
-    engines = [DeviceMST(e, *edge_range(e.m, r, world), config=cfg) for r in range(world)]
-    assert sum(x.e_hi - x.e_lo for x in engines) == e.m
-    steppers = [HipStepper(x) for x in engines]
-    done = False
-    while not done:
-        counts = [s.minedge() for s in steppers]
-        while counts[0] is None:  # a level opened: OR-combine the fragment flags (emulated MAX)
-            assert all(c is None for c in counts)
-            bufs = [s.exchange_buffer() for s in steppers]
-            red = bufs[0].clone()
-            for b in bufs[1:]:
-                red = torch.maximum(red, b)
-            for b in bufs:
-                b.copy_(red)
-            counts = [s.minedge() for s in steppers]
-        assert len(set(counts)) == 1
-        if counts[0]:
-            dense = [s.pack(counts[0]).clone() for s in steppers]
-            red = dense[0]
-            for d in dense[1:]:
-                red = torch.minimum(red, d)
-            for s in steppers:
-                s.unpack(red)
-            hooks = [s.hook_local() for s in steppers]  # owner-computes hook (a level's round 0)
-            assert len(set(h is None for h in hooks)) == 1
-            if hooks[0] is not None:
-                nz = sum((h != 0).to(torch.int64) for h in hooks)
-                assert int(nz.max().item()) <= 1  # one owner per winning edge
-                hmax = hooks[0].clone()
-                for h in hooks[1:]:
-                    hmax = torch.maximum(hmax, h)
-                for s in steppers:
-                    s.unpack_hook(hmax)
-        dones = [s.contract() for s in steppers]
-        assert len(set(dones)) == 1
-        done = dones[0]
-    totals = []
-    for s in steppers:
-        res, _ = s.finish()
-        totals.append((res.total_weight, res.num_mst_edges))
-        s.close()
-    # the MSF flags are the OR over the ranks (an owner-computed hook marks its owner's copy)
-    flags = engines[0].in_mst.clone()
-    for x in engines[1:]:
-        flags = torch.maximum(flags, x.in_mst)
-    assert np.array_equal(flags[: e.m].cpu().numpy().astype(bool), ref.in_mst_host())
-    rr, _ = ref.run()
-    assert set(totals) == {(rr.total_weight, rr.num_mst_edges)}
+    steppers = [HipStepper(DeviceMST(bad, *edge_range(e.m, r, world), config=cfg)) for r in range(world)]
+    try:
+        assert all(s.minedge() is None for s in steppers)  # level 0 opened on every rank
+        bufs = [s.exchange_buffer() for s in steppers]
+        assert all(b.numel() == e.n + 1 for b in bufs)  # n flags + the error byte
+        red = bufs[0].clone()
+        for b in bufs[1:]:
+            red = torch.maximum(red, b)
+        for b in bufs:
+            b.copy_(red)
+        for s in steppers:
+            with pytest.raises(_native.GHSError) as ei:
+                s.minedge()
+            assert ei.value.code == _native.GHS_E_NONCANON
+    finally:
+        for s in steppers:
+            s.close()
 
 
-def test_build_arcs_utility(torch_cuda):
-    """ghs_build_arcs (ingest utility): 2m arcs grouped by source, each edge once per side."""
+@pytest.fixture(scope="module")
+def rmat_s26_reference(torch_cuda):
+    """BASELINE config 4's graph (R-MAT s26, ~1.05B canonical edges) and its single-GPU MSF,
+    checked bit-exact against the independent torch Boruvka (full-size parity of config 4)."""
+    torch = torch_cuda
+    from distributed_ghs_implementation_amd.device import DeviceMST, generate_rmat
+    from torch_boruvka import msf_boruvka
+    e = generate_rmat(26, 16, seed=1, wseed=2)
+    eng = DeviceMST(e)
+    res, _ = eng.run()
+    flags = eng.in_mst[: e.m].clone()
+    del eng
+    torch.cuda.empty_cache()
+    ref = msf_boruvka(e.n, e.u, e.v, e.w)
+    assert torch.equal(flags.bool(), ref), "s26 single-GPU MSF differs from the torch Boruvka checker"
+    del ref
+    torch.cuda.empty_cache()
+    w = (e.w.to(torch.int64) & 0xFFFFFFFF)
+    assert int(flags.sum().item()) == res.num_mst_edges
+    assert int(w[flags.bool()].sum().item()) == res.total_weight
+    del w
+    yield e, flags, (res.total_weight, res.num_mst_edges)
+    del e
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_partitioned_s26_emulated(world, rmat_s26_reference, torch_cuda):
+    """BASELINE config 4 (R-MAT s26 edge-partitioned over 2/4/8 ranks, all-reduces emulated on
+    one GPU): the OR of the ranks' flags is the s26 MSF (single GPU == torch Boruvka checker)
+    and every rank reports the same totals."""
+    torch = torch_cuda
+    e, ref_flags, ref_tot = rmat_s26_reference
+    flags, totals = _emulate_ranks(e, world)
+    assert torch.equal(flags, ref_flags)
+    assert set(totals) == {ref_tot}
+    del flags
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("scale,ef,seed,wseed", [(12, 16, 1, 2), (16, 16, 1, 2), (18, 16, 3, 4), (14, 8, 9, 0)])
+def test_rmat_generator_matches_oracle(scale, ef, seed, wseed, torch_cuda):
+    """Generator parity: the raw GPU tuples equal oracle/generators.c tuple for
+    tuple, and the GPU canonical list (rocPRIM sort + unique, self-loops dropped, hashed weights)
+    equals the oracle's canonicalisation of the same tuples, bit-exact."""
+    import torch
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import _ptr, _stream, generate_rmat
+    ora = _oracle()
+    L = _native.load()
+    T = ef << scale
+    keys = torch.empty(T, dtype=torch.int64, device="cuda")
+    _native.check(L.ghs_rmat_tuples(scale, ef, seed, _ptr(keys), _stream()))
+    k = keys.cpu().numpy().view(np.uint64)
+    uu, vv = ora.rmat_pairs_c(scale, ef, seed)
+    a = np.minimum(uu, vv).astype(np.uint64)
+    b = np.maximum(uu, vv).astype(np.uint64)
+    exp = np.where(uu == vv, np.uint64((1 << (2 * scale)) - 1), (a << np.uint64(scale)) | b)
+    assert np.array_equal(k, exp)
+    g = generate_rmat(scale, ef, seed=seed, wseed=wseed).to_host()
+    n, cu, cv, cw = ora.rmat_canonical(scale, ef, seed, wseed)
+    assert g.n == n and g.m == len(cu)
+    assert np.array_equal(g.u, cu) and np.array_equal(g.v, cv) and np.array_equal(g.w, cw)
+
+
+@pytest.mark.parametrize("k,mode,wseed", [(2, 0, 2), (3, 1, 2), (257, 0, 2), (1000, 1, 2), (1024, 0, 77)])
+def test_grid_generator_matches_oracle(k, mode, wseed, torch_cuda):
+    from distributed_ghs_implementation_amd.device import generate_grid
+    ora = _oracle()
+    g = generate_grid(k, mode, wseed=wseed).to_host()
+    n, u, v, w = ora.grid_canonical(k, mode, wseed)
+    assert g.n == n and g.m == len(u) == 2 * k * (k - 1)
+    assert np.array_equal(g.u, u) and np.array_equal(g.v, v) and np.array_equal(g.w, w)
+
+
+def test_check_canonical_utility(torch_cuda):
     import ctypes
     import torch
     from distributed_ghs_implementation_amd import _native
     from distributed_ghs_implementation_amd.device import _ptr, _stream, generate_rmat
     L = _native.load()
     e = generate_rmat(12, 16, seed=1, wseed=2)
-    A = 2 * e.m
-    asrc = torch.empty(A, dtype=torch.int32, device="cuda")
-    adst = torch.empty(A, dtype=torch.int32, device="cuda")
-    akey = torch.empty(A, dtype=torch.int64, device="cuda")
-    tb = L.ghs_build_arcs_temp_bytes(e.n, e.m)
-    tmp = torch.empty(tb, dtype=torch.uint8, device="cuda")
-    _native.check(L.ghs_build_arcs(e.n, e.m, _ptr(e.u), _ptr(e.v), _ptr(e.w), _ptr(asrc), _ptr(adst), _ptr(akey),
-                                   _ptr(tmp), tb, _stream()))
-    s = asrc.cpu().numpy().view(np.uint32)
-    d = adst.cpu().numpy().view(np.uint32)
-    k = akey.cpu().numpy().view(np.uint64)
-    assert np.all(np.diff(s.astype(np.int64)) >= 0)
-    g = e.to_host()
-    eid = (k & np.uint64(0xFFFFFFFF)).astype(np.int64)
-    assert np.array_equal(np.bincount(eid, minlength=g.m), np.full(g.m, 2))
-    assert np.array_equal(np.minimum(s, d), g.u[eid]) and np.array_equal(np.maximum(s, d), g.v[eid])
-    assert np.array_equal((k >> np.uint64(32)).astype(np.uint32), g.w[eid])
     ok = ctypes.c_int(0)
     _native.check(L.ghs_check_canonical(e.n, e.m, _ptr(e.u), _ptr(e.v), _stream(), ctypes.byref(ok)))
     assert ok.value == 1
+    v = e.v.clone()
+    v[e.m // 2] = e.u[e.m // 2]  # u == v breaks u < v
+    _native.check(L.ghs_check_canonical(e.n, e.m, _ptr(e.u), _ptr(v), _stream(), ctypes.byref(ok)))
+    assert ok.value == 0
 
 
 def test_rmat_s20_oracle_and_determinism(torch_cuda):
@@ -387,3 +493,24 @@ def test_cli_graph_dir_with_check(tmp_path, torch_cuda):
     assert main(["--graph-dir", str(d), "--check", "--quiet"]) == 0
     res = json.load(open(d / "ghs_mst.json"))
     assert res["total_weight"] == 11 and res["num_edges"] == 5  # README_MPI.md:228-235
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_any_numeric_weights_through_ghsalgorithm(seed, torch_cuda):
+    """Negative / float / > 2^32 weights (nx.Graph accepts them, so the reference's GHSAlgorithm
+    does: ghs_implementation.py:417-440) go through the engine as dense ranks: the same edges as
+    canonical Kruskal on the original values, reported with the caller's weights."""
+    import random
+    from distributed_ghs_implementation_amd import GHSAlgorithm
+    ora = _oracle()
+    rng = random.Random(seed)
+    n = 2000
+    pool = [-7.5, -1, 0, 0.25, 3, 3.0000001, 1 << 40, -(1 << 35), 1e12]
+    edges = [(rng.randrange(n), rng.randrange(n), rng.choice(pool)) for _ in range(12000)]
+    ghs = GHSAlgorithm(n, edges)
+    got = ghs.run()
+    canon = ora.canonicalize_py_any(n, edges)
+    ref_in, ref_w = ora.kruskal_py(n, canon)
+    assert got == [(a, b) for (a, b, _), f in zip(canon, ref_in) if f]
+    assert ghs.mst_weight == pytest.approx(ref_w, rel=1e-12)
+    assert ghs.mst_triples() == [t for t, f in zip(canon, ref_in) if f]
