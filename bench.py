@@ -1,30 +1,28 @@
 """Benchmark: MST edges processed/sec on R-MAT (BASELINE.json metric) + % HBM roofline.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--scale S] [--workload rmat|grid]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scale S] [--workload rmat|grid|grid-gradient]
 
 A step = one full MST of the device-resident canonical edge list (BASELINE.md "Definitions"):
 validation, the weight-level plan, every level's pass and all Boruvka rounds -> in_mst flags +
-total weight.
-Inputs are generated on the GPU before the timed region (synthetic R-MAT, Graph500 parameters,
-unique hashed weights — no dataset download). N=1: R-MAT scale 24 (BASELINE config 3).
-N>1 (torch.distributed.run, one rank per GPU, RCCL all-reduce MIN per round): every rank holds
-the replicated canonical list and streams its contiguous canonical-edge range; scale
-min(26, 24 + log2 N) (config 4: s26 on 8 GPUs).
-
-Rank 0 prints ONE JSON line. `roofline` is for the dominant kernel of the step (largest
-time over the timed steps) among the instrumented ones: k_filter (canonical stream + giant-bitmap
-filter + level-1 split; 12 B per canonical edge read + 16 B per entry written), k_select
-(validation + level-0 split; same accounting) and the compacting min-edge kernel (24 B per live
-edge + 16 B per survivor). Durations are HIP events recorded by libghs_mst.so on the launch
-stream: k_filter / k_select inside the timed steps, the min-edge launches in one extra
-instrumented step after them (GHS_TIME_ROUNDS=1; per-round events would add idle time to the
-timed steps); all three are listed under "kernels". `traffic` comes from the
-committed PMC profile (profiles/**/<workload>_pmc.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes,
-gfx950-corrected, tools/gpu/pmc_traffic.sh) when one exists for this workload, else null.
-CPU baselines on bounded samples (same generator, smaller scale), rank 0 at N=1 only:
-`cpu_baseline` = the all-cores OpenMP Borůvka (oracle/boruvka_omp.c, kind "port",
-OMP_NUM_THREADS threads) on R-MAT s23; `cpu_baseline_serial` = the oracle's C Kruskal (1 thread)
-on R-MAT s21; `cpu_baseline_networkx` = NetworkX Kruskal (the reference's verifier) on R-MAT s16.
+total weight. Inputs are generated on the GPU before the timed region (synthetic R-MAT, Graph500
+parameters, unique hashed weights — no dataset download).
+  N = 1: R-MAT scale 24 (BASELINE config 3), the headline `value`; the line also carries
+         `scaling_base`: R-MAT scale 26 (config 4's graph) solved on this one GPU.
+  N > 1 (torch.distributed.run, one rank per GPU, RCCL): strong scaling on R-MAT scale 26 —
+         every N solves the same graph, so scaling_base and the N > 1 lines form one curve.
+Rank 0 prints ONE JSON line. After the timed steps one extra step runs with every kernel launch
+bracketed by HIP events on the solve's stream (libghs_mst.so ghs_profile_enable): `kernels` lists
+every kernel's time per step and achieved GB/s under its algorithmic byte model (launch_bytes),
+`roofline` is the dominant kernel's (largest time in that step; k_select / k_filter durations are
+the event averages inside the timed steps), `stage1_roofline` is BASELINE.md's stage-1 figure
+(24 B per live edge over every min-edge round / the min-edge kernels' time). `traffic` comes from
+the committed PMC profile (profiles/**/<workload>_pmc.json: rocprofv3 FETCH_SIZE / WRITE_SIZE
+passes, tools/gpu/pmc_traffic.sh) when one exists, else null.
+CPU baselines, rank 0 at N=1 only: `cpu_baseline` = the all-cores OpenMP Borůvka
+(oracle/boruvka_omp.c, kind "port") on the workload's own graph with every CPU the process may
+use (affinity / cgroup quota / OMP_NUM_THREADS, reported under host_cpus); `cpu_baseline_serial`
+= the oracle's C Kruskal (1 thread) on R-MAT s22; `cpu_baseline_networkx` = NetworkX Kruskal (the
+reference's verifier) on R-MAT s16.
 """
 import argparse
 import glob
@@ -50,82 +48,154 @@ def parse():
     ap.add_argument("--edgefactor", type=int, default=16)
     ap.add_argument("--workload", choices=["rmat", "grid", "grid-gradient"], default="rmat")
     ap.add_argument("--grid-k", type=int, default=16384)
-    ap.add_argument("--cpu-scale", type=int, default=21, help="R-MAT scale of the CPU-baseline sample")
+    ap.add_argument("--cpu-scale", type=int, default=22, help="R-MAT scale of the serial-Kruskal sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--omp-scale", type=int, default=23, help="R-MAT scale of the OpenMP Boruvka baseline sample")
     ap.add_argument("--nx-scale", type=int, default=16, help="R-MAT scale of the NetworkX baseline sample")
     ap.add_argument("--verify", action="store_true", help="check the result against the oracle (slow at s24)")
     ap.add_argument("--stats", action="store_true", help="print per-round stats to stderr")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse ranks sharing a GPU)")
     ap.add_argument("--verify-ranks", action="store_true", help="N>1: check every rank holds the same MSF")
+    ap.add_argument("--no-scaling-base", action="store_true", help="N=1: skip the s26 strong-scaling point")
     return ap.parse_args()
 
 
-def minedge_roofline(all_stats):
-    """The compacting min-edge kernel (rounds >= 2 of a level; SURVEY.md 8(d) stage 1): 24 B per
-    live edge read (a 4 + b 4 + key 8 + lab[a] 4 + lab[b] 4) + 16 B per surviving edge written.
-    Returns (achieved GB/s, bytes per launch, avg ms per launch, launches) or None."""
-    tot_bytes = 0.0
-    tot_ms = 0.0
-    launches = 0
-    for stats in all_stats:
-        for r, st in enumerate(stats):
-            first_of_level = r == 0 or stats[r - 1]["level"] != st["level"]
-            if first_of_level or st["live_arcs"] == 0 or st["ms_minedge"] <= 0:
-                continue
-            nxt = stats[r + 1] if r + 1 < len(stats) else None
-            survivors = nxt["live_arcs"] if nxt is not None and nxt["level"] == st["level"] else 0
-            tot_bytes += 24.0 * st["live_arcs"] + 16.0 * survivors
-            tot_ms += st["ms_minedge"]
-            launches += 1
-    if launches == 0 or tot_ms <= 0:
-        return None
-    return tot_bytes / (tot_ms * 1e-3) / 1e9, tot_bytes / launches, tot_ms / launches, launches
+# Algorithmic bytes per launch of every profiled kernel (DESIGN.md "Kernels"): what the
+# algorithm must move, counting a random gather as its element size. `rec` is one profiled launch
+# (round / level / host-known items), `st` the solve's round stats, `res` its Result.
+def _round_of(rec, stats):
+    """The stats entry of a launch's round, or None for a lookahead no-op round (a level's
+    trailing rounds reuse the next level's round index with their own, older level)."""
+    r = rec["round"]
+    if r < len(stats) and stats[r]["level"] == rec["level"]:
+        return r
+    return None
 
 
-def pass_roofline(results, which):
-    """A canonical pass (one launch per step): 12 B per canonical edge streamed (u, v, w) + 16 B
-    per entry written. k_filter's bitmap probes hit the L2-resident bitmap and are not HBM bytes.
-    Returns (achieved GB/s, bytes per launch, avg ms per launch, launches) or None."""
-    ms = [getattr(r, "ms_" + which) for r in results]
-    out = [getattr(r, which + "_out") for r in results]
-    if not ms or min(ms) <= 0:
+def _next_live(stats, r):
+    return stats[r + 1]["live_arcs"] if r + 1 < len(stats) and stats[r + 1]["level"] == stats[r]["level"] else 0
+
+
+def _first_round(stats, r):
+    return r == 0 or stats[r - 1]["level"] != stats[r]["level"]
+
+
+def launch_bytes(rec, stats, res, n):
+    k = rec["kernel"]
+    if k == "k_select":
+        return 12.0 * res.canon_edges + 16.0 * res.select_out  # u, v, w stream + level-0 edges out
+    if k == "k_filter":
+        return 12.0 * res.canon_edges + 16.0 * res.filter_out  # stream + level-1 and pending edges out
+    if k == "k_resolve":
+        return 8.0 * n + n / 8.0  # lab read + write, giant bitmap
+    if k == "k_jump_ident":
+        return 17.0 * n  # lab 4 + par 4 + best 8 + keep flag 1 per vertex
+    r = _round_of(rec, stats)
+    if r is None:
+        return 0.0
+    st = stats[r]
+    live, act = st["live_arcs"], st["active_components"]
+    if k == "k_level_pass":
+        return 16.0 * rec["items"] + 16.0 * st["level_arcs"]  # pending in (+ level edges out)
+    if k == "k_seed_runs":
+        return 12.0 * live  # a 4 + key 8
+    if k == "k_minedge<IDENT>":
+        return 16.0 * live  # a 4 + b 4 + key 8 (roots: no gathers)
+    if k == "k_minedge<COMPACT>":
+        return 24.0 * live + 16.0 * _next_live(stats, r)  # + lab[a], lab[b]; survivors out
+    if k == "k_win":
+        e = live if _first_round(stats, r) else _next_live(stats, r)
+        return 32.0 * e  # a, b, key + best[a], best[b]
+    if k == "k_hook":
+        return 40.0 * act  # act, best, eu/ev, lab x2, best[other], par
+    if k == "k_jump":
+        return 21.0 * act  # act, par, lab, best, keep flag
+    if k == "k_select_lb":
+        return 2.0 * rec["items"]  # keep bytes, two passes
+    return 0.0
+
+
+STAGE1 = ("k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>")
+
+
+def kernel_table(records, stats, res, n):
+    """Per kernel: launches, ms per step, algorithmic bytes, achieved GB/s (one profiled step)."""
+    tab = {}
+    for rec in records:
+        t = tab.setdefault(rec["kernel"], {"launches": 0, "ms": 0.0, "bytes": 0.0})
+        t["launches"] += 1
+        t["ms"] += max(rec["ms"], 0.0)
+        t["bytes"] += launch_bytes(rec, stats, res, n)
+    for t in tab.values():
+        t["achieved_gbs"] = t["bytes"] / (t["ms"] * 1e-3) / 1e9 if t["ms"] > 0 and t["bytes"] > 0 else None
+        t["ms"] = round(t["ms"], 4)
+    return tab
+
+
+def stage1_roofline(records, stats):
+    """BASELINE.md's stage-1 roofline: 24 B x sum over rounds of the live edges / sum of the
+    min-edge time (round 0's IDENT launch + its a-side seeding, and the compacting launches)."""
+    live = sum(st["live_arcs"] for st in stats)
+    ms = sum(max(r["ms"], 0.0) for r in records if r["kernel"] in STAGE1 and _round_of(r, stats) is not None)
+    if ms <= 0 or live == 0:
         return None
-    bpl = 12.0 * results[0].canon_edges + 16.0 * out[0]
-    avg = sum(ms) / len(ms)
-    return bpl / (avg * 1e-3) / 1e9, bpl, avg, len(ms)
+    ach = 24.0 * live / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "live_edges": int(live), "ms": round(ms, 4),
+            "kernels": list(STAGE1),
+            "definition": "24 B x sum of live edges over every min-edge round / sum of stage-1 time (BASELINE.md)"}
+
+
+PMC_NAMES = {"k_minedge<IDENT>": "k_minedge<true, false>", "k_minedge<COMPACT>": "k_minedge<false, true>"}
 
 
 def load_traffic(workload_tag, kernel):
-    """Per-launch HBM bytes of `kernel` from a committed PMC profile (profiles/**/*_pmc.json)."""
+    """Per-launch HBM bytes of `kernel` from a committed PMC profile (profiles/**/*_pmc.json,
+    the newest round's wins)."""
     best = None
+    name = PMC_NAMES.get(kernel, kernel)
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*_pmc.json"), recursive=True)):
         try:
             d = json.load(open(p))
         except Exception:
             continue
-        k = d.get("kernels", {}).get(kernel)
+        k = d.get("kernels", {}).get(name)
         if d.get("workload") == workload_tag and k and k.get("traffic_bytes_per_launch"):
             best = dict(k, _path=os.path.relpath(p, ROOT))
     return best
 
 
-def roofline_obj(roof, kernel, tag, note):
-    ach, bpl, msl, launches = roof
+def roofline_obj(kernel, t, tag, note):
     traffic = load_traffic(tag, kernel)
+    ach = t["achieved_gbs"] or 0.0
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4),
             "traffic": (round(traffic["traffic_bytes_per_launch"]) if traffic else None),
-            "kernel": kernel, "note": note, "algorithmic_bytes_per_launch": round(bpl),
-            "avg_launch_ms": round(msl, 4), "launches": launches,
+            "kernel": kernel, "note": note, "algorithmic_bytes_per_launch": round(t["bytes"] / t["launches"]),
+            "avg_launch_ms": round(t["ms"] / t["launches"], 4), "launches": t["launches"],
+            "ms_per_step": t["ms"], "timing": t.get("timing", "HIP events around every launch of one profiled step"),
             "traffic_source": traffic["_path"] if traffic else None}
 
 
-def cpu_baseline(scale, edgefactor):
-    """Oracle C Kruskal (1 thread) on R-MAT(scale) generated by the same GPU generator."""
-    import numpy as np  # noqa: F401
+def host_cpus():
+    """CPUs this process may use: os.cpu_count() (the whole machine), the affinity mask, and the
+    cgroup CPU quota (the GPU box grants a share of a large host)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except Exception:
+        pass
+    usable = min(aff, quota) if quota else aff
+    omp = int(os.environ.get("OMP_NUM_THREADS") or 0)
+    return {"os_cpu_count": os.cpu_count(), "affinity": aff, "cgroup_quota": quota, "usable": usable,
+            "omp_num_threads": omp or None}
 
+
+def cpu_baseline_serial(scale, edgefactor):
+    """Oracle C Kruskal (1 thread) on R-MAT(scale) generated by the same GPU generator."""
     from distributed_ghs_implementation_amd.device import generate_rmat
     from oracle import oracle
     e = generate_rmat(scale, edgefactor, seed=1, wseed=2)
@@ -137,35 +207,28 @@ def cpu_baseline(scale, edgefactor):
     dt = time.perf_counter() - t0
     return {"value": g.m / dt, "unit": "edges/s", "cores": 1, "kind": "port",
             "sample": f"R-MAT scale {scale} edgefactor {edgefactor} (same generator/seeds as the GPU workload, "
-                      f"{g.m} canonical edges) through oracle/kruskal.c canonical Kruskal, 1 thread, "
-                      f"{dt:.2f} s; host os.cpu_count()={os.cpu_count()}",
+                      f"{g.m} canonical edges) through oracle/kruskal.c canonical Kruskal, 1 thread, {dt:.2f} s",
             "seconds": dt}
 
 
-def omp_baseline(scale, edgefactor, threads=None):
-    """The all-cores CPU baseline: oracle/boruvka_omp.c, an OpenMP Borůvka
-    over the canonical list (same canonical MSF, parity in tests/test_oracle.py), on R-MAT(scale)
-    from the same generator. threads: OMP_NUM_THREADS (16 on the GPU box), else the process's
-    CPUs capped at 16. Its weight/edge count is checked against one GPU solve of the same graph."""
-    from distributed_ghs_implementation_amd.device import DeviceMST, generate_rmat
+def cpu_baseline_omp(g, gpu_result, tag):
+    """The all-cores CPU baseline: oracle/boruvka_omp.c, an OpenMP Boruvka over
+    the canonical list (same canonical MSF, parity in tests/test_oracle.py), on the GPU
+    workload's own graph `g` (host copy), with every CPU this process may use (affinity and
+    cgroup quota; OMP_NUM_THREADS when the box sets it). Checked against the GPU solve."""
     from oracle import oracle
-    if threads is None:
-        threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, len(os.sched_getaffinity(0)))
-    e = generate_rmat(scale, edgefactor, seed=1, wseed=2)
-    gres, _ = DeviceMST(e).run()
-    g = e.to_host()
-    del e
+    cpus = host_cpus()
+    threads = cpus["omp_num_threads"] or cpus["usable"]
     oracle.boruvka_omp_c(min(g.n, 1024), g.u[:0], g.v[:0], g.w[:0], threads=threads)  # load outside the timing
     t0 = time.perf_counter()
     _, tw, k, rounds = oracle.boruvka_omp_c(g.n, g.u, g.v, g.w, threads=threads)
     dt = time.perf_counter() - t0
-    ok = (tw, k) == (gres.total_weight, gres.num_mst_edges)
+    ok = (tw, k) == (gpu_result.total_weight, gpu_result.num_mst_edges)
     return {"value": g.m / dt, "unit": "edges/s", "cores": threads, "kind": "port",
-            "sample": f"R-MAT scale {scale} edgefactor {edgefactor} ({g.m} canonical edges) through "
-                      f"oracle/boruvka_omp.c OpenMP Boruvka, {threads} threads, {rounds} rounds, {dt:.2f} s; "
-                      f"weight/edges {'==' if ok else '!='} the GPU solve of the same graph; "
-                      f"host os.cpu_count()={os.cpu_count()}",
-            "seconds": dt, "matches_gpu": ok}
+            "sample": f"the GPU workload itself ({tag}, {g.m} canonical edges) through oracle/boruvka_omp.c "
+                      f"OpenMP Boruvka, {threads} threads, {rounds} rounds, {dt:.2f} s; weight/edges "
+                      f"{'==' if ok else '!='} the GPU solve",
+            "seconds": dt, "matches_gpu": ok, "host_cpus": cpus}
 
 
 def end_to_end(edges, gen_s, dev_result):
@@ -181,9 +244,10 @@ def end_to_end(edges, gen_s, dev_result):
     dt = time.perf_counter() - t0
     return {"generation_ms": round(gen_s * 1e3, 1),
             "host_path_ms": round(dt * 1e3, 2), "host_path_edges_per_s": round(g.m / dt, 1),
-            "host_path_matches_device": (r.total_weight, r.num_edges) == (dev_result[0], dev_result[1]),
+            "host_path_matches_device": (r.total_weight, r.num_edges) == (dev_result.total_weight,
+                                                                          dev_result.num_mst_edges),
             "note": "ghs_mst_host from pageable numpy arrays (H2D 12 B/edge, solve, D2H m flags); "
-                    "generation = GPU R-MAT/grid + canonical radix sort + dedupe, once per graph"}
+                    "generation = GPU R-MAT/grid + canonical radix sort + dedupe, once per graph"}, g
 
 
 def networkx_baseline(scale, edgefactor):
@@ -215,6 +279,57 @@ def networkx_baseline(scale, edgefactor):
             "seconds": dt, "weight_matches_oracle": tw == ref_tw}
 
 
+def make_workload(args, world):
+    from distributed_ghs_implementation_amd.device import generate_grid, generate_rmat
+    if args.workload == "rmat":
+        # N = 1: the s24 headline (BASELINE config 3); N > 1: strong scaling on s26 (config 4)
+        scale = args.scale if args.scale is not None else (24 if world == 1 else 26)
+        edges = generate_rmat(scale, args.edgefactor, seed=1, wseed=2)
+        tag = f"rmat-s{scale}-ef{args.edgefactor}"
+        cfg = {"workload": tag, "generator": "R-MAT A,B,C,D=.57,.19,.19,.05, seeds 1/2, self-loops dropped, "
+               "deduplicated, unique hashed u32 weights", "scale": scale, "edgefactor": args.edgefactor}
+    else:
+        k = args.grid_k
+        edges = generate_grid(k, 1 if args.workload == "grid-gradient" else 0)
+        tag = f"{args.workload}-{k}x{k}"
+        cfg = {"workload": tag, "grid_k": k}
+    return edges, tag, cfg
+
+
+def time_steps(step, steps, warmup, world, dist):
+    import torch
+    for _ in range(warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = [step() for _ in range(steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt, out
+
+
+def profile_step(step, n):
+    """One extra, untimed step with every launch bracketed by HIP events (libghs_mst.so
+    ghs_profile_enable): per-kernel durations, the dominant kernel, the stage-1 roofline."""
+    from distributed_ghs_implementation_amd import _native
+    _native.profile_enable(True)
+    try:
+        res, stats = step()
+        recs = _native.profile_read()
+    finally:
+        _native.profile_enable(False)
+    stats = list(stats)
+    return kernel_table(recs, stats, res, n), stage1_roofline(recs, stats), recs
+
+
 def main():
     args = parse()
     import torch
@@ -231,62 +346,27 @@ def main():
     if world > 1:
         dist.init_process_group(args.backend)
 
-    from distributed_ghs_implementation_amd.device import DeviceMST, generate_grid, generate_rmat
+    from distributed_ghs_implementation_amd.device import DeviceMST
     from distributed_ghs_implementation_amd.distributed import DistributedMST
 
     t_gen = time.perf_counter()
-    if args.workload == "rmat":
-        scale = args.scale if args.scale is not None else min(26, 24 + int(round(math.log2(max(world, 1)))))
-        edges = generate_rmat(scale, args.edgefactor, seed=1, wseed=2)
-        tag = f"rmat-s{scale}-ef{args.edgefactor}"
-        cfg = {"workload": tag, "generator": "R-MAT A,B,C,D=.57,.19,.19,.05, seeds 1/2, self-loops dropped, "
-               "deduplicated, unique hashed u32 weights", "scale": scale, "edgefactor": args.edgefactor}
-    else:
-        k = args.grid_k
-        edges = generate_grid(k, 1 if args.workload == "grid-gradient" else 0)
-        tag = f"{args.workload}-{k}x{k}"
-        cfg = {"workload": tag, "grid_k": k}
+    edges, tag, cfg = make_workload(args, world)
     torch.cuda.synchronize()
     gen_s = time.perf_counter() - t_gen
     n, m = edges.n, edges.m
     cfg.update({"n": n, "m": m, "partition": f"canonical edge ranges x{world}", "parallelism": f"edges{world}"})
 
-    if world > 1:
-        eng = DistributedMST(edges, rank, world)
-        step = eng.run
-    else:
-        eng = DeviceMST(edges)
-        step = eng.run
-
-    for _ in range(args.warmup):
-        step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    all_stats = []
-    results = []
-    raw_results = []
-    for _ in range(args.steps):
-        res, stats = step()
-        all_stats.append(stats)
-        results.append((res.total_weight, res.num_mst_edges, res.rounds, res.ms_total, res.levels))
-        raw_results.append(res)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    if len(set((r[0], r[1]) for r in results)) != 1:
+    eng = DistributedMST(edges, rank, world) if world > 1 else DeviceMST(edges)
+    step = eng.run
+    dt, outs = time_steps(step, args.steps, args.warmup, world, dist)
+    results = [r for r, _ in outs]
+    if len(set((r.total_weight, r.num_mst_edges) for r in results)) != 1:
         raise RuntimeError("non-deterministic MST across steps")
     if world > 1 and args.verify_ranks:
         # every rank must hold the same MSF: (weight, edges, checksum of the chosen eids)
         flags = eng.gather_in_mst()
         chk = int((torch.nonzero(flags).flatten().to(torch.int64) % 1000003).sum().item())
-        mine = torch.tensor([results[-1][0], results[-1][1], chk], dtype=torch.int64)
+        mine = torch.tensor([results[-1].total_weight, results[-1].num_mst_edges, chk], dtype=torch.int64)
         if args.backend == "nccl":
             mine = mine.cuda()
         allv = [torch.zeros_like(mine) for _ in range(world)]
@@ -294,59 +374,75 @@ def main():
         if any(not torch.equal(a.cpu(), allv[0].cpu()) for a in allv):
             raise RuntimeError(f"ranks disagree on the MSF: {[a.tolist() for a in allv]}")
         if rank == 0:
-            print(f"ranks agree: weight {results[-1][0]} edges {results[-1][1]} eid checksum {chk}", file=sys.stderr)
+            print(f"ranks agree: weight {results[-1].total_weight} edges {results[-1].num_mst_edges} eid checksum {chk}",
+                  file=sys.stderr)
 
-    # one more, untimed step with the compacting min-edge launches bracketed by HIP events
-    # (GHS_TIME_ROUNDS: ~5.7 us of idle per event, so the timed steps above carry none)
-    os.environ["GHS_TIME_ROUNDS"] = "1"
-    try:
-        _, inst_stats = step()
-    finally:
-        os.environ.pop("GHS_TIME_ROUNDS", None)
-    roof_me = minedge_roofline([inst_stats])
-    roof_f = pass_roofline(raw_results, "filter")
-    roof_s = pass_roofline(raw_results, "select")
+    ktab, s1, _ = profile_step(step, n)
+    # the canonical passes are also timed inside the timed steps (two events per pass, no idle
+    # between dependent kernels of note): prefer those averages for k_select / k_filter
+    for name, attr in (("k_select", "ms_select"), ("k_filter", "ms_filter")):
+        ms = [getattr(r, attr) for r in results]
+        if name in ktab and ms and min(ms) > 0:
+            t = ktab[name]
+            t["ms"] = round(sum(ms) / len(ms) * t["launches"], 4)
+            t["achieved_gbs"] = t["bytes"] / (t["ms"] * 1e-3) / 1e9
+            t["timing"] = "HIP events around the launch inside the timed steps (average)"
     line = None
     if rank == 0:
         ms_per_step = dt * 1e3 / args.steps
         value = m * args.steps / dt
-        kernels = {}
-        if roof_f:
-            kernels["k_filter"] = roofline_obj(
-                roof_f, "k_filter", tag, "dominant kernel of the step: canonical stream (12 B/edge) + giant-bitmap "
-                "probe per heavy edge (L2-request bound, DESIGN.md) + level-1/pending writes (16 B/entry)")
-        if roof_s:
-            kernels["k_select"] = roofline_obj(roof_s, "k_select", tag,
-                                               "canonical stream + validation + level-0 split")
-        if roof_me:
-            kernels["k_minedge"] = roofline_obj(
-                roof_me, "k_minedge<false, true>", tag, "min-edge with relabel + compaction, rounds >= 2 "
-                "(SURVEY 8(d) stage 1: 24 B per live edge + 16 B per survivor)")
-        # the roofline object is the dominant kernel's (largest time per step)
-        dom = max(kernels.values(), key=lambda k: k["avg_launch_ms"] * k["launches"]) if kernels else None
-        roofline = dom
-        s0 = all_stats[-1]
+        with_bytes = {k: v for k, v in ktab.items() if v["bytes"] > 0}
+        dom = max(ktab, key=lambda k: ktab[k]["ms"])
+        if dom not in with_bytes:  # report the largest kernel that has a byte model
+            dom = max(with_bytes, key=lambda k: with_bytes[k]["ms"]) if with_bytes else None
+        roofline = roofline_obj(dom, ktab[dom], tag, "dominant kernel of the step (largest time in the profiled "
+                                "step among every launch; algorithmic bytes per DESIGN.md)") if dom else None
+        s0 = outs[-1][1]
+        res0 = results[-1]
         breakdown = {
-            "rounds": results[-1][2],
-            "engine_ms_last_step": round(results[-1][3], 3),
-            "levels": results[-1][4],
-            "per_round": [{"level": s["level"], "level_arcs": s["level_arcs"], "live_arcs": s["live_arcs"],
-                           "fragments": s["active_components"], "hooks": s["hooks"],
-                           "ms_minedge": round(s["ms_minedge"], 4), "ms_hook": round(s["ms_hook"], 4),
-                           "ms_jump": round(s["ms_jump"], 4), "ms_next": round(s["ms_active"], 4)} for s in s0],
+            "rounds": res0.rounds, "engine_ms_last_step": round(res0.ms_total, 3), "levels": res0.levels,
+            "per_round": [{"level": st["level"], "level_edges": st["level_arcs"], "live_edges": st["live_arcs"],
+                           "fragments": st["active_components"], "hooks": st["hooks"]} for st in s0],
         }
-        cpu = cpu_nx = cpu_omp = e2e = None
+        kernels = {k: {"launches": v["launches"], "ms_per_step": v["ms"],
+                       "algorithmic_bytes": round(v["bytes"]),
+                       "achieved_gbs": round(v["achieved_gbs"], 1) if v["achieved_gbs"] else None,
+                       "frac": round(v["achieved_gbs"] / HBM_PEAK_GBS, 4) if v["achieved_gbs"] else None}
+                   for k, v in sorted(ktab.items(), key=lambda kv: -kv[1]["ms"])}
+        cpu = cpu_omp = cpu_nx = e2e = None
+        scaling_base = None
         if world == 1 and not args.no_cpu_baseline:
-            e2e = end_to_end(edges, gen_s, results[-1])
-            cpu = cpu_baseline(args.cpu_scale, args.edgefactor)
-            cpu_omp = omp_baseline(args.omp_scale, args.edgefactor)
+            e2e, g = end_to_end(edges, gen_s, res0)
+            cpu_omp = cpu_baseline_omp(g, res0, tag)
+            del g
+            cpu = cpu_baseline_serial(args.cpu_scale, args.edgefactor)
             cpu_nx = networkx_baseline(args.nx_scale, args.edgefactor)
         line = {"metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
-                "data": "synthetic (generated on GPU)", "config": cfg, "roofline": roofline,
-                "cpu_baseline": cpu_omp, "cpu_baseline_serial": cpu, "cpu_baseline_networkx": cpu_nx, "end_to_end": e2e, "kernels": kernels, "mst": {"total_weight": results[-1][0], "edges": results[-1][1]},
-                "breakdown": breakdown}
+                "higher_is_better": True, "scaling": "strong" if world > 1 else "weak", "vs_baseline": None,
+                "dtype": "u64", "data": "synthetic (generated on GPU)", "config": cfg, "roofline": roofline,
+                "stage1_roofline": s1, "cpu_baseline": cpu_omp, "cpu_baseline_serial": cpu,
+                "cpu_baseline_networkx": cpu_nx, "end_to_end": e2e, "kernels": kernels,
+                "mst": {"total_weight": res0.total_weight, "edges": res0.num_mst_edges}, "breakdown": breakdown}
+    del eng
+    if world == 1 and args.workload == "rmat" and args.scale is None and not args.no_scaling_base:
+        # the strong-scaling reference point: config 4's graph (R-MAT s26) on this one GPU, the
+        # graph every N > 1 line of `bench.py --gpus N` solves
+        del edges
+        torch.cuda.empty_cache()
+        sargs = argparse.Namespace(**vars(args))
+        sargs.scale = 26
+        e26, tag26, _ = make_workload(sargs, 1)
+        eng26 = DeviceMST(e26)
+        dt26, outs26 = time_steps(eng26.run, max(2, args.steps // 2), 1, 1, dist)
+        steps26 = max(2, args.steps // 2)
+        if rank == 0:
+            line["scaling_base"] = {"workload": tag26, "n_gpus": 1, "m": e26.m, "steps": steps26,
+                                    "value": round(e26.m * steps26 / dt26, 1),
+                                    "ms_per_step": round(dt26 * 1e3 / steps26, 4),
+                                    "note": "bench.py --gpus N > 1 solves this graph (strong scaling); this is its N=1 point"}
+        del eng26, e26
+    if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

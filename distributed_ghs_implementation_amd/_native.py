@@ -40,6 +40,7 @@ EXPORTED_SYMBOLS = (
     "ghs_solver_contract", "ghs_solver_finish", "ghs_solver_reset", "ghs_solver_destroy",
     "ghs_solver_hook_local", "ghs_solver_unpack_hook",
     "ghs_rmat_temp_bytes", "ghs_rmat_generate", "ghs_rmat_tuples", "ghs_grid_generate",
+    "ghs_profile_enable", "ghs_profile_read", "ghs_kernel_name",
 )
 
 
@@ -110,6 +111,39 @@ class Result(ctypes.Structure):
         ("select_out", ctypes.c_uint64),
         ("filter_out", ctypes.c_uint64),
     ]
+
+
+class KernelRecord(ctypes.Structure):
+    """ghs_kernel_record_t: one profiled launch (ghs_profile_enable / ghs_profile_read)."""
+    _fields_ = [
+        ("kernel", ctypes.c_uint32),
+        ("round", ctypes.c_uint32),
+        ("level", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+        ("items", ctypes.c_uint64),
+        ("ms", ctypes.c_float),
+        ("reserved2", ctypes.c_float),
+    ]
+
+
+def profile_enable(on=True):
+    check(load().ghs_profile_enable(1 if on else 0))
+
+
+def profile_read():
+    """Drain the per-launch profile: [{"kernel": name, "round", "level", "items", "ms"}, ...]."""
+    L = load()
+    out = []
+    while True:
+        buf = (KernelRecord * 4096)()
+        c = ctypes.c_uint32(0)
+        check(L.ghs_profile_read(buf, 4096, ctypes.byref(c)))
+        for i in range(c.value):
+            r = buf[i]
+            out.append({"kernel": L.ghs_kernel_name(r.kernel).decode(), "round": r.round, "level": r.level,
+                        "items": r.items, "ms": r.ms})
+        if c.value < 4096:
+            return out
 
 
 class Config(ctypes.Structure):
@@ -183,6 +217,9 @@ def load():
             "ghs_rmat_temp_bytes": (sz, [u32, u32]),
             "ghs_rmat_generate": (i32, [u32, u32, u64, u64, vp, vp, vp, P(u64), vp, sz, vp]),
             "ghs_rmat_tuples": (i32, [u32, u32, u64, vp, vp]),
+            "ghs_profile_enable": (i32, [i32]),
+            "ghs_profile_read": (i32, [vp, u32, P(u32)]),
+            "ghs_kernel_name": (ctypes.c_char_p, [u32]),
             "ghs_grid_generate": (i32, [u32, u32, u64, vp, vp, vp, vp]),
         }
         for name, (res, args) in sigs.items():

@@ -2089,6 +2089,7 @@ struct HostRes {
   hipEvent_t pass_ev[4] = {};           // the canonical passes' events
   hipEvent_t plan_ev = nullptr;         // the weight sample has landed in h_sample
   unsigned long long seq = 0;           // round reports issued through h_slot (monotonic across solves)
+  std::vector<hipEvent_t> prof_ev;      // ghs_profile_enable: two events per launch
 };
 
 // Timing-only events: no system-scope fence when they are recorded (they are read only through
@@ -2110,6 +2111,8 @@ static int hostres_init(HostRes *r) {
 static void hostres_free(HostRes *r) {
   for (hipEvent_t e : r->ev_pool) (void)hipEventDestroy(e);
   r->ev_pool.clear();
+  for (hipEvent_t e : r->prof_ev) (void)hipEventDestroy(e);
+  r->prof_ev.clear();
   for (int i = 0; i < 4; ++i)
     if (r->pass_ev[i]) (void)hipEventDestroy(r->pass_ev[i]);
   if (r->plan_ev) (void)hipEventDestroy(r->plan_ev);
@@ -2200,7 +2203,72 @@ struct ghs_solver {
   std::chrono::steady_clock::time_point t0;
   char *ws_base = nullptr;      // the caller's workspace (carved by workspace_layout)
   bool seed_runs = true;        // level 0 round 0: a-side runs by k_seed_runs (GHS_SEED_RUNS=0: off)
+  bool prof = false;            // ghs_profile_enable: every launch bracketed by events
+  struct ProfRec {
+    ghs_kernel_record_t rec;
+    size_t ev;                  // index of its first event in res->prof_ev
+  };
+  std::vector<ProfRec> prof_recs;
 };
+
+// ---- per-launch profile (ghs_profile_enable / ghs_profile_read) ------------------------------
+// Every kernel launch of a solve bracketed by two HIP events on the solve's stream: the bench's
+// per-kernel durations (and the dominant kernel of its roofline line) come from these. The
+// events add idle time between launches (~5.7 us each), so the bench times its steps without
+// them and profiles one extra step.
+static std::mutex g_prof_mutex;
+static bool g_prof_on = false;
+static std::vector<ghs_kernel_record_t> g_prof;
+
+static const char *const KERNEL_NAMES[GHS_K_COUNT] = {
+    "k_select", "k_filter", "k_level_pass", "k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>",
+    "k_win", "k_hook", "k_jump_ident", "k_jump", "k_select_lb", "k_resolve", "k_giant", "k_scan_counts",
+    "k_plan", "k_init", "k_pack", "k_unpack", "k_round_report"};
+
+struct KtScope {
+  ghs_solver *s;
+  KtScope(ghs_solver *s_, uint32_t kernel, uint64_t items) : s(s_->prof ? s_ : nullptr) {
+    if (!s) return;
+    std::vector<hipEvent_t> &pool = s->res->prof_ev;
+    const size_t idx = s->prof_recs.size() * 2;
+    while (pool.size() < idx + 2) {
+      hipEvent_t ev = nullptr;
+      if (hipEventCreateWithFlags(&ev, TIMING_EVENT_FLAGS) != hipSuccess) {
+        s = nullptr;
+        return;
+      }
+      pool.push_back(ev);
+    }
+    ghs_solver::ProfRec r{};
+    r.rec.kernel = kernel;
+    r.rec.round = s->round;
+    r.rec.level = s->level;
+    r.rec.items = items;
+    r.ev = idx;
+    s->prof_recs.push_back(r);
+    (void)hipEventRecord(pool[idx], s->stream);
+  }
+  ~KtScope() {
+    if (s) (void)hipEventRecord(s->res->prof_ev[s->prof_recs.back().ev + 1], s->stream);
+  }
+};
+#define KT(kernel, items) KtScope _kt_scope(s, (kernel), (items))
+
+// after the solve: durations into the process-wide profile (one stream sync)
+static int prof_collect(ghs_solver *s) {
+  if (!s->prof || s->prof_recs.empty()) return GHS_OK;
+  GHS_HIP_CHECK(hipStreamSynchronize(s->stream));
+  std::lock_guard<std::mutex> lock(g_prof_mutex);
+  for (const auto &r : s->prof_recs) {
+    ghs_kernel_record_t rec = r.rec;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, s->res->prof_ev[r.ev], s->res->prof_ev[r.ev + 1]) != hipSuccess) ms = -1.f;
+    rec.ms = ms;
+    g_prof.push_back(rec);
+  }
+  s->prof_recs.clear();
+  return GHS_OK;
+}
 
 static std::mutex g_mutex;  // the one-shot entry points are serialised per process
 static HostRes *g_create_pool = nullptr;  // set (under g_mutex) while ghs_mst_device creates its solver
@@ -2301,7 +2369,10 @@ static int select_lb(ghs_solver *s, const uint32_t *act, const unsigned long lon
                      uint32_t *out, unsigned long long *d_total, RoundSlot *slot = nullptr, unsigned long long seq = 0) {
   if (bound == 0) {
     GHS_HIP_CHECK(hipMemsetAsync(d_total, 0, 8, s->stream));
-    if (slot) k_round_report<<<1, 1, 0, s->stream>>>(slot, seq, s->cnt, d_total, d_count);
+    if (slot) {
+      KT(GHS_K_ROUND_REPORT, 0);
+      k_round_report<<<1, 1, 0, s->stream>>>(slot, seq, s->cnt, d_total, d_count);
+    }
     GHS_HIP_CHECK(hipGetLastError());
     return GHS_OK;
   }
@@ -2310,6 +2381,7 @@ static int select_lb(ghs_solver *s, const uint32_t *act, const unsigned long lon
   const uint64_t G = (bound + per - 1) / per;
   const uint64_t nb = (bound + G * LB_GROUP - 1) / (G * LB_GROUP);
   if (nb > LB_MAX_TILES || G >= (1ull << 20)) GHS_FAIL(GHS_E_STATE, "select: bad tiling");
+  KT(GHS_K_SELECT_LB, bound);
   k_select_lb<<<(unsigned)nb, BLOCK, 0, s->stream>>>(s->flags, act, d_count, (uint32_t)G, out, d_total, s->lb_state,
                                                      next_tag(s), slot, seq, s->cnt);
   GHS_HIP_CHECK(hipGetLastError());
@@ -2345,9 +2417,12 @@ static uint32_t plan_levels_count(const ghs_solver *s) {
 static int plan_levels_enqueue(ghs_solver *s) {
   const uint32_t L = plan_levels_count(s);
   const uint32_t ns = (L > 1 && s->m > 0) ? (uint32_t)std::min<uint64_t>(NSAMPLE_W, s->m) : 0u;
-  if (ns) k_sample_weights<<<grid_for(ns, 256, 256), 256, 0, s->stream>>>(s->m, s->ew, ns, s->sample);
-  k_plan<<<1, 1024, 0, s->stream>>>(s->sample, ns, s->n, s->m, L, level1_auto(s->cfg, s->n, s->m), s->cfg.level_growth,
-                                    s->d_thr);
+  {
+    KT(GHS_K_PLAN, ns);
+    if (ns) k_sample_weights<<<grid_for(ns, 256, 256), 256, 0, s->stream>>>(s->m, s->ew, ns, s->sample);
+    k_plan<<<1, 1024, 0, s->stream>>>(s->sample, ns, s->n, s->m, L, level1_auto(s->cfg, s->n, s->m), s->cfg.level_growth,
+                                      s->d_thr);
+  }
   GHS_HIP_CHECK(hipGetLastError());
   GHS_HIP_CHECK(hipMemcpyAsync(s->h_thr, s->d_thr, (PLAN_MAX + 1) * 8, hipMemcpyDeviceToHost, s->stream));
   GHS_HIP_CHECK(hipEventRecord(s->res->plan_ev, s->stream));
@@ -2398,8 +2473,14 @@ static int open_level(ghs_solver *s, bool async_open = false) {
 
   if (!first) {
     // find the giant fragment from a sample, compress labels and build its bitmap (on device)
-    k_giant<<<1, 1024, 0, st>>>(s->n, s->lab, s->giant, s->cnt + C_ERR);
-    k_resolve<<<grid_for(s->n, BLOCK, 16384), BLOCK, 0, st>>>(s->n, s->lab, s->giant, s->bits, s->cnt + C_ERR);
+    {
+      KT(GHS_K_GIANT, 0);
+      k_giant<<<1, 1024, 0, st>>>(s->n, s->lab, s->giant, s->cnt + C_ERR);
+    }
+    {
+      KT(GHS_K_RESOLVE, s->n);
+      k_resolve<<<grid_for(s->n, BLOCK, 16384), BLOCK, 0, st>>>(s->n, s->lab, s->giant, s->bits, s->cnt + C_ERR);
+    }
     GHS_HIP_CHECK(hipGetLastError());
   }
 
@@ -2421,11 +2502,15 @@ static int open_level(ghs_solver *s, bool async_open = false) {
     G = grid_for(TC, ARCS_PER_BLOCK, s->seg_g);
     if (TC) {
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[0], st));
-      k_select<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range + 1, Y.src, Y.dst, Y.key,
-                                    Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR);
+      {
+        KT(GHS_K_SELECT, TC);
+        k_select<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range + 1, Y.src, Y.dst, Y.key,
+                                      Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR);
+      }
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[1], st));
       GHS_HIP_CHECK(hipGetLastError());
       G *= BLOCK / WAVE;  // one output segment per wave
+      KT(GHS_K_SCAN, G);
       k_scan_counts<<<1, 1024, 0, st>>>(Y.seg_count, G, Y.seg_prefix, s->cnt + C_LIVE);
     } else {
       GHS_HIP_CHECK(hipMemsetAsync(Y.seg_prefix, 0, 16, st));
@@ -2441,12 +2526,16 @@ static int open_level(ghs_solver *s, bool async_open = false) {
       G = grid_for(TC, ARCS_PER_BLOCK, s->seg_g);
       if (TC) {
         GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[2], st));
+        {
+        KT(GHS_K_FILTER, TC);
         k_filter<<<G, BLOCK, 0, st>>>(s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range, s->bits, s->giant, s->lab,
                                       Y.src, Y.dst, Y.key, Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key,
                                       RO.seg_start, RO.seg_count, mark);
+        }
         GHS_HIP_CHECK(hipGetLastError());
         GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[3], st));
         s->filter_run = true;
+        KT(GHS_K_SCAN, G);
         k_scan_counts<<<1, 1024, 0, st>>>(RO.seg_count, G, RO.seg_prefix, s->cnt + C_PENDING);
         k_scan_counts<<<1, 1024, 0, st>>>(Y.seg_count, G, Y.seg_prefix, s->cnt + C_LIVE);
       } else {
@@ -2462,10 +2551,14 @@ static int open_level(ghs_solver *s, bool async_open = false) {
       // heavier survivors -> RO regions. Fixed grid: block b owns 1/seg_g of the virtual range.
       G = s->lp_g;
       SegView in{RI.seg_start, RI.seg_prefix, s->rem_nseg};
+      {
+      KT(GHS_K_LEVEL_PASS, s->rem_total);
       k_level_pass<<<G, BLOCK, 0, st>>>(RI.src, RI.dst, RI.key, in, d_range + 1, s->lab, s->bits, s->giant, Y.src, Y.dst, Y.key,
                                         Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key, RO.seg_start, RO.seg_count,
                                         mark);
+      }
       GHS_HIP_CHECK(hipGetLastError());
+      KT(GHS_K_SCAN, G);
       k_scan_counts<<<1, 1024, 0, st>>>(RO.seg_count, G, RO.seg_prefix, s->cnt + C_PENDING);
       k_scan_counts<<<1, 1024, 0, st>>>(Y.seg_count, G, Y.seg_prefix, s->cnt + C_LIVE);
       GHS_HIP_CHECK(hipGetLastError());
@@ -2565,6 +2658,7 @@ static inline const unsigned long long *cur_act_count(ghs_solver *s) {
 
 // the pending region scan as its own launch (when no hook kernel follows to carry it)
 static void flush_scan(ghs_solver *s) {
+  KT(GHS_K_SCAN, s->cmp_g);
   k_scan_counts<<<1, 1024, 0, s->stream>>>(s->scan_buf->seg_count, s->cmp_g, s->scan_buf->seg_prefix, s->cnt + C_LIVE);
   s->scan_pending = false;
 }
@@ -2581,12 +2675,18 @@ static int enqueue_minedge(ghs_solver *s) {
       const unsigned g = s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->ident_g) : s->ident_g;
       // level 0 (labels are the vertices): a-side runs seeded first, mostly by plain stores
       const bool seed = s->level == 0 && s->seed_runs;
-      if (seed) k_seed_runs<<<g, BLOCK, 0, s->stream>>>(I.src, I.key, in, s->best);
+      const uint64_t items = s->arcs_known ? s->cur_arcs : 0;
+      if (seed) {
+        KT(GHS_K_SEED_RUNS, items);
+        k_seed_runs<<<g, BLOCK, 0, s->stream>>>(I.src, I.key, in, s->best);
+      }
+      KT(GHS_K_MINEDGE_IDENT, items);
       k_minedge<true, false><<<g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, nullptr, nullptr,
                                                          nullptr, nullptr, nullptr, !seed);
     }
   } else {
     // fixed grid: every one of the seg_g blocks writes its region's count
+    KT(GHS_K_MINEDGE_COMPACT, 0);
     k_minedge<false, true><<<s->cmp_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, O.src, O.dst,
                                                           O.key, O.seg_start, O.seg_count, true);
     // the regions' prefix scan is left to the round's hook kernel (or a scan launch before the
@@ -2623,6 +2723,7 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
     } else if (edge_form) {
       const ArcBuf &I = s->buf[s->cur];
       SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
+      KT(GHS_K_WIN, s->arcs_known ? s->cur_arcs : 0);
       k_win<<<s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->win_g) : s->win_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->best,
                                                                                    s->par, s->in_mst, s->cnt + C_WEIGHT, nullptr);
     } else if (dual) {
@@ -2630,14 +2731,19 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
       if (s->scan_pending) flush_scan(s);
       const ArcBuf &O = s->buf[s->cur ^ 1];
       SegView in{O.seg_start, O.seg_prefix, s->cmp_g};
-      k_win<<<s->win_g, BLOCK, 0, s->stream>>>(O.src, O.dst, O.key, in, s->best, s->par, s->in_mst, s->cnt + C_WEIGHT,
-                                               d_nact);
+      {
+        KT(GHS_K_WIN, 0);
+        k_win<<<s->win_g, BLOCK, 0, s->stream>>>(O.src, O.dst, O.key, in, s->best, s->par, s->in_mst, s->cnt + C_WEIGHT,
+                                                 d_nact);
+      }
       GHS_HIP_CHECK(hipGetLastError());
+      KT(GHS_K_HOOK, 0);
       k_hook<<<gh, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
                                          s->cnt + C_WEIGHT, s->cnt + C_ERR, nullptr, 0, nullptr, nullptr, false,
                                          s->cnt + C_LIVE);
     } else {
       const ArcBuf *sb = s->scan_pending ? s->scan_buf : nullptr;
+      KT(GHS_K_HOOK, 0);
       k_hook<<<gh, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
                                          s->cnt + C_WEIGHT, s->cnt + C_ERR, sb ? sb->seg_count : nullptr, s->cmp_g,
                                          sb ? sb->seg_prefix : nullptr, s->cnt + C_LIVE, s->level_round == 0, nullptr);
@@ -2646,11 +2752,14 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
     GHS_HIP_CHECK(hipGetLastError());
     if (s->detail) record(s, 2);
     // Stage 3, then the next active list (one launch each)
-    if (s->act_ident && s->cfg.num_ranks <= 1)
+    if (s->act_ident && s->cfg.num_ranks <= 1) {
+      KT(GHS_K_JUMP_IDENT, s->n);
       k_jump_ident<<<grid_for(((uint64_t)s->n + 3) / 4, BLOCK, 16384), BLOCK, 0, s->stream>>>(s->n, s->par, s->lab, s->best,
                                                                                           s->flags, s->cnt + C_ERR);
-    else
+    } else {
+      KT(GHS_K_JUMP, 0);
       k_jump<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->par, s->lab, s->best, s->flags, s->cnt + C_ERR);
+    }
     GHS_HIP_CHECK(hipGetLastError());
     if (s->detail) record(s, 3);
     if (int rc = select_lb(s, act, d_nact, bound, s->act[nb], act_count(s, nb), slot, seq)) return rc;
@@ -2794,6 +2903,26 @@ static int run_level_pipelined(ghs_solver *s) {
 extern "C" {
 
 int ghs_abi_version(void) { return GHS_MST_ABI_VERSION; }
+
+int ghs_profile_enable(int on) {
+  std::lock_guard<std::mutex> lock(g_prof_mutex);
+  g_prof_on = on != 0;
+  g_prof.clear();
+  return GHS_OK;
+}
+
+int ghs_profile_read(ghs_kernel_record_t *out, uint32_t capacity, uint32_t *count) {
+  if (!count) GHS_FAIL(GHS_E_ARG, "count is NULL");
+  std::lock_guard<std::mutex> lock(g_prof_mutex);
+  const uint32_t n = (uint32_t)std::min<size_t>(g_prof.size(), capacity);
+  if (n && !out) GHS_FAIL(GHS_E_ARG, "out is NULL");
+  for (uint32_t i = 0; i < n; ++i) out[i] = g_prof[i];
+  *count = n;
+  g_prof.erase(g_prof.begin(), g_prof.begin() + n);
+  return GHS_OK;
+}
+
+const char *ghs_kernel_name(uint32_t kernel) { return kernel < GHS_K_COUNT ? KERNEL_NAMES[kernel] : "?"; }
 const char *ghs_last_error(void) { return ghs::g_err.c_str(); }
 
 int ghs_device_count(int *count) {
@@ -2825,6 +2954,7 @@ static int solver_begin(ghs_solver *s) {
   s->h_thr = reinterpret_cast<uint64_t *>(s->res->h_sample);
   s->t0 = std::chrono::steady_clock::now();
   if (int rc = plan_levels_enqueue(s)) return rc;
+  KT(GHS_K_INIT, n);
   if (n) {
     if ((e = hipMemsetAsync(s->best, 0xff, (size_t)n * 8, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset best: ") + hipGetErrorString(e));
     k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->lab, n);
@@ -2864,6 +2994,7 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   { const char *dbg = getenv("GHS_DEBUG"); s->debug = dbg && dbg[0] == '1'; }
   { const char *det = getenv("GHS_DETAIL"); s->detail = det && det[0] == '1'; }
   { const char *tr = getenv("GHS_TIME_ROUNDS"); s->time_rounds = tr && tr[0] == '1'; }
+  { std::lock_guard<std::mutex> lock(g_prof_mutex); s->prof = g_prof_on; }
   if (const char *la = getenv("GHS_LOOKAHEAD")) {  // A/B tests: rounds in flight ahead of the check
     const long v = strtol(la, nullptr, 10);
     s->lookahead = (uint32_t)(v < 0 ? 0 : (v > 4 ? 4 : v));
@@ -2952,6 +3083,7 @@ int ghs_solver_pack_best(ghs_solver_t *s, int64_t *d_dense) {
   if (s->phase != 1) GHS_FAIL(GHS_E_STATE, "pack_best must follow minedge");
   if (s->nact) {
     const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
+    KT(GHS_K_PACK, s->nact);
     k_pack_best<<<grid_for(s->nact, 256, 16384), 256, 0, s->stream>>>(act, cur_act_count(s), s->best, d_dense);
     GHS_HIP_CHECK(hipGetLastError());
   }
@@ -2963,6 +3095,7 @@ int ghs_solver_unpack_best(ghs_solver_t *s, const int64_t *d_dense) {
   if (s->phase != 1) GHS_FAIL(GHS_E_STATE, "unpack_best must follow minedge");
   if (s->nact) {
     const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
+    KT(GHS_K_UNPACK, s->nact);
     k_unpack_best<<<grid_for(s->nact, 256, 16384), 256, 0, s->stream>>>(act, cur_act_count(s), s->best, d_dense);
     GHS_HIP_CHECK(hipGetLastError());
   }
@@ -2984,6 +3117,7 @@ int ghs_solver_hook_local(ghs_solver_t *s, int32_t *d_dense, uint64_t *count) {
     k_win<<<s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->win_g) : s->win_g, BLOCK, 0, s->stream>>>(
         I.src, I.dst, I.key, in, s->best, s->par, s->in_mst, nullptr, nullptr);
   }
+  KT(GHS_K_PACK, s->nact);
   k_pack_hook<<<grid_for(s->nact, 256, 16384), 256, 0, s->stream>>>(act, cur_act_count(s), s->par, d_dense);
   GHS_HIP_CHECK(hipGetLastError());
   *count = s->nact;
@@ -2996,6 +3130,7 @@ int ghs_solver_unpack_hook(ghs_solver_t *s, const int32_t *d_dense) {
     GHS_FAIL(GHS_E_STATE, "unpack_hook must follow hook_local");
   if (s->nact) {
     const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
+    KT(GHS_K_UNPACK, s->nact);
     k_unpack_hook<<<grid_for(s->nact, BLOCK, HOOK_G), BLOCK, 0, s->stream>>>(act, cur_act_count(s), d_dense, s->best,
                                                                             s->par, s->cnt + C_WEIGHT);
     GHS_HIP_CHECK(hipGetLastError());
@@ -3045,6 +3180,7 @@ int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *
     GHS_HIP_CHECK(hipStreamSynchronize(s->stream));
   }
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s->t0).count();
+  if (int rc = prof_collect(s)) return rc;
   const uint32_t ns = (uint32_t)std::min<size_t>(s->stats.size(), GHS_MAX_ROUND_STATS);
   for (uint32_t r = 0; r < ns; ++r) {
     float t[4] = {0, 0, 0, 0};
@@ -3088,6 +3224,7 @@ int ghs_solver_reset(ghs_solver_t *s) {
   t.debug = s->debug; t.lookahead = s->lookahead; t.seed_runs = s->seed_runs;
   { const char *det = getenv("GHS_DETAIL"); t.detail = det && det[0] == '1'; }
   { const char *tr = getenv("GHS_TIME_ROUNDS"); t.time_rounds = tr && tr[0] == '1'; }
+  { std::lock_guard<std::mutex> lock(g_prof_mutex); t.prof = g_prof_on; }
   t.seg_g = s->seg_g; t.cmp_g = s->cmp_g; t.ident_g = s->ident_g; t.win_g = s->win_g; t.lp_g = s->lp_g;
   t.ws_base = s->ws_base;
   workspace_layout(t.n, t.e_hi - t.e_lo, &t, t.ws_base);

@@ -182,6 +182,31 @@ int ghs_solver_finish(ghs_solver_t *h, ghs_result_t *result, ghs_round_stats_t *
 int ghs_solver_reset(ghs_solver_t *h);
 int ghs_solver_destroy(ghs_solver_t *h);
 
+/* ---- per-launch profile ------------------------------------------------------------------
+ * The reference measured only wall time (time.time(), ghs_implementation.py:453-464,
+ * ghs_implementation_mpi.py:920-933). With profiling on, every kernel launch of later solves is
+ * bracketed by two HIP events on the solve's stream and its duration lands in a process-wide
+ * list (read and drained by ghs_profile_read). The events idle the GPU ~6 us each between
+ * launches: profile a separate solve, not the timed ones. */
+enum ghs_kernel_id {
+  GHS_K_SELECT = 0, GHS_K_FILTER, GHS_K_LEVEL_PASS, GHS_K_SEED_RUNS, GHS_K_MINEDGE_IDENT, GHS_K_MINEDGE_COMPACT,
+  GHS_K_WIN, GHS_K_HOOK, GHS_K_JUMP_IDENT, GHS_K_JUMP, GHS_K_SELECT_LB, GHS_K_RESOLVE, GHS_K_GIANT, GHS_K_SCAN,
+  GHS_K_PLAN, GHS_K_INIT, GHS_K_PACK, GHS_K_UNPACK, GHS_K_ROUND_REPORT, GHS_K_COUNT
+};
+typedef struct ghs_kernel_record {
+  uint32_t kernel;  /* ghs_kernel_id */
+  uint32_t round;   /* round index (all levels) when launched; a lookahead no-op round past a
+                       level's end reuses the next level's index with its own (older) level */
+  uint32_t level;   /* weight level when launched */
+  uint32_t reserved;
+  uint64_t items;   /* host-known work count at launch (edges / vertices / fragments), 0 = unknown */
+  float ms;         /* event-to-event duration */
+  float reserved2;
+} ghs_kernel_record_t;
+int ghs_profile_enable(int on);  /* also clears the list */
+int ghs_profile_read(ghs_kernel_record_t *out, uint32_t capacity, uint32_t *count);
+const char *ghs_kernel_name(uint32_t kernel);
+
 /* ---- synthetic graph generators (device; BASELINE.json configs 3-5) ----------------------
  * R-MAT (Graph500 A,B,C,D = .57,.19,.19,.05, edgefactor ef, 2^scale vertices, seeded vertex
  * permutation), self-loops dropped, duplicates removed, canonical order, unique weights
