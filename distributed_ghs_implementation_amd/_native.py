@@ -119,7 +119,7 @@ class KernelRecord(ctypes.Structure):
         ("kernel", ctypes.c_uint32),
         ("round", ctypes.c_uint32),
         ("level", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("solver", ctypes.c_uint32),
         ("items", ctypes.c_uint64),
         ("ms", ctypes.c_float),
         ("reserved2", ctypes.c_float),
@@ -141,7 +141,7 @@ def profile_read():
         for i in range(c.value):
             r = buf[i]
             out.append({"kernel": L.ghs_kernel_name(r.kernel).decode(), "round": r.round, "level": r.level,
-                        "items": r.items, "ms": r.ms})
+                        "solver": r.solver, "items": r.items, "ms": r.ms})
         if c.value < 4096:
             return out
 

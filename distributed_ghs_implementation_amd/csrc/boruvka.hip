@@ -455,14 +455,19 @@ GHS_STREAM_KERNEL_6 void k_minedge(const uint32_t *__restrict__ src, const uint3
                                  const uint64_t *__restrict__ key, SegView in, const uint32_t *__restrict__ lab,
                                  uint64_t *__restrict__ best, uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
                                  uint64_t *__restrict__ okey, uint64_t *__restrict__ oseg_start,
-                                 uint64_t *__restrict__ oseg_count, bool aside) {
+                                 uint64_t *__restrict__ oseg_count, bool aside,
+                                 const unsigned long long *__restrict__ guard_nact) {
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
   __shared__ uint32_t s_seg[2];
   __shared__ uint32_t s_hl[HOT_SLOTS];
   __shared__ unsigned long long s_hk[HOT_SLOTS];
   __shared__ WaveStage s_stage[COMPACT ? BLOCK / WAVE : 1];
   const int lane = threadIdx.x & (WAVE - 1);
-  const uint64_t T = in.prefix[in.nseg];
+  // a pipelined single-rank level runs one round ahead of the host's termination check: a round
+  // that starts with <= 1 active fragment is such a discarded lookahead round (the level is
+  // complete) — its blocks write empty regions instead of streaming every remaining edge
+  const bool noop = COMPACT && guard_nact && *guard_nact <= 1;
+  const uint64_t T = noop ? 0 : in.prefix[in.nseg];
   hot_init(s_hl, s_hk);
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;  // multiple of 4
   const uint64_t vb = Q * blockIdx.x;
@@ -1986,8 +1991,12 @@ __global__ __launch_bounds__(BLOCK) void k_select_lb(const uint8_t *__restrict__
   const uint32_t t = blockIdx.x;
   const uint64_t count = *d_count;
   const uint64_t tb = (uint64_t)t * groups * LB_GROUP;  // first item of the tile
+  // groups holding items below the count (block-uniform): a lookahead round's select over an
+  // upper-bound grid finds few or no items and skips the rest of its tile
+  const uint32_t live_groups =
+      tb >= count ? 0u : (uint32_t)umin64((uint64_t)groups, (count - tb + LB_GROUP - 1) / LB_GROUP);
   uint32_t mine = 0;  // kept items of this lane (pass 1)
-  for (uint32_t g = 0; g < groups; ++g)
+  for (uint32_t g = 0; g < live_groups; ++g)
     mine += __popc(keep_bits16(flags, tb + (uint64_t)g * LB_GROUP + (uint64_t)threadIdx.x * 16, count));
   uint32_t tot;
   (void)block_offsets(mine, s_wcnt, &tot);  // block total (barriers inside)
@@ -2009,7 +2018,7 @@ __global__ __launch_bounds__(BLOCK) void k_select_lb(const uint8_t *__restrict__
   if (!s_ok) return;
   // pass 2: the keep bytes again (L2-resident) -> out, in item order
   uint64_t run = s_excl;
-  for (uint32_t g = 0; g < groups; ++g) {
+  for (uint32_t g = 0; g < live_groups; ++g) {
     const uint64_t i0 = tb + (uint64_t)g * LB_GROUP + (uint64_t)threadIdx.x * 16;
     uint32_t bits = keep_bits16(flags, i0, count);
     uint32_t gt;
@@ -2204,6 +2213,7 @@ struct ghs_solver {
   char *ws_base = nullptr;      // the caller's workspace (carved by workspace_layout)
   bool seed_runs = true;        // level 0 round 0: a-side runs by k_seed_runs (GHS_SEED_RUNS=0: off)
   bool prof = false;            // ghs_profile_enable: every launch bracketed by events
+  uint32_t prof_id = 0;         // tag of this handle's profile records (creation order)
   struct ProfRec {
     ghs_kernel_record_t rec;
     size_t ev;                  // index of its first event in res->prof_ev
@@ -2219,6 +2229,7 @@ struct ghs_solver {
 static std::mutex g_prof_mutex;
 static bool g_prof_on = false;
 static std::vector<ghs_kernel_record_t> g_prof;
+static uint32_t g_prof_next_id = 0;
 
 static const char *const KERNEL_NAMES[GHS_K_COUNT] = {
     "k_select", "k_filter", "k_level_pass", "k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>",
@@ -2244,6 +2255,7 @@ struct KtScope {
     r.rec.round = s->round;
     r.rec.level = s->level;
     r.rec.items = items;
+    r.rec.solver = s->prof_id;
     r.ev = idx;
     s->prof_recs.push_back(r);
     (void)hipEventRecord(pool[idx], s->stream);
@@ -2682,13 +2694,14 @@ static int enqueue_minedge(ghs_solver *s) {
       }
       KT(GHS_K_MINEDGE_IDENT, items);
       k_minedge<true, false><<<g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, nullptr, nullptr,
-                                                         nullptr, nullptr, nullptr, !seed);
+                                                         nullptr, nullptr, nullptr, !seed, nullptr);
     }
   } else {
     // fixed grid: every one of the seg_g blocks writes its region's count
     KT(GHS_K_MINEDGE_COMPACT, 0);
     k_minedge<false, true><<<s->cmp_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, O.src, O.dst,
-                                                          O.key, O.seg_start, O.seg_count, true);
+                                                          O.key, O.seg_start, O.seg_count, true,
+                                                          s->cfg.num_ranks <= 1 ? cur_act_count(s) : nullptr);
     // the regions' prefix scan is left to the round's hook kernel (or a scan launch before the
     // next consumer): s->scan_pending
     s->scan_pending = true;
@@ -2994,7 +3007,11 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   { const char *dbg = getenv("GHS_DEBUG"); s->debug = dbg && dbg[0] == '1'; }
   { const char *det = getenv("GHS_DETAIL"); s->detail = det && det[0] == '1'; }
   { const char *tr = getenv("GHS_TIME_ROUNDS"); s->time_rounds = tr && tr[0] == '1'; }
-  { std::lock_guard<std::mutex> lock(g_prof_mutex); s->prof = g_prof_on; }
+  {
+    std::lock_guard<std::mutex> lock(g_prof_mutex);
+    s->prof = g_prof_on;
+    s->prof_id = g_prof_next_id++;
+  }
   if (const char *la = getenv("GHS_LOOKAHEAD")) {  // A/B tests: rounds in flight ahead of the check
     const long v = strtol(la, nullptr, 10);
     s->lookahead = (uint32_t)(v < 0 ? 0 : (v > 4 ? 4 : v));
@@ -3225,6 +3242,7 @@ int ghs_solver_reset(ghs_solver_t *s) {
   { const char *det = getenv("GHS_DETAIL"); t.detail = det && det[0] == '1'; }
   { const char *tr = getenv("GHS_TIME_ROUNDS"); t.time_rounds = tr && tr[0] == '1'; }
   { std::lock_guard<std::mutex> lock(g_prof_mutex); t.prof = g_prof_on; }
+  t.prof_id = s->prof_id;
   t.seg_g = s->seg_g; t.cmp_g = s->cmp_g; t.ident_g = s->ident_g; t.win_g = s->win_g; t.lp_g = s->lp_g;
   t.ws_base = s->ws_base;
   workspace_layout(t.n, t.e_hi - t.e_lo, &t, t.ws_base);

@@ -198,7 +198,7 @@ typedef struct ghs_kernel_record {
   uint32_t round;   /* round index (all levels) when launched; a lookahead no-op round past a
                        level's end reuses the next level's index with its own (older) level */
   uint32_t level;   /* weight level when launched */
-  uint32_t reserved;
+  uint32_t solver;  /* the launching solver handle (creation order in the process) */
   uint64_t items;   /* host-known work count at launch (edges / vertices / fragments), 0 = unknown */
   float ms;         /* event-to-event duration */
   float reserved2;

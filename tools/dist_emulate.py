@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--no-ref", action="store_true", help="skip the single-GPU reference (profiling)")
+    ap.add_argument("--profile", action="store_true",
+                    help="per-launch HIP-event profile of the last rep: kernel ms per round of the max rank")
     args = ap.parse_args()
     import torch
     from distributed_ghs_implementation_amd import _native
@@ -49,14 +51,21 @@ def main():
     engines = [DeviceMST(e, *edge_range(e.m, r, W), config=cfg) for r in range(W)]
     steppers = [HipStepper(x) for x in engines]
 
+    from collections import defaultdict
+    kprof = None  # [round][rank] -> {kernel: ms}
+
     def timed(r, fn):
         torch.cuda.synchronize()
         t = time.perf_counter()
         out = fn()
         torch.cuda.synchronize()
-        return out, (time.perf_counter() - t) * 1e3
+        dt = (time.perf_counter() - t) * 1e3
+        return out, dt
 
     for rep in range(args.reps):
+        if args.profile and rep == args.reps - 1:
+            _native.profile_enable(True)
+            kprof = []
         if rep:
             for s in steppers:
                 s.reset()
@@ -119,6 +128,14 @@ def main():
             done = dones[0]
             rounds.append({"max_rank_ms": round(max(ms), 4), "min_rank_ms": round(min(ms), 4), "collectives": coll})
         res = [s.finish()[0] for s in steppers]
+        if kprof is not None:  # records land at finish; solver tags in creation (= rank) order
+            recs = _native.profile_read()
+            ids = sorted(set(r["solver"] for r in recs))
+            kprof = [[defaultdict(float) for _ in range(W)] for _ in range(len(rounds))]
+            for rec in recs:
+                rk = ids.index(rec["solver"])
+                if rec["round"] < len(rounds):
+                    kprof[rec["round"]][rk][rec["kernel"]] += rec["ms"]
         if ref_flags is not None:
             flags = engines[0].in_mst[: e.m].clone()
             for x in engines[1:]:
@@ -131,6 +148,21 @@ def main():
                           "single_gpu_ms": one_ms and round(one_ms, 3), "rounds": len(rounds),
                           "sum_max_rank_compute_ms": round(compute, 3), "collective_bytes": payload,
                           "per_round": rounds}), flush=True)
+        if kprof is not None:
+            tot = defaultdict(float)
+            for i, per_rank in enumerate(kprof):
+                worst = max(range(W), key=lambda r: sum(per_rank[r].values()))
+                ks = per_rank[worst]
+                for k, v in ks.items():
+                    tot[k] += v
+                print(f"# round {i}: rank {worst} kernels {sum(ks.values()):.3f} ms of {rounds[i]['max_rank_ms']:.3f} | " +
+                      " ".join(f"{k}={v:.3f}" for k, v in sorted(ks.items(), key=lambda kv: -kv[1]) if v >= 0.005),
+                      file=sys.stderr)
+            print("# per solve (max rank per round): " + " ".join(f"{k}={v:.3f}" for k, v in
+                                                                  sorted(tot.items(), key=lambda kv: -kv[1])),
+                  file=sys.stderr)
+            _native.profile_enable(False)
+            kprof = None
     for s in steppers:
         s.close()
 

@@ -1,0 +1,55 @@
+"""One profiled solve (every launch bracketed by HIP events): per-round kernel times next to the
+round's live edges / active fragments / hooks.
+
+    python tools/round_profile.py [--workload rmat|grid|grid-gradient] [--scale 24] [--grid-k 16384]
+"""
+import argparse
+import os
+import sys
+from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="rmat")
+    ap.add_argument("--scale", type=int, default=24)
+    ap.add_argument("--grid-k", type=int, default=16384)
+    ap.add_argument("--reps", type=int, default=2)
+    args = ap.parse_args()
+    import torch
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import DeviceMST, generate_grid, generate_rmat
+    if args.workload == "rmat":
+        e = generate_rmat(args.scale, 16, seed=1, wseed=2)
+    else:
+        e = generate_grid(args.grid_k, 1 if args.workload == "grid-gradient" else 0)
+    eng = DeviceMST(e)
+    eng.run()
+    torch.cuda.synchronize()
+    for _ in range(args.reps):
+        _native.profile_enable(True)
+        res, stats = eng.run()
+        recs = _native.profile_read()
+        _native.profile_enable(False)
+    stats = list(stats)
+    per = defaultdict(lambda: defaultdict(float))
+    other = defaultdict(float)
+    for r in recs:
+        ok = r["round"] < len(stats) and stats[r["round"]]["level"] == r["level"]
+        key = r["round"] if ok else ("noop", r["level"])
+        per[key][r["kernel"]] += r["ms"]
+    tot = sum(r["ms"] for r in recs)
+    print(f"m={e.m} n={e.n} rounds={res.rounds} levels={res.levels} sum of launches {tot:.3f} ms")
+    for i, st in enumerate(stats):
+        ks = per.get(i, {})
+        print(f"r{i:2d} L{st['level']} live {st['live_arcs']:>11d} frags {st['active_components']:>10d} "
+              f"hooks {st['hooks']:>9d} | " + " ".join(f"{k}={v * 1e3:.0f}" for k, v in sorted(ks.items(), key=lambda kv: -kv[1])))
+    for k, ks in per.items():
+        if isinstance(k, tuple):
+            print("noop", k, " ".join(f"{a}={v * 1e3:.0f}" for a, v in ks.items()))
+
+
+if __name__ == "__main__":
+    main()
