@@ -202,6 +202,23 @@ __device__ __forceinline__ void block_offsets_w(uint32_t mine, uint32_t *s_wcnt,
   __syncthreads();
 }
 
+// Two compaction streams' offsets from ONE scan: the per-lane counts (<= 4 each; a block's
+// totals < 2^16) are packed into the two halves of a 32-bit word, so the level / pending split of
+// a tile costs one shuffle scan and one pair of barriers instead of two.
+struct Offs2 {
+  uint32_t lane_excl[2], wave_before[2], wave_cnt[2], total[2];
+};
+__device__ __forceinline__ Offs2 block_offsets_w2(uint32_t mine0, uint32_t mine1, uint32_t *s_wcnt) {
+  uint32_t le, wb, wc, t;
+  block_offsets_w(mine0 | (mine1 << 16), s_wcnt, &le, &wb, &wc, &t);
+  Offs2 o;
+  o.lane_excl[0] = le & 0xffffu;  o.lane_excl[1] = le >> 16;
+  o.wave_before[0] = wb & 0xffffu; o.wave_before[1] = wb >> 16;
+  o.wave_cnt[0] = wc & 0xffffu;   o.wave_cnt[1] = wc >> 16;
+  o.total[0] = t & 0xffffu;       o.total[1] = t >> 16;
+  return o;
+}
+
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -1649,13 +1666,13 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
         touch_giant |= (ga[j] | gb[j]) != 0u;
       }
     }
-    uint32_t le, wb, wc, tlev, trem;
-    block_offsets_w((uint32_t)__popc(lmask), s_wcnt, &le, &wb, &wc, &tlev);
-    stage_write(s_stage[threadIdx.x / WAVE], la, lb, key, lmask, le, wc, lsrc, ldst, lkey, vb + nlev + wb);
-    block_offsets_w((uint32_t)__popc(rmask), s_wcnt, &le, &wb, &wc, &trem);
-    stage_write(s_stage[threadIdx.x / WAVE], a, b, key, rmask, le, wc, osrc, odst, okey, vb + nrem + wb);
-    nlev += tlev;
-    nrem += trem;
+    const Offs2 o = block_offsets_w2((uint32_t)__popc(lmask), (uint32_t)__popc(rmask), s_wcnt);
+    stage_write(s_stage[threadIdx.x / WAVE], la, lb, key, lmask, o.lane_excl[0], o.wave_cnt[0], lsrc, ldst, lkey,
+                vb + nlev + o.wave_before[0]);
+    stage_write(s_stage[threadIdx.x / WAVE], a, b, key, rmask, o.lane_excl[1], o.wave_cnt[1], osrc, odst, okey,
+                vb + nrem + o.wave_before[1]);
+    nlev += o.total[0];
+    nrem += o.total[1];
   }
   if (__syncthreads_or(touch_giant ? 1 : 0) && threadIdx.x == 0 && mark) mark[giant] = 1;
   // both outputs padded to a multiple of 4 with dead entries (a = LABEL_NONE)
@@ -1798,13 +1815,13 @@ GHS_STREAM_KERNEL_6 void k_level_pass(const uint32_t *__restrict__ ru, const uin
         touch_giant |= (ga[j] | gb[j]) != 0u;
       }
     }
-    uint32_t le, wb, wc, tlev, trem;
-    block_offsets_w(mlev, s_wcnt, &le, &wb, &wc, &tlev);
-    stage_write(s_stage[threadIdx.x / WAVE], la, lb, k, lmask, le, wc, lsrc, ldst, lkey, vb + nlev + wb);
-    block_offsets_w(mrem, s_wcnt, &le, &wb, &wc, &trem);
-    stage_write(s_stage[threadIdx.x / WAVE], a, b, k, rmask, le, wc, ou, ov, okey, vb + nrem + wb);
-    nlev += tlev;
-    nrem += trem;
+    const Offs2 o = block_offsets_w2(mlev, mrem, s_wcnt);
+    stage_write(s_stage[threadIdx.x / WAVE], la, lb, k, lmask, o.lane_excl[0], o.wave_cnt[0], lsrc, ldst, lkey,
+                vb + nlev + o.wave_before[0]);
+    stage_write(s_stage[threadIdx.x / WAVE], a, b, k, rmask, o.lane_excl[1], o.wave_cnt[1], ou, ov, okey,
+                vb + nrem + o.wave_before[1]);
+    nlev += o.total[0];
+    nrem += o.total[1];
   }
   if (__syncthreads_or(touch_giant ? 1 : 0) && threadIdx.x == 0 && mark) mark[giant] = 1;
   // both outputs padded to a multiple of 4 with dead entries (a = LABEL_NONE)
