@@ -14,7 +14,7 @@ for rep in $(seq 1 ${REPS:-1}); do
 for v in $VARIANTS; do
   name=${v%%:*}
   envs=${v#*:}
-  ( IFS=','; for kv in $envs; do [ -n "$kv" ] && export "$kv"; done
+  ( IFS=','; for kv in $envs; do [ -n "$kv" ] && export "$kv"; done; unset IFS
     timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-scaling-base ${BENCH_ARGS} > "$OUT/$name.$rep.json" 2> "$OUT/$name.$rep.err" ) || { echo "bench $name failed"; tail -30 "$OUT/$name.$rep.err"; exit 1; }
   python3 -c "import json;d=json.load(open('$OUT/$name.$rep.json'));print('$name', 'value', round(d['value']/1e9,3), 'ms', round(d['ms_per_step'],3), {k: round(v['ms_per_step'],3) for k, v in list((d.get('kernels') or {}).items())[:${TOPK:-6}]})"
 done
