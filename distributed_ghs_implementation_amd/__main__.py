@@ -13,7 +13,12 @@
     --check-result FILE
                    verify an existing result JSON against the graph; no GPU, no solve
 
-Multi-GPU (one process per GPU):
+    --gpus N       one process drives N GPUs of this node (RCCL clique, ghs_mst_multi)
+    --generator {rmat,grid} --scale S --seed X
+                   solve a synthetic BASELINE graph generated on the GPU instead of reading one
+                   (R-MAT 2^S vertices, edgefactor 16; grid: --scale is the side k)
+
+Multi-GPU, one process per GPU:
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         -m distributed_ghs_implementation_amd --graph-dir D
 """
@@ -32,12 +37,23 @@ def main(argv=None):
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify the result (check_mst.py)")
     ap.add_argument("--check-result", type=str, default=None, help="verify an existing result JSON only")
+    ap.add_argument("--gpus", type=int, default=1, help="GPUs driven by this one process (RCCL clique)")
+    ap.add_argument("--generator", choices=["rmat", "grid"], default=None, help="synthetic graph instead of a file")
+    ap.add_argument("--scale", type=int, default=16, help="R-MAT scale (2^scale vertices) / grid side k")
+    ap.add_argument("--seed", type=int, default=1, help="generator seed (weights: seed + 1)")
     args = ap.parse_args(argv)
 
     from . import graph as G
 
     t0 = time.perf_counter()
-    g = G.read_mstbin(args.graph) if args.graph else G.read_graph_dir(args.graph_dir)
+    if args.generator:
+        from .device import generate_grid, generate_rmat
+        e = (generate_rmat(args.scale, 16, seed=args.seed, wseed=args.seed + 1) if args.generator == "rmat"
+             else generate_grid(args.scale, 0, wseed=args.seed + 1))
+        g = e.to_host()
+        del e
+    else:
+        g = G.read_mstbin(args.graph) if args.graph else G.read_graph_dir(args.graph_dir)
     t_read = time.perf_counter() - t0
 
     if args.check_result:
@@ -70,12 +86,16 @@ def main(argv=None):
         dist.destroy_process_group()
     else:
         from .mst import minimum_spanning_forest
-        r = minimum_spanning_forest(g)
+        r = minimum_spanning_forest(g, num_gpus=args.gpus)
         triples, rounds, ms = r.triples(), r.rounds, r.ms_total
     if rank != 0:
         return 0
-    out = args.output or os.path.join(args.graph_dir if not args.graph else os.path.dirname(args.graph) or ".",
-                                      "ghs_mst.json")
+    if args.output:
+        out = args.output
+    elif args.generator:
+        out = "ghs_mst.json"
+    else:
+        out = os.path.join(args.graph_dir if not args.graph else os.path.dirname(args.graph) or ".", "ghs_mst.json")
     res = G.write_result(out, triples)
     if args.mpi_compat:
         G.write_result(os.path.join(os.path.dirname(out), "mst_result_mpi.json"), triples)
@@ -83,7 +103,7 @@ def main(argv=None):
         print("=" * 70)
         print("Boruvka MST on MI355X (HIP) — drop-in for the GHS MPI path")
         print("=" * 70)
-        print(f"Nodes: {g.n}  Edges: {g.m}  GPUs: {world}")
+        print(f"Nodes: {g.n}  Edges: {g.m}  GPUs: {max(world, args.gpus)}")
         print(f"MST edges: {res['num_edges']}  Total MST weight: {res['total_weight']}")
         print(f"Rounds (GHS levels): {rounds}  engine time: {ms:.3f} ms  read: {t_read * 1e3:.1f} ms")
         if res["num_edges"] == g.n - 1:

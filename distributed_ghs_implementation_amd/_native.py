@@ -32,7 +32,7 @@ _ERR_NAMES = {
 
 # every symbol include/ghs_mst.h declares (tests check the .so exports all of them)
 EXPORTED_SYMBOLS = (
-    "ghs_abi_version", "ghs_last_error", "ghs_device_count", "ghs_mst_host",
+    "ghs_abi_version", "ghs_last_error", "ghs_device_count", "ghs_mst_host", "ghs_mst_multi",
     "ghs_default_config", "ghs_workspace_bytes", "ghs_mst_device",
     "ghs_check_canonical",
     "ghs_solver_create", "ghs_solver_minedge", "ghs_solver_exchange_buffer", "ghs_solver_pack_best",
@@ -199,6 +199,7 @@ def load():
             "ghs_last_error": (ctypes.c_char_p, []),
             "ghs_device_count": (i32, [P(i32)]),
             "ghs_mst_host": (i32, [u32, u64, vp, vp, vp, vp, P(Result), P(RoundStats)]),
+            "ghs_mst_multi": (i32, [u32, u64, vp, vp, vp, i32, vp, vp, vp, P(Result), P(RoundStats)]),
             "ghs_default_config": (None, [P(Config)]),
             "ghs_check_canonical": (i32, [u32, u64, vp, vp, vp, P(i32)]),
             "ghs_workspace_bytes": (sz, [u32, u64, u64]),

@@ -804,7 +804,8 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
                                                 unsigned long long *__restrict__ err,
                                                 const uint64_t *__restrict__ scan_count, uint32_t scan_n,
                                                 uint64_t *__restrict__ scan_prefix, unsigned long long *__restrict__ scan_total,
-                                                bool resolved, const unsigned long long *__restrict__ guard_live) {
+                                                bool resolved, const unsigned long long *__restrict__ guard_live,
+                                                uint32_t own_lo, uint32_t own_hi) {
   __shared__ unsigned long long s_w[BLOCK / WAVE], s_c[BLOCK / WAVE];
   unsigned long long wsum = 0, cnt = 0;
   const uint64_t nact = *d_nact;
@@ -823,7 +824,9 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
       const bool mutual = best[other] == k;
       if (!(mutual && c < other)) {
         p = other;
-        in_mst[eid] = 1;
+        // several ranks: each marks only the MSF flags of its own edge range [own_lo, own_hi)
+        // (the totals count every hook on every rank)
+        if (eid >= own_lo && eid < own_hi) in_mst[eid] = 1;
         wsum += k >> 32;
         cnt += 1;
       }
@@ -2770,13 +2773,14 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
       KT(GHS_K_HOOK, 0);
       k_hook<<<gh, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
                                          s->cnt + C_WEIGHT, s->cnt + C_ERR, nullptr, 0, nullptr, nullptr, false,
-                                         s->cnt + C_LIVE);
+                                         s->cnt + C_LIVE, (uint32_t)s->e_lo, (uint32_t)s->e_hi);
     } else {
       const ArcBuf *sb = s->scan_pending ? s->scan_buf : nullptr;
       KT(GHS_K_HOOK, 0);
       k_hook<<<gh, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
                                          s->cnt + C_WEIGHT, s->cnt + C_ERR, sb ? sb->seg_count : nullptr, s->cmp_g,
-                                         sb ? sb->seg_prefix : nullptr, s->cnt + C_LIVE, s->level_round == 0, nullptr);
+                                         sb ? sb->seg_prefix : nullptr, s->cnt + C_LIVE, s->level_round == 0, nullptr,
+                                         (uint32_t)s->e_lo, (uint32_t)s->e_hi);
       s->scan_pending = false;
     }
     GHS_HIP_CHECK(hipGetLastError());
@@ -2976,7 +2980,6 @@ size_t ghs_workspace_bytes(uint32_t n, uint64_t m, uint64_t local_edges) {
 static int solver_begin(ghs_solver *s) {
   hipError_t e;
   const uint32_t n = s->n;
-  const uint64_t m = s->m;
   s->h_cnt = s->res->h_cnt;
   s->h_slot = s->res->h_slot;
   s->d_slot = s->res->d_slot;
@@ -2990,7 +2993,8 @@ static int solver_begin(ghs_solver *s) {
     k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->lab, n);
     k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->par, n);  // every root: par[r] == r
   }
-  if (m && (e = hipMemsetAsync(s->in_mst, 0, m, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset in_mst: ") + hipGetErrorString(e));
+  // only the solver's own edge range: it never writes a flag outside [e_lo, e_hi)
+  if (s->e_hi > s->e_lo && (e = hipMemsetAsync(s->in_mst + s->e_lo, 0, s->e_hi - s->e_lo, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset in_mst: ") + hipGetErrorString(e));
   if ((e = hipMemsetAsync(s->lb_state, 0, LB_MAX_TILES * 8, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset select state: ") + hipGetErrorString(e));
   k_init_counters<<<1, 64, 0, s->stream>>>(s->cnt, n);
   if ((e = hipGetLastError()) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("init kernels: ") + hipGetErrorString(e));

@@ -14,10 +14,10 @@ per round:
     in a level's first round the hook is owner-computes: each rank hooks the fragments whose
     winning edge it holds and the int32 parent slots are combined with all_reduce(MAX);
   * result: the totals are identical on every rank by construction (same inputs, same
-    decisions); an owner-computed hook marks its edge's in_mst flag on the owning rank only, so
-    the flags are combined on demand (`gather_in_mst`: uint8 MAX all-reduce, outside the solve)
-    and rank 0 writes the output (the reference gathered BRANCH edges to rank 0,
-    ghs_implementation_mpi.py:760-779).
+    decisions); every MSF flag is written by the rank that owns its edge, each rank clearing and
+    writing only its own range, so the flags are assembled on demand (`gather_in_mst`: an
+    all-gather of the ranks' slices, outside the solve) and rank 0 writes the output (the
+    reference gathered BRANCH edges to rank 0, ghs_implementation_mpi.py:760-779).
 
 The round loop (`run_rounds`) is written against a small stepper interface so that the same
 orchestration can be exercised on CPU with the gloo backend in tests (tests inject a CPU
@@ -196,11 +196,25 @@ class DistributedMST:
             self.stepper = None
 
     def gather_in_mst(self):
-        """OR the ranks' MSF flags (collective: every rank calls it). Returns the device flags."""
-        flags = self.engine.in_mst[: self.edges.m]
-        if dist.is_initialized() and dist.get_world_size(self.group) > 1:
-            dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=self.group)
-        return flags
+        """Assemble the MSF flags from every rank's own slice [e_lo, e_hi) (collective: every rank
+        calls it; an all-gather of equal-size padded slices). Returns the device flags (m)."""
+        m = self.edges.m
+        flags = self.engine.in_mst[:m]
+        if not (dist.is_initialized() and dist.get_world_size(self.group) > 1):
+            return flags
+        world = dist.get_world_size(self.group)
+        ranges = [edge_range(m, r, world) for r in range(world)]
+        width = max(hi - lo for lo, hi in ranges)
+        dev = flags.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        mine = torch.zeros(width, dtype=torch.uint8, device=dev)
+        lo, hi = ranges[self.rank]
+        mine[: hi - lo] = flags[lo:hi].to(dev)
+        parts = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine, group=self.group)
+        out = torch.empty(m, dtype=torch.uint8, device=flags.device)
+        for (plo, phi), part in zip(ranges, parts):
+            out[plo:phi] = part[: phi - plo].to(flags.device)
+        return out
 
     def in_mst_host(self):
         """The MSF flags as a host bool array (collective, see gather_in_mst)."""

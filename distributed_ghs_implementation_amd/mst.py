@@ -54,8 +54,10 @@ class MSTResult:
         return mst_result_dict(self.triples(), algorithm)
 
 
-def minimum_spanning_forest(graph):
-    """Run the HIP engine on a CanonicalGraph (host arrays) -> MSTResult."""
+def minimum_spanning_forest(graph, num_gpus=1, devices=None):
+    """Run the HIP engine on a CanonicalGraph (host arrays) -> MSTResult. num_gpus > 1 (or an
+    explicit device list): one process drives that many GPUs of this node as an RCCL clique
+    (ghs_mst_multi: the MPI path's multi-rank solve as one call)."""
     if not isinstance(graph, CanonicalGraph):
         raise TypeError("expected a CanonicalGraph (use graph.canonicalize)")
     L = _native.load()
@@ -65,8 +67,14 @@ def minimum_spanning_forest(graph):
     res = _native.Result()
     stats = (_native.RoundStats * _native.GHS_MAX_ROUND_STATS)()
     u, v, w = graph.u, graph.v, graph.w
-    _native.check(L.ghs_mst_host(graph.n, m, u.ctypes.data, v.ctypes.data, w.ctypes.data, in_mst.ctypes.data,
-                                 ctypes.byref(res), stats))
+    if num_gpus > 1 or devices is not None:
+        devs = list(range(num_gpus)) if devices is None else [int(d) for d in devices]
+        arr = (ctypes.c_int * len(devs))(*devs)
+        _native.check(L.ghs_mst_multi(graph.n, m, u.ctypes.data, v.ctypes.data, w.ctypes.data, len(devs), arr,
+                                      None, in_mst.ctypes.data, ctypes.byref(res), stats))
+    else:
+        _native.check(L.ghs_mst_host(graph.n, m, u.ctypes.data, v.ctypes.data, w.ctypes.data, in_mst.ctypes.data,
+                                     ctypes.byref(res), stats))
     st = [stats[i].as_dict() for i in range(res.num_stats)]
     out = MSTResult(graph, in_mst[:m], res.total_weight, res.rounds, st, res.ms_total)
     if out.num_edges != res.num_mst_edges:

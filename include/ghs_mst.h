@@ -107,6 +107,22 @@ int ghs_device_count(int *count);
 int ghs_mst_host(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t *v, const uint32_t *w,
                  uint8_t *in_mst, ghs_result_t *result, ghs_round_stats_t *stats);
 
+/* ---- one process, several GPUs ------------------------------------------------------------
+ * Replaces the MPI path as ONE call (ghs_implementation_mpi.py:884-954: mpiexec with one rank per
+ * vertex, pickled p2p messages, Barrier, gather of the BRANCH edges to rank 0 at :760-779):
+ * num_gpus devices of this node (devices: their HIP ids, NULL = 0..num_gpus-1, distinct) form an
+ * RCCL clique (ncclCommInitAll); one host thread per device copies the canonical list (host
+ * arrays, as ghs_mst_host) to its device and runs the stepwise solver below over its own edge
+ * range [r*m/N, (r+1)*m/N) (4-aligned), with the round's collectives over RCCL (uint8 MAX of
+ * the level flags, int64 MIN of the best keys, int32 MAX of the owner-computed hooks). in_mst
+ * (host, m bytes) = the devices' own-range flags; result/stats are device 0's (the totals are
+ * checked equal on every device). cfg may be NULL (defaults; num_ranks is set to num_gpus).
+ * An input error (non-canonical list) fails the call on every device together (the error byte
+ * of the flag exchange); a device fault (GHS_E_HIP) is not recoverable. */
+int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t *v, const uint32_t *w,
+                  int num_gpus, const int *devices, const ghs_config_t *cfg, uint8_t *in_mst,
+                  ghs_result_t *result, ghs_round_stats_t *stats);
+
 /* ---- device-resident API -----------------------------------------------------------------
  * Input: the canonical edge list in HBM (d_u, d_v, d_w: m uint32 each, 16-byte aligned) — the
  * device form of the reference's per-node neighbour files node_<id>.json
@@ -145,9 +161,10 @@ int ghs_check_canonical(uint32_t n, uint64_t m, const uint32_t *d_u, const uint3
  *         ghs_solver_contract(h, &done)        hook + pointer-jump + next fragment list
  *   ghs_solver_finish(h, result, stats); ghs_solver_destroy(h)
  * Identical inputs on every rank => identical hook decisions => identical totals (ghs_solver_finish)
- * on every rank. The MSF flags are NOT replicated when ghs_solver_hook_local is used (the
- * default of the Python driver): each rank's d_in_mst then holds the hooks whose winning edge
- * it owns, and the MSF is the OR over the ranks (see ghs_solver_hook_local).
+ * on every rank. MSF flags are owner-written: a solver clears and writes d_in_mst[e] only for its
+ * own range e in [e_lo, e_hi) and never touches the rest, so the MSF is the concatenation of the
+ * ranks' slices (an all-gather of [e_lo, e_hi) from every rank; the reference gathered BRANCH
+ * edges to rank 0, ghs_implementation_mpi.py:760-779).
  * Errors: a rank that finds its edge range non-canonical records it in the exchanged flag
  * buffer (its last byte), so after the caller's MAX every rank returns GHS_E_NONCANON from the
  * same ghs_solver_minedge call — no rank is left waiting in a collective. */
@@ -168,10 +185,8 @@ int ghs_solver_unpack_best(ghs_solver_t *h, const int64_t *d_dense);
  * and hands them to unpack_hook, after which contract skips its own hook. *count = 0: not
  * applicable this round (contract hooks in fragment form, as without the call). Replaces the
  * per-fragment gathers of the fragment-form hook with 4 bytes per active fragment on the wire.
- * The MSF flag of such a hook is set only on the rank that owns the edge: after a solve that
- * used hook_local, d_in_mst of each rank holds a subset and the OR over the ranks (a uint8 MAX
- * all-reduce of the m flags, or a gather of each rank's [e_lo, e_hi) slice plus the rest) is
- * the MSF; the totals of ghs_solver_finish are complete on every rank. */
+ * The MSF flag of such a hook is set only on the rank that owns the edge (as every flag: see
+ * above); the totals of ghs_solver_finish are complete on every rank. */
 int ghs_solver_hook_local(ghs_solver_t *h, int32_t *d_dense, uint64_t *count);
 int ghs_solver_unpack_hook(ghs_solver_t *h, const int32_t *d_dense);
 /* hook + jump + next list; *done = 1 when every level is complete */

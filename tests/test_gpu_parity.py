@@ -159,7 +159,7 @@ def test_stepwise_solver_equals_monolithic(torch_cuda):
 def _emulate_ranks(e, world, cfg=None):
     """`world` edge-range engines on one GPU stepping in lock step, the collectives emulated with
     torch.maximum / torch.minimum (exactly what RCCL's MAX / MIN all-reduce compute). Returns the
-    OR of the ranks' MSF flags (an owner-computed hook marks its owner's copy only) and every
+    MSF flags assembled from the ranks' own slices (each rank writes only [e_lo, e_hi)) and every
     rank's (total weight, MSF edges)."""
     import torch
     from distributed_ghs_implementation_amd import _native
@@ -168,6 +168,8 @@ def _emulate_ranks(e, world, cfg=None):
     cfg = cfg or _native.make_config(num_ranks=world)
     engines = [DeviceMST(e, *edge_range(e.m, r, world), config=cfg) for r in range(world)]
     assert sum(x.e_hi - x.e_lo for x in engines) == e.m
+    for x in engines:  # a sentinel outside each rank's own range: it must never be written
+        x.in_mst.fill_(7)
     steppers = [HipStepper(x) for x in engines]
     try:
         done = False
@@ -207,9 +209,13 @@ def _emulate_ranks(e, world, cfg=None):
         for s in steppers:
             res, _ = s.finish()
             totals.append((res.total_weight, res.num_mst_edges))
-        flags = engines[0].in_mst[: e.m].clone()
-        for x in engines[1:]:
-            flags = torch.maximum(flags, x.in_mst[: e.m])
+        # owner-written flags: the MSF is the concatenation of the ranks' own slices, and no rank
+        # wrote outside its range
+        flags = torch.empty(e.m, dtype=torch.uint8, device=e.u.device)
+        for x in engines:
+            flags[x.e_lo:x.e_hi] = x.in_mst[x.e_lo:x.e_hi]
+            assert bool((x.in_mst[: x.e_lo] == 7).all()) and bool((x.in_mst[x.e_hi: e.m] == 7).all())
+        assert int(flags.max().item() if e.m else 0) <= 1
         return flags, totals
     finally:
         for s in steppers:
@@ -514,3 +520,54 @@ def test_any_numeric_weights_through_ghsalgorithm(seed, torch_cuda):
     assert got == [(a, b) for (a, b, _), f in zip(canon, ref_in) if f]
     assert ghs.mst_weight == pytest.approx(ref_w, rel=1e-12)
     assert ghs.mst_triples() == [t for t, f in zip(canon, ref_in) if f]
+
+
+@pytest.mark.parametrize("name", ["readme6.json", "cgf_n1000_p05.json.gz", "ties_4.json", "empty.json"])
+def test_multi_gpu_entry_one_device_vs_oracle(name, torch_cuda):
+    """ghs_mst_multi (one process, RCCL clique via ncclCommInitAll, one host thread per device)
+    on the box's one device: the same flags as canonical Kruskal. The collective calls of the
+    multi-rank protocol run (a 1-rank RCCL communicator); N > 1 needs an 8-GPU node."""
+    from distributed_ghs_implementation_amd import canonicalize, minimum_spanning_forest
+    ora = _oracle()
+    fx = load_fixture(name)
+    g = canonicalize(fx["num_nodes"], edges=fx["edges"])
+    r = minimum_spanning_forest(g, devices=[0])
+    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    assert np.array_equal(r.in_mst, ref_in.astype(bool))
+    assert r.total_weight == ref_tw == fx["expected_total_weight"] and r.num_edges == ref_k
+
+
+def test_multi_gpu_entry_rmat_and_bad_devices(torch_cuda):
+    import torch
+    from distributed_ghs_implementation_amd import _native, minimum_spanning_forest
+    from distributed_ghs_implementation_amd.device import generate_rmat
+    ora = _oracle()
+    g = generate_rmat(18, 16, seed=1, wseed=2).to_host()
+    r = minimum_spanning_forest(g, devices=[0])
+    ref_in, ref_tw, _ = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    assert np.array_equal(r.in_mst, ref_in.astype(bool)) and r.total_weight == ref_tw
+    with pytest.raises(_native.GHSError) as ei:  # one rank per GPU
+        minimum_spanning_forest(g, devices=[0, 0])
+    assert ei.value.code == _native.GHS_E_ARG
+    with pytest.raises(_native.GHSError) as ei:
+        minimum_spanning_forest(g, num_gpus=torch.cuda.device_count() + 1)
+    assert ei.value.code == _native.GHS_E_ARG
+    # a non-canonical list fails through the multi-GPU entry as well (error byte of the exchange)
+    from distributed_ghs_implementation_amd.graph import CanonicalGraph
+    bad = CanonicalGraph(g.n, g.u.copy(), g.v.copy(), g.w)
+    bad.v[g.m // 2] = bad.u[g.m // 2]
+    with pytest.raises(_native.GHSError) as ei:
+        minimum_spanning_forest(bad, devices=[0])
+    assert ei.value.code == _native.GHS_E_NONCANON
+
+
+def test_cli_generator_and_multi_gpu_flag(tmp_path, torch_cuda):
+    import json
+    from distributed_ghs_implementation_amd.__main__ import main
+    out = tmp_path / "r.json"
+    assert main(["--generator", "rmat", "--scale", "12", "--gpus", "1", "--output", str(out), "--check", "--quiet"]) == 0
+    res = json.load(open(out))
+    ora = _oracle()
+    n, u, v, w = ora.rmat_canonical(12, 16, 1, 2)
+    _, ref_tw, ref_k = ora.kruskal_c(n, u, v, w)
+    assert res["total_weight"] == ref_tw and res["num_edges"] == ref_k

@@ -137,9 +137,9 @@ def main():
                 if rec["round"] < len(rounds):
                     kprof[rec["round"]][rk][rec["kernel"]] += rec["ms"]
         if ref_flags is not None:
-            flags = engines[0].in_mst[: e.m].clone()
-            for x in engines[1:]:
-                flags = torch.maximum(flags, x.in_mst[: e.m])  # OR over the ranks
+            flags = torch.empty_like(ref_flags)
+            for x in engines:  # owner-written: each rank's own slice
+                flags[x.e_lo:x.e_hi] = x.in_mst[x.e_lo:x.e_hi]
             assert torch.equal(flags, ref_flags), "emulated ranks differ from the single-GPU MSF"
             assert all(r.total_weight == rres.total_weight for r in res)
         compute = sum(r["max_rank_ms"] for r in rounds)
