@@ -805,7 +805,8 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
                                                 const uint64_t *__restrict__ scan_count, uint32_t scan_n,
                                                 uint64_t *__restrict__ scan_prefix, unsigned long long *__restrict__ scan_total,
                                                 bool resolved, const unsigned long long *__restrict__ guard_live,
-                                                uint32_t own_lo, uint32_t own_hi) {
+                                                uint32_t own_lo, uint32_t own_hi,
+                                                const uint32_t *__restrict__ vlab, const uint32_t *__restrict__ dpos) {
   __shared__ unsigned long long s_w[BLOCK / WAVE], s_c[BLOCK / WAVE];
   unsigned long long wsum = 0, cnt = 0;
   const uint64_t nact = *d_nact;
@@ -816,9 +817,16 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
     uint32_t p = c;
     if (k != KEY_NONE) {
       const uint32_t eid = (uint32_t)k;
-      // a level's first round: k_resolve left every label a root (one read, no walk)
-      const uint32_t la = resolved ? lab[eu[eid]] : find_lab(lab, eu[eid], err);
-      const uint32_t lb = resolved ? lab[ev[eid]] : find_lab(lab, ev[eid], err);
+      // a level's first round: k_resolve left every label a root (one read, no walk). A dense level
+      // (several ranks): an endpoint's level-open root vlab[x] (resolved), its dense label
+      // dpos[vlab[x]], then the walk through the dense labels
+      uint32_t xa = eu[eid], xb = ev[eid];
+      if (dpos) {
+        xa = dpos[vlab[xa]];
+        xb = dpos[vlab[xb]];
+      }
+      const uint32_t la = resolved ? lab[xa] : find_lab(lab, xa, err);
+      const uint32_t lb = resolved ? lab[xb] : find_lab(lab, xb, err);
       if (la != c && lb != c) atomicOr(err, 2ull);  // the chosen edge must leave c
       const uint32_t other = (la == c) ? lb : la;
       const bool mutual = best[other] == k;
@@ -1849,6 +1857,76 @@ GHS_STREAM_KERNEL_6 void k_level_pass(const uint32_t *__restrict__ ru, const uin
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Dense levels (several ranks). Once a level's active list A (nact0 fragment roots, identical on
+// every rank) is selected, the level runs in a dense label space 0..nact0-1: pos[A[i]] = i, the
+// rank's level edges are relabelled through pos, and best / lab / par become nact0-sized arrays.
+// The level-opening round's all-reduce slots are then best itself (sequential pack / unpack, no
+// gathers and scatters over the vertex arrays through A), the jump runs over the dense identity
+// list, and the whole level's state stays in nact0 * 16 B. At the level's end every fragment's
+// root is mapped back to vertex labels (vlab[A[i]] = A[root(i)]). SURVEY.md §7(d) "dense relabel
+// of live components" — the per-rank volume the vertex-indexed multi-rank rounds paid.
+// ------------------------------------------------------------------------------------------
+__global__ void k_dense_open(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
+                             uint32_t *__restrict__ pos, uint32_t *__restrict__ vtx, uint32_t *__restrict__ dlab,
+                             uint32_t *__restrict__ dpar, uint64_t *__restrict__ dbest,
+                             unsigned long long *__restrict__ dense_count) {
+  const uint64_t nact = *d_nact;
+  const uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (t0 == 0) *dense_count = nact;
+  for (uint64_t i = t0; i < nact; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = act[i];
+    pos[c] = (uint32_t)i;
+    vtx[i] = c;
+    dlab[i] = (uint32_t)i;
+    dpar[i] = (uint32_t)i;
+    dbest[i] = KEY_NONE;
+  }
+}
+
+// the rank's level edges (a, b: vertex labels of active roots) -> dense labels, in place; the
+// regions' 4-entry tiles as in k_minedge (one region lookup per block range, 16-B accesses)
+__global__ __launch_bounds__(BLOCK) void k_relabel_dense(uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
+                                                         SegView in, const uint32_t *__restrict__ pos) {
+  __shared__ uint32_t s_seg[2];
+  const uint64_t T = in.prefix[in.nseg];
+  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
+  const uint64_t vb = Q * blockIdx.x;
+  const uint64_t ve = (vb + Q < T) ? vb + Q : T;
+  if (threadIdx.x == 0) {
+    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
+    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
+  }
+  __syncthreads();
+  const uint32_t slo = s_seg[0], shi = s_seg[1];
+  for (uint64_t v = vb + (uint64_t)threadIdx.x * 4; v < ve; v += ARCS_PER_BLOCK) {
+    const uint64_t i0 = tile_phys(in, slo, shi, v, ve);
+    uint4 a = *reinterpret_cast<const uint4 *>(src + i0);
+    uint4 b = *reinterpret_cast<const uint4 *>(dst + i0);
+    uint32_t A[4] = {a.x, a.y, a.z, a.w}, B[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // region padding (a == LABEL_NONE) stays dead
+      const bool live = A[j] != LABEL_NONE;
+      const uint32_t pa = pos[live ? A[j] : 0u], pb = pos[live ? B[j] : 0u];
+      A[j] = live ? pa : LABEL_NONE;
+      B[j] = live ? pb : B[j];
+    }
+    *reinterpret_cast<uint4 *>(src + i0) = make_uint4(A[0], A[1], A[2], A[3]);
+    *reinterpret_cast<uint4 *>(dst + i0) = make_uint4(B[0], B[1], B[2], B[3]);
+  }
+}
+
+// level end: every dense fragment's root back to vertex labels
+__global__ void k_dense_close(const uint32_t *__restrict__ vtx, const unsigned long long *__restrict__ d_nact,
+                              const uint32_t *__restrict__ dlab, uint32_t *__restrict__ vlab,
+                              unsigned long long *__restrict__ err) {
+  const uint64_t nact = *d_nact;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nact; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = find_lab(dlab, (uint32_t)i, err);
+    vlab[vtx[i]] = vtx[r];
+  }
+}
+
 // Multi-rank error agreement: a rank's own error bits -> the error byte flags[n] of the level's
 // exchanged flag buffer (2: non-canonical input, 1: another invariant), and after the caller's
 // MAX all-reduce the combined byte -> this rank's error bits, so every rank fails in the same
@@ -2089,6 +2167,7 @@ enum : int {
   C_ERR = C_ERR_IDX,  // invariant / canonicity error bits
   C_PENDING = 5,  // pending edges (virtual total) after the last level pass
   C_N = 6,        // n (the count of the identity active list)
+  C_NDENSE = 7,   // fragments of a dense level (several ranks): the count of its identity list
   C_ACT = 8,      // [8], [9]: lengths of the active lists act[0], act[1]
   C_COUNT = 16
 };
@@ -2232,6 +2311,15 @@ struct ghs_solver {
   std::chrono::steady_clock::time_point t0;
   char *ws_base = nullptr;      // the caller's workspace (carved by workspace_layout)
   bool seed_runs = true;        // level 0 round 0: a-side runs by k_seed_runs (GHS_SEED_RUNS=0: off)
+  // dense levels (several ranks, see k_dense_open): the dense arrays, the vertex arrays they stand
+  // in for while a level runs, and the level's fragment count
+  uint32_t *dlab = nullptr, *dpar = nullptr, *dpos = nullptr, *dvtx = nullptr;
+  uint64_t *dbest = nullptr;
+  uint32_t *vlab = nullptr, *vpar = nullptr;
+  uint64_t *vbest = nullptr;
+  bool dense_mode = false;      // several ranks and the dense arrays exist (GHS_DENSE=0: off)
+  bool level_dense = false;     // the open level runs in dense labels
+  uint64_t dense_n = 0;
   bool prof = false;            // ghs_profile_enable: every launch bracketed by events
   uint32_t prof_id = 0;         // tag of this handle's profile records (creation order)
   struct ProfRec {
@@ -2254,7 +2342,7 @@ static uint32_t g_prof_next_id = 0;
 static const char *const KERNEL_NAMES[GHS_K_COUNT] = {
     "k_select", "k_filter", "k_level_pass", "k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>",
     "k_win", "k_hook", "k_jump_ident", "k_jump", "k_select_lb", "k_resolve", "k_giant", "k_scan_counts",
-    "k_plan", "k_init", "k_pack", "k_unpack", "k_round_report"};
+    "k_plan", "k_init", "k_pack_best", "k_unpack_best", "k_round_report", "k_pack_hook", "k_unpack_hook", "k_dense"};
 
 struct KtScope {
   ghs_solver *s;
@@ -2324,7 +2412,7 @@ static HostRes *pooled_res(int *rc) {
 
 static constexpr uint32_t NSAMPLE_MAX = NSAMPLE_W;
 
-static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, char *base) {
+static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs_solver *s, char *base) {
   size_t off = 0;
   auto carve = [&](size_t bytes) -> char * {
     char *p = base ? base + off : nullptr;
@@ -2339,6 +2427,13 @@ static size_t workspace_layout(uint32_t n, uint64_t local_edges, ghs_solver *s, 
   p = carve(N * 8); if (s) s->best = (uint64_t *)p;
   p = carve(N * 4); if (s) s->act[0] = (uint32_t *)p;
   p = carve(N * 4); if (s) s->act[1] = (uint32_t *)p;
+  if (local_edges < m) {  // a rank of a multi-rank solve: the dense-level arrays
+    p = carve(N * 4); if (s) s->dlab = (uint32_t *)p;
+    p = carve(N * 4); if (s) s->dpar = (uint32_t *)p;
+    p = carve(N * 8); if (s) s->dbest = (uint64_t *)p;
+    p = carve(N * 4); if (s) s->dpos = (uint32_t *)p;
+    p = carve(N * 4); if (s) s->dvtx = (uint32_t *)p;
+  }
   p = carve(N + 1); if (s) s->flags = (uint8_t *)p;  // + the multi-rank error byte flags[n]
   p = carve(((N + 127) / 128) * 16 + 16); if (s) s->bits = (uint64_t *)p;
   p = carve(NSAMPLE_MAX * 4); if (s) s->sample = (uint32_t *)p;
@@ -2610,10 +2705,46 @@ static int open_level(ghs_solver *s, bool async_open = false) {
   return async_open ? open_level_async(s) : open_level_finish(s);
 }
 
+// ---- dense levels (several ranks; kernels at k_dense_open) ------------------------------------
+static int dense_open(ghs_solver *s) {
+  hipStream_t st = s->stream;
+  const uint64_t nact = s->nact;
+  {
+    KT(GHS_K_DENSE, nact);
+    k_dense_open<<<grid_for(nact, 256, 16384), 256, 0, st>>>(s->act[0], s->cnt + C_ACT, s->dpos, s->dvtx, s->dlab,
+                                                             s->dpar, s->dbest, s->cnt + C_NDENSE);
+    const ArcBuf &Y = s->buf[s->cur];
+    SegView in{Y.seg_start, Y.seg_prefix, s->cur_nseg};
+    if (s->cur_arcs)
+      k_relabel_dense<<<grid_for(s->cur_arcs, ARCS_PER_BLOCK, SEG_G), BLOCK, 0, st>>>(Y.src, Y.dst, in, s->dpos);
+  }
+  GHS_HIP_CHECK(hipGetLastError());
+  s->vlab = s->lab; s->vpar = s->par; s->vbest = s->best;
+  s->lab = s->dlab; s->par = s->dpar; s->best = s->dbest;
+  s->level_dense = true;
+  s->dense_n = nact;
+  s->act_ident = true;  // round 0: every dense fragment 0..nact0-1 (count C_NDENSE)
+  return GHS_OK;
+}
+
+static int dense_close(ghs_solver *s) {
+  if (!s->level_dense) return GHS_OK;
+  {
+    KT(GHS_K_DENSE, s->dense_n);
+    k_dense_close<<<grid_for(s->dense_n, 256, 16384), 256, 0, s->stream>>>(s->dvtx, s->cnt + C_NDENSE, s->dlab, s->vlab,
+                                                                           s->cnt + C_ERR);
+  }
+  GHS_HIP_CHECK(hipGetLastError());
+  s->lab = s->vlab; s->par = s->vpar; s->best = s->vbest;
+  s->level_dense = false;
+  return GHS_OK;
+}
+
 // ---- second half of opening a level: the active list and the one host sync ------------------
 // The active fragments are those with an edge in this level — on a multi-rank solve, on ANY rank
 // (the flags were OR-combined by the caller), so every rank selects the same list in the same
 // order and the all-reduce slots line up.
+static int dense_open(ghs_solver *s);
 static int open_level_finish(ghs_solver *s) {
   hipStream_t st = s->stream;
   const uint32_t lv = s->level;
@@ -2655,6 +2786,7 @@ static int open_level_finish(ghs_solver *s) {
   s->level_nact = s->nact;
   s->level_round = 0;
   s->level_open = true;
+  if (s->dense_mode) return dense_open(s);
   return GHS_OK;
 }
 
@@ -2685,7 +2817,7 @@ static int open_level_async(ghs_solver *s) {
 
 static inline unsigned long long *act_count(ghs_solver *s, int which) { return s->cnt + C_ACT + which; }
 static inline const unsigned long long *cur_act_count(ghs_solver *s) {
-  return s->act_ident ? s->cnt + C_N : act_count(s, s->act_cur);
+  return s->act_ident ? s->cnt + (s->level_dense ? C_NDENSE : C_N) : act_count(s, s->act_cur);
 }
 
 // the pending region scan as its own launch (when no hook kernel follows to carry it)
@@ -2773,22 +2905,24 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
       KT(GHS_K_HOOK, 0);
       k_hook<<<gh, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
                                          s->cnt + C_WEIGHT, s->cnt + C_ERR, nullptr, 0, nullptr, nullptr, false,
-                                         s->cnt + C_LIVE, (uint32_t)s->e_lo, (uint32_t)s->e_hi);
+                                         s->cnt + C_LIVE, (uint32_t)s->e_lo, (uint32_t)s->e_hi, nullptr, nullptr);
     } else {
       const ArcBuf *sb = s->scan_pending ? s->scan_buf : nullptr;
       KT(GHS_K_HOOK, 0);
       k_hook<<<gh, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
                                          s->cnt + C_WEIGHT, s->cnt + C_ERR, sb ? sb->seg_count : nullptr, s->cmp_g,
                                          sb ? sb->seg_prefix : nullptr, s->cnt + C_LIVE, s->level_round == 0, nullptr,
-                                         (uint32_t)s->e_lo, (uint32_t)s->e_hi);
+                                         (uint32_t)s->e_lo, (uint32_t)s->e_hi, s->level_dense ? s->vlab : nullptr,
+                                         s->level_dense ? s->dpos : nullptr);
       s->scan_pending = false;
     }
     GHS_HIP_CHECK(hipGetLastError());
     if (s->detail) record(s, 2);
     // Stage 3, then the next active list (one launch each)
-    if (s->act_ident && s->cfg.num_ranks <= 1) {
-      KT(GHS_K_JUMP_IDENT, s->n);
-      k_jump_ident<<<grid_for(((uint64_t)s->n + 3) / 4, BLOCK, 16384), BLOCK, 0, s->stream>>>(s->n, s->par, s->lab, s->best,
+    if (s->act_ident && (s->cfg.num_ranks <= 1 || s->level_dense)) {
+      const uint32_t ni = s->level_dense ? (uint32_t)s->dense_n : s->n;
+      KT(GHS_K_JUMP_IDENT, ni);
+      k_jump_ident<<<grid_for(((uint64_t)ni + 3) / 4, BLOCK, 16384), BLOCK, 0, s->stream>>>(ni, s->par, s->lab, s->best,
                                                                                           s->flags, s->cnt + C_ERR);
     } else {
       KT(GHS_K_JUMP, 0);
@@ -2972,8 +3106,7 @@ void ghs_default_config(ghs_config_t *cfg) {
 }
 
 size_t ghs_workspace_bytes(uint32_t n, uint64_t m, uint64_t local_edges) {
-  (void)m;
-  return workspace_layout(n, local_edges, nullptr, nullptr);
+  return workspace_layout(n, m, local_edges, nullptr, nullptr);
 }
 
 // The per-solve start of a solver: plan, state arrays, counters (create, and reset between solves).
@@ -3014,7 +3147,7 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   if (m && (!d_u || !d_v || !d_w || !d_in_mst)) GHS_FAIL(GHS_E_ARG, "d_u/d_v/d_w/d_in_mst is NULL");
   if ((((uintptr_t)d_u) | ((uintptr_t)d_v) | ((uintptr_t)d_w)) & 15)
     GHS_FAIL(GHS_E_ARG, "d_u/d_v/d_w must be 16-byte aligned");
-  const size_t need = workspace_layout(n, e_hi - e_lo, nullptr, nullptr);
+  const size_t need = workspace_layout(n, m, e_hi - e_lo, nullptr, nullptr);
   if (!d_workspace || workspace_bytes < need)
     GHS_FAIL(GHS_E_NOMEM, "workspace too small: need " + std::to_string(need) + " bytes");
   if (((uintptr_t)d_workspace) & 255) GHS_FAIL(GHS_E_ARG, "workspace must be 256-byte aligned");
@@ -3054,7 +3187,11 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   }
   if (cfg) s->cfg = *cfg; else default_config(&s->cfg);
   s->ws_base = (char *)d_workspace;
-  workspace_layout(n, e_hi - e_lo, s, s->ws_base);
+  workspace_layout(n, m, e_hi - e_lo, s, s->ws_base);
+  {
+    const char *dn = getenv("GHS_DENSE");
+    s->dense_mode = s->cfg.num_ranks > 1 && s->dlab != nullptr && !(dn && dn[0] == '0');
+  }
 
   if (g_create_pool) {
     s->res = g_create_pool;
@@ -3146,16 +3283,30 @@ int ghs_solver_hook_local(ghs_solver_t *s, int32_t *d_dense, uint64_t *count) {
   if (s->phase != 1) GHS_FAIL(GHS_E_STATE, "hook_local must follow unpack_best");
   // a level's first round with several ranks (its edges carry the current roots); labels and
   // fragment ids must fit the int32 MAX exchange
+  // a level's first round (its edges carry the current roots), or any round of a dense level (the
+  // compaction's survivors carry the roots of the round); labels and fragment ids must fit the
+  // int32 MAX exchange
   if (s->cfg.num_ranks <= 1 || s->level_round != 0 || !s->nact || s->hooked || s->n > (1u << 31)) return GHS_OK;
   if (!d_dense) GHS_FAIL(GHS_E_ARG, "dense is NULL");
   const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
-  if (s->cur_arcs || !s->arcs_known) {
-    const ArcBuf &I = s->buf[s->cur];
-    SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
-    k_win<<<s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->win_g) : s->win_g, BLOCK, 0, s->stream>>>(
-        I.src, I.dst, I.key, in, s->best, s->par, s->in_mst, nullptr, nullptr);
+  if (s->level_round == 0) {
+    if (s->cur_arcs || !s->arcs_known) {
+      const ArcBuf &I = s->buf[s->cur];
+      SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
+      KT(GHS_K_WIN, s->arcs_known ? s->cur_arcs : 0);
+      k_win<<<s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->win_g) : s->win_g, BLOCK, 0, s->stream>>>(
+          I.src, I.dst, I.key, in, s->best, s->par, s->in_mst, nullptr, nullptr);
+    }
+  } else {
+    // this round's compaction output: the surviving (inter-fragment) edges, relabelled to the
+    // round's roots; every fragment's winning edge is one of them, on exactly one rank
+    if (s->scan_pending) flush_scan(s);
+    const ArcBuf &O = s->buf[s->cur ^ 1];
+    SegView in{O.seg_start, O.seg_prefix, s->cmp_g};
+    KT(GHS_K_WIN, 0);
+    k_win<<<s->win_g, BLOCK, 0, s->stream>>>(O.src, O.dst, O.key, in, s->best, s->par, s->in_mst, nullptr, nullptr);
   }
-  KT(GHS_K_PACK, s->nact);
+  KT(GHS_K_PACK_HOOK, s->nact);
   k_pack_hook<<<grid_for(s->nact, 256, 16384), 256, 0, s->stream>>>(act, cur_act_count(s), s->par, d_dense);
   GHS_HIP_CHECK(hipGetLastError());
   *count = s->nact;
@@ -3168,7 +3319,7 @@ int ghs_solver_unpack_hook(ghs_solver_t *s, const int32_t *d_dense) {
     GHS_FAIL(GHS_E_STATE, "unpack_hook must follow hook_local");
   if (s->nact) {
     const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
-    KT(GHS_K_UNPACK, s->nact);
+    KT(GHS_K_UNPACK_HOOK, s->nact);
     k_unpack_hook<<<grid_for(s->nact, BLOCK, HOOK_G), BLOCK, 0, s->stream>>>(act, cur_act_count(s), d_dense, s->best,
                                                                             s->par, s->cnt + C_WEIGHT);
     GHS_HIP_CHECK(hipGetLastError());
@@ -3197,6 +3348,7 @@ int ghs_solver_contract(ghs_solver_t *s, int *done) {
   s->nact = s->h_cnt[C_ACT + nb];
   advance_round(s);
   if (s->nact <= 1) {  // level complete (one active fragment: its remaining edges are internal)
+    if (int rc = dense_close(s)) return rc;
     close_level(s);
   } else {
     s->phase = 0;
@@ -3266,7 +3418,8 @@ int ghs_solver_reset(ghs_solver_t *s) {
   t.prof_id = s->prof_id;
   t.seg_g = s->seg_g; t.cmp_g = s->cmp_g; t.ident_g = s->ident_g; t.win_g = s->win_g; t.lp_g = s->lp_g;
   t.ws_base = s->ws_base;
-  workspace_layout(t.n, t.e_hi - t.e_lo, &t, t.ws_base);
+  workspace_layout(t.n, t.m, t.e_hi - t.e_lo, &t, t.ws_base);
+  t.dense_mode = s->dense_mode;
   const bool owned = s->res == &s->own;
   HostRes *pool = s->res;
   t.own = std::move(s->own);

@@ -206,7 +206,8 @@ int ghs_solver_destroy(ghs_solver_t *h);
 enum ghs_kernel_id {
   GHS_K_SELECT = 0, GHS_K_FILTER, GHS_K_LEVEL_PASS, GHS_K_SEED_RUNS, GHS_K_MINEDGE_IDENT, GHS_K_MINEDGE_COMPACT,
   GHS_K_WIN, GHS_K_HOOK, GHS_K_JUMP_IDENT, GHS_K_JUMP, GHS_K_SELECT_LB, GHS_K_RESOLVE, GHS_K_GIANT, GHS_K_SCAN,
-  GHS_K_PLAN, GHS_K_INIT, GHS_K_PACK, GHS_K_UNPACK, GHS_K_ROUND_REPORT, GHS_K_COUNT
+  GHS_K_PLAN, GHS_K_INIT, GHS_K_PACK, GHS_K_UNPACK, GHS_K_ROUND_REPORT, GHS_K_PACK_HOOK, GHS_K_UNPACK_HOOK,
+  GHS_K_DENSE, GHS_K_COUNT
 };
 typedef struct ghs_kernel_record {
   uint32_t kernel;  /* ghs_kernel_id */

@@ -144,9 +144,16 @@ def main():
             assert all(r.total_weight == rres.total_weight for r in res)
         compute = sum(r["max_rank_ms"] for r in rounds)
         payload = sum(b for r in rounds for _, b in r["collectives"])
+        # ring all-reduce: every rank sends (and receives) 2 (N-1)/N of the buffer
+        wire = sum(2.0 * (W - 1) / W * b for r in rounds for _, b in r["collectives"])
+        ncoll = sum(len(r["collectives"]) for r in rounds)
         print(json.dumps({"scale": args.scale, "world": W, "rep": rep, "m": e.m, "n": e.n,
                           "single_gpu_ms": one_ms and round(one_ms, 3), "rounds": len(rounds),
                           "sum_max_rank_compute_ms": round(compute, 3), "collective_bytes": payload,
+                          "wire_bytes_per_rank": int(wire), "collectives": ncoll,
+                          "projected_ms_busbw_300": round(compute + wire / 300e9 * 1e3 + ncoll * 0.02, 3),
+                          "projection_note": "compute + wire bytes per rank / 300 GB/s ring bus bandwidth + "
+                                             "20 us latency per collective (assumptions, not measured)",
                           "per_round": rounds}), flush=True)
         if kprof is not None:
             tot = defaultdict(float)
