@@ -36,6 +36,7 @@ EXPORTED_SYMBOLS = (
     "ghs_default_config", "ghs_workspace_bytes", "ghs_mst_device",
     "ghs_check_canonical",
     "ghs_solver_create", "ghs_solver_minedge", "ghs_solver_exchange_buffer", "ghs_solver_pack_best",
+    "ghs_solver_flag_bits", "ghs_solver_merge_flag_bits",
     "ghs_solver_unpack_best",
     "ghs_solver_contract", "ghs_solver_finish", "ghs_solver_reset", "ghs_solver_destroy",
     "ghs_solver_hook_local", "ghs_solver_unpack_hook",
@@ -207,6 +208,8 @@ def load():
             "ghs_solver_create": (i32, [u32, u64, vp, vp, vp, u64, u64, P(Config), vp, sz, vp, vp, P(vp)]),
             "ghs_solver_minedge": (i32, [vp, P(u64)]),
             "ghs_solver_exchange_buffer": (i32, [vp, P(vp), P(u64)]),
+            "ghs_solver_flag_bits": (i32, [vp, P(vp), P(u64)]),
+            "ghs_solver_merge_flag_bits": (i32, [vp, vp, u32]),
             "ghs_solver_pack_best": (i32, [vp, vp]),
             "ghs_solver_unpack_best": (i32, [vp, vp]),
             "ghs_solver_contract": (i32, [vp, P(i32)]),

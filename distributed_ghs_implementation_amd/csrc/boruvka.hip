@@ -1941,6 +1941,64 @@ __global__ void k_flag_to_err(const uint8_t *__restrict__ flag, unsigned long lo
   if (f) atomicOr(err, f >= 2 ? 8ull : 32ull);
 }
 
+// Level-open flag exchange as bitmaps (several ranks): the n + 1 flag bytes (fragments + error
+// byte) packed to bits — each rank contributes (n + 1) / 8 bytes to an all-gather instead of n + 1
+// bytes to a MAX all-reduce (half the bytes on the wire per rank, one eighth in the buffer) — and
+// the gathered bitmaps OR-ed back into the flag bytes. One wave per 64-bit word.
+__device__ __forceinline__ uint32_t nz_bits16(uint4 f) {  // bit k = byte k of the 16 is nonzero
+  const uint32_t w[4] = {f.x, f.y, f.z, f.w};
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) r |= (((w[k >> 2] >> (8 * (k & 3))) & 0xffu) ? 1u : 0u) << k;
+  return r;
+}
+
+// one thread per 64-bit word: 64 flag bytes in four 16-B loads (a wave reads 4 KB contiguous)
+__global__ void k_pack_flag_bits(const uint8_t *__restrict__ flags, uint64_t nf, uint64_t *__restrict__ bits) {
+  const uint64_t words = (nf + 63) / 64;
+  for (uint64_t wd = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; wd < words; wd += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i0 = wd * 64;
+    uint64_t b = 0;
+    if (i0 + 64 <= nf) {
+      const uint4 *f = reinterpret_cast<const uint4 *>(flags + i0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b |= (uint64_t)nz_bits16(f[q]) << (16 * q);
+    } else {
+      for (uint64_t i = i0; i < nf; ++i) b |= (uint64_t)(flags[i] != 0) << (i - i0);
+    }
+    bits[wd] = b;
+  }
+}
+
+// one thread per word: OR of the ranks' words, 64 flag bytes written as four 16-B stores
+__global__ void k_merge_flag_bits(const uint64_t *__restrict__ all, uint32_t nranks, uint64_t words, uint64_t nf,
+                                  uint8_t *__restrict__ flags, uint8_t *__restrict__ err_byte) {
+  for (uint64_t wd = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; wd < words; wd += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t b = 0;
+    for (uint32_t r = 0; r < nranks; ++r) b |= all[(uint64_t)r * words + wd];
+    const uint64_t i0 = wd * 64;
+    if (i0 + 64 < nf) {  // wholly below the error byte
+      uint4 *f = reinterpret_cast<uint4 *>(flags + i0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t bb = (uint32_t)(b >> (16 * q + 4 * k)) & 15u;  // 4 flags -> 4 bytes
+          w[k] = (bb & 1u) | ((bb & 2u) << 7) | ((bb & 4u) << 14) | ((bb & 8u) << 21);
+        }
+        f[q] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    } else {
+      for (uint64_t i = i0; i < nf; ++i) {
+        const uint8_t x = (uint8_t)((b >> (i - i0)) & 1u);
+        if (i + 1 < nf) flags[i] = x;
+        else *err_byte = x ? 2 : 0;  // bit n: some rank saw bad input (or failed)
+      }
+    }
+  }
+}
+
 __global__ void k_iota(uint32_t *__restrict__ a, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     a[i] = (uint32_t)i;
@@ -2316,6 +2374,7 @@ struct ghs_solver {
   uint32_t *dlab = nullptr, *dpar = nullptr, *dpos = nullptr, *dvtx = nullptr;
   uint64_t *dbest = nullptr;
   uint32_t *vlab = nullptr, *vpar = nullptr;
+  uint64_t *flag_bits = nullptr;  // the packed level-open flags (ghs_solver_flag_bits)
   uint64_t *vbest = nullptr;
   bool dense_mode = false;      // several ranks and the dense arrays exist (GHS_DENSE=0: off)
   bool level_dense = false;     // the open level runs in dense labels
@@ -2342,7 +2401,7 @@ static uint32_t g_prof_next_id = 0;
 static const char *const KERNEL_NAMES[GHS_K_COUNT] = {
     "k_select", "k_filter", "k_level_pass", "k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>",
     "k_win", "k_hook", "k_jump_ident", "k_jump", "k_select_lb", "k_resolve", "k_giant", "k_scan_counts",
-    "k_plan", "k_init", "k_pack_best", "k_unpack_best", "k_round_report", "k_pack_hook", "k_unpack_hook", "k_dense"};
+    "k_plan", "k_init", "k_pack_best", "k_unpack_best", "k_round_report", "k_pack_hook", "k_unpack_hook", "k_dense", "k_flag_bits"};
 
 struct KtScope {
   ghs_solver *s;
@@ -2436,6 +2495,7 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
   }
   p = carve(N + 1); if (s) s->flags = (uint8_t *)p;  // + the multi-rank error byte flags[n]
   p = carve(((N + 127) / 128) * 16 + 16); if (s) s->bits = (uint64_t *)p;
+  p = carve(((N + 1 + 63) / 64) * 8); if (s) s->flag_bits = (uint64_t *)p;
   p = carve(NSAMPLE_MAX * 4); if (s) s->sample = (uint32_t *)p;
   p = carve((PLAN_MAX + 1) * 8); if (s) s->d_thr = (uint64_t *)p;
   p = carve(16); if (s) s->giant = (uint32_t *)p;
@@ -3250,6 +3310,34 @@ int ghs_solver_exchange_buffer(ghs_solver_t *s, uint8_t **d_flags, uint64_t *byt
   GHS_HIP_CHECK(hipStreamSynchronize(s->stream));  // the flags are complete before the caller reads them
   *d_flags = s->flags;
   *bytes = (uint64_t)s->n + 1;  // n fragment flags + the error byte
+  return GHS_OK;
+}
+
+int ghs_solver_flag_bits(ghs_solver_t *s, uint64_t **d_bits, uint64_t *words) {
+  if (!s || !d_bits || !words) GHS_FAIL(GHS_E_ARG, "solver/d_bits/words is NULL");
+  if (!s->pending_exchange) GHS_FAIL(GHS_E_STATE, "no exchange pending");
+  const uint64_t nf = (uint64_t)s->n + 1, nw = (nf + 63) / 64;
+  {
+    KT(GHS_K_FLAG_BITS, nw);
+    k_pack_flag_bits<<<grid_for(nw, 256, 16384), 256, 0, s->stream>>>(s->flags, nf, s->flag_bits);
+  }
+  GHS_HIP_CHECK(hipGetLastError());
+  GHS_HIP_CHECK(hipStreamSynchronize(s->stream));  // complete before the caller's collective reads it
+  *d_bits = s->flag_bits;
+  *words = nw;
+  return GHS_OK;
+}
+
+int ghs_solver_merge_flag_bits(ghs_solver_t *s, const uint64_t *d_all, uint32_t nranks) {
+  if (!s || !d_all || nranks == 0) GHS_FAIL(GHS_E_ARG, "solver/d_all is NULL or nranks is 0");
+  if (!s->pending_exchange) GHS_FAIL(GHS_E_STATE, "no exchange pending");
+  const uint64_t nf = (uint64_t)s->n + 1, nw = (nf + 63) / 64;
+  {
+    KT(GHS_K_FLAG_BITS, nw);
+    k_merge_flag_bits<<<grid_for(nw, 256, 16384), 256, 0, s->stream>>>(d_all, nranks, nw, nf, s->flags,
+                                                                       s->flags + s->n);
+  }
+  GHS_HIP_CHECK(hipGetLastError());
   return GHS_OK;
 }
 

@@ -3,7 +3,7 @@
 // MPI path (ghs_implementation_mpi.py:884-954: mpiexec -n <vertices> ranks exchanging pickled
 // point-to-point messages, then Barrier + gather of the BRANCH edges to rank 0, :760-779) with
 // one rank per GPU and the collectives of include/ghs_mst.h's stepwise protocol:
-//   level open   flags (n fragment bytes + error byte)   all-reduce MAX  (uint8)
+//   level open   flags (n fragment bits + error bit)     all-gather, OR on the device
 //   every round  best keys of the active fragments       all-reduce MIN  (int64, key ^ 2^63)
 //   level round 0 owner-computed hooks (par ^ fragment)  all-reduce MAX  (int32)
 // Each device holds the replicated canonical list and owns the contiguous canonical-edge range
@@ -28,6 +28,7 @@ struct DevRes {
   uint8_t *in_mst = nullptr;   // m flags (own range written)
   int64_t *dense = nullptr;    // all-reduce slots (<= n)
   int32_t *dense_hook = nullptr;
+  uint64_t *gathered = nullptr;  // num_gpus x the level-open flag bitmap
   ghs_solver_t *solver = nullptr;
   ncclComm_t comm = nullptr;
   int rc = GHS_OK;
@@ -88,6 +89,7 @@ int setup(DevRes &d, int r, int N, uint32_t n, uint64_t m, const uint32_t *u, co
   MULTI_HIP(hipMalloc((void **)&d.in_mst, m ? m : 1));
   MULTI_HIP(hipMalloc((void **)&d.dense, ((size_t)n + 1) * 8));
   MULTI_HIP(hipMalloc((void **)&d.dense_hook, ((size_t)n + 1) * 4));
+  MULTI_HIP(hipMalloc((void **)&d.gathered, (size_t)N * (((size_t)n + 1 + 63) / 64) * 8));
   ghs_config_t c2;
   if (cfg) c2 = *cfg; else ghs_default_config(&c2);
   c2.num_ranks = (uint32_t)N;
@@ -107,11 +109,12 @@ int run(DevRes &d, uint64_t m, int r, int N, uint8_t *in_mst_out) {
     }
     uint64_t count = 0;
     int rc = ghs_solver_minedge(d.solver, &count);
-    while (rc == GHS_NEED_EXCHANGE) {  // a level opened: OR its fragment flags (+ error byte)
-      uint8_t *flags = nullptr;
-      uint64_t bytes = 0;
-      MULTI_GHS(ghs_solver_exchange_buffer(d.solver, &flags, &bytes));
-      MULTI_NCCL(ncclAllReduce(flags, flags, bytes, ncclUint8, ncclMax, d.comm, d.stream));
+    while (rc == GHS_NEED_EXCHANGE) {  // a level opened: OR its fragment flags (+ error bit)
+      uint64_t *bits = nullptr;
+      uint64_t words = 0;
+      MULTI_GHS(ghs_solver_flag_bits(d.solver, &bits, &words));
+      MULTI_NCCL(ncclAllGather(bits, d.gathered, words, ncclUint64, d.comm, d.stream));
+      MULTI_GHS(ghs_solver_merge_flag_bits(d.solver, d.gathered, (uint32_t)N));
       rc = ghs_solver_minedge(d.solver, &count);
     }
     MULTI_GHS(rc);
@@ -146,7 +149,7 @@ void release(DevRes &d) {
   if (d.solver) ghs_solver_destroy(d.solver);
   if (d.comm) ncclCommDestroy(d.comm);
   if (d.stream) (void)hipStreamSynchronize(d.stream);
-  for (void *p : {d.canon, d.ws, (void *)d.in_mst, (void *)d.dense, (void *)d.dense_hook})
+  for (void *p : {d.canon, d.ws, (void *)d.in_mst, (void *)d.dense, (void *)d.dense_hook, (void *)d.gathered})
     if (p) (void)hipFree(p);
   if (d.stream) (void)hipStreamDestroy(d.stream);
 }

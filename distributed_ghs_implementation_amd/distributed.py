@@ -7,8 +7,10 @@ per round:
   * partition: rank r owns the contiguous canonical-edge range [r*m/N, (r+1)*m/N) and streams
     only ITS edges through the level passes; the canonical edge list (to resolve a chosen
     edge's endpoints) and the fragment state are replicated;
-  * per level: the fragments with a level edge on ANY rank (n-byte flags, all_reduce MAX) form
-    the identical active list of every rank;
+  * per level: the fragments with a level edge on ANY rank form the identical active list of
+    every rank — each rank's n flags packed to a bitmap and all-gathered (OR-ed on the device),
+    (n + 1) / 8 bytes per rank (or the n + 1 flag bytes all-reduced with MAX);
+    the level then runs in dense labels 0..nact0-1 (boruvka.hip k_dense_open);
   * per round: local min-edge over the rank's level edges -> dense best[] slots of the active
     fragments -> all_reduce(MIN) -> identical hook / pointer-jump / next-list on every rank;
     in a level's first round the hook is owner-computes: each rank hooks the fragments whose
@@ -57,11 +59,25 @@ class HipStepper:
         return int(c.value)
 
     def exchange_buffer(self):
-        """The level's active-fragment flags (uint8, n) as a torch view to all-reduce with MAX."""
+        """The level's active-fragment flags (uint8, n + 1 with the error byte) as a torch view to
+        all-reduce with MAX."""
         p = ctypes.c_void_p(0)
         nb = ctypes.c_uint64(0)
         _native.check(self.L.ghs_solver_exchange_buffer(self.h, ctypes.byref(p), ctypes.byref(nb)))
         return _device_u8_view(p.value, int(nb.value), self.e.edges.device, self.e.ws)
+
+    def flag_bits(self):
+        """The same flags packed to int64 bitmap words (a view of the workspace) to all-gather."""
+        p = ctypes.c_void_p(0)
+        nw = ctypes.c_uint64(0)
+        _native.check(self.L.ghs_solver_flag_bits(self.h, ctypes.byref(p), ctypes.byref(nw)))
+        return _device_u8_view(p.value, 8 * int(nw.value), self.e.edges.device, self.e.ws).view(torch.int64)
+
+    def merge_flag_bits(self, gathered, nranks):
+        """OR the all-gathered bitmaps (rank-major, contiguous) into the level's flags."""
+        gathered = gathered.contiguous()
+        _native.check(self.L.ghs_solver_merge_flag_bits(self.h, _ptr(gathered), int(nranks)))
+        self._keep = gathered  # alive until the stream has consumed it (next call syncs)
 
     def pack(self, count):
         _native.check(self.L.ghs_solver_pack_best(self.h, _ptr(self.dense)))
@@ -107,19 +123,28 @@ class HipStepper:
             pass
 
 
-def run_rounds(stepper, allreduce_min, max_rounds=4096, allreduce_max=None):
+def run_rounds(stepper, allreduce_min, max_rounds=4096, allreduce_max=None, allgather=None):
     """The level loop shared by every backend: (level open: OR the fragment flags), min-edge,
     all-reduce MIN, (a level's first round: owner-computes hook, all-reduce MAX), contract.
 
     `allreduce_min(tensor)` / `allreduce_max(tensor)` reduce in place across ranks (identity for
-    one rank; allreduce_max defaults to allreduce_min's backend with MAX). Returns the number of
-    rounds executed (all weight levels). Raises RuntimeError past `max_rounds` (hang guard;
-    Boruvka needs at most ceil(log2 n) + 1 rounds per level)."""
+    one rank; allreduce_max defaults to allreduce_min's backend with MAX). `allgather(tensor) ->
+    (nranks, tensor)` (default: allreduce_min.gather when present) lets a stepper with bitmap
+    flags (flag_bits / merge_flag_bits) exchange (n + 1) / 8 bytes per rank instead of
+    all-reducing n + 1 flag bytes. Returns the number of rounds executed (all weight levels).
+    Raises RuntimeError past `max_rounds` (hang guard; Boruvka needs at most ceil(log2 n) + 1
+    rounds per level)."""
     rounds = 0
+    gather = allgather or getattr(allreduce_min, "gather", None)
+    use_bits = gather is not None and hasattr(stepper, "flag_bits")
     while True:
         count = stepper.minedge()
         while count is None:  # a level opened: its active fragments = flagged on ANY rank
-            (allreduce_max or allreduce_min.max)(stepper.exchange_buffer())
+            if use_bits:
+                nranks, gathered = gather(stepper.flag_bits())
+                stepper.merge_flag_bits(gathered, nranks)
+            else:
+                (allreduce_max or allreduce_min.max)(stepper.exchange_buffer())
             count = stepper.minedge()
         if count:
             dense = stepper.pack(count)
@@ -145,9 +170,24 @@ def _torch_allreduce(op, group=None):
     return fn
 
 
+def _torch_allgather(group=None):
+    def fn(t):
+        if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+            return 1, t
+        world = dist.get_world_size(group)
+        out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
+        if dist.get_backend(group) == "nccl":
+            dist.all_gather_into_tensor(out, t, group=group)
+        else:
+            dist.all_gather(list(out.chunk(world)), t, group=group)
+        return world, out
+    return fn
+
+
 def torch_allreduce_min(group=None):
     fn = _torch_allreduce(dist.ReduceOp.MIN, group)
     fn.max = _torch_allreduce(dist.ReduceOp.MAX, group)
+    fn.gather = _torch_allgather(group)
     return fn
 
 

@@ -113,8 +113,8 @@ int ghs_mst_host(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t *v, c
  * num_gpus devices of this node (devices: their HIP ids, NULL = 0..num_gpus-1, distinct) form an
  * RCCL clique (ncclCommInitAll); one host thread per device copies the canonical list (host
  * arrays, as ghs_mst_host) to its device and runs the stepwise solver below over its own edge
- * range [r*m/N, (r+1)*m/N) (4-aligned), with the round's collectives over RCCL (uint8 MAX of
- * the level flags, int64 MIN of the best keys, int32 MAX of the owner-computed hooks). in_mst
+ * range [r*m/N, (r+1)*m/N) (4-aligned), with the round's collectives over RCCL (all-gather of the
+ * level-flag bitmaps, int64 MIN of the best keys, int32 MAX of the owner-computed hooks). in_mst
  * (host, m bytes) = the devices' own-range flags; result/stats are device 0's (the totals are
  * checked equal on every device). cfg may be NULL (defaults; num_ranks is set to num_gpus).
  * An input error (non-canonical list) fails the call on every device together (the error byte
@@ -177,6 +177,12 @@ int ghs_solver_minedge(ghs_solver_t *h, uint64_t *num_active);
 /* the flag array to OR-combine (uint8 MAX all-reduce) after GHS_NEED_EXCHANGE: n fragment flags
  * + 1 error byte (*bytes = n + 1) */
 int ghs_solver_exchange_buffer(ghs_solver_t *h, uint8_t **d_flags, uint64_t *bytes);
+/* the same exchange as bitmaps (half the wire bytes of the MAX all-reduce per rank): flag_bits
+ * packs the n + 1 flags into *words uint64 words; the caller all-gathers every rank's words
+ * (rank-major, nranks x words) and hands the gathered buffer to merge_flag_bits (OR), then calls
+ * ghs_solver_minedge again — instead of exchange_buffer + MAX all-reduce */
+int ghs_solver_flag_bits(ghs_solver_t *h, uint64_t **d_bits, uint64_t *words);
+int ghs_solver_merge_flag_bits(ghs_solver_t *h, const uint64_t *d_all, uint32_t nranks);
 int ghs_solver_pack_best(ghs_solver_t *h, int64_t *d_dense);
 int ghs_solver_unpack_best(ghs_solver_t *h, const int64_t *d_dense);
 /* optional, after unpack_best (a level's first round, several ranks): owner-computes CONNECT.
@@ -207,7 +213,7 @@ enum ghs_kernel_id {
   GHS_K_SELECT = 0, GHS_K_FILTER, GHS_K_LEVEL_PASS, GHS_K_SEED_RUNS, GHS_K_MINEDGE_IDENT, GHS_K_MINEDGE_COMPACT,
   GHS_K_WIN, GHS_K_HOOK, GHS_K_JUMP_IDENT, GHS_K_JUMP, GHS_K_SELECT_LB, GHS_K_RESOLVE, GHS_K_GIANT, GHS_K_SCAN,
   GHS_K_PLAN, GHS_K_INIT, GHS_K_PACK, GHS_K_UNPACK, GHS_K_ROUND_REPORT, GHS_K_PACK_HOOK, GHS_K_UNPACK_HOOK,
-  GHS_K_DENSE, GHS_K_COUNT
+  GHS_K_DENSE, GHS_K_FLAG_BITS, GHS_K_COUNT
 };
 typedef struct ghs_kernel_record {
   uint32_t kernel;  /* ghs_kernel_id */

@@ -156,7 +156,7 @@ def test_stepwise_solver_equals_monolithic(torch_cuda):
     assert rc.total_weight == ra.total_weight and rc.rounds == ra.rounds
 
 
-def _emulate_ranks(e, world, cfg=None):
+def _emulate_ranks(e, world, cfg=None, bitmaps=True):
     """`world` edge-range engines on one GPU stepping in lock step, the collectives emulated with
     torch.maximum / torch.minimum (exactly what RCCL's MAX / MIN all-reduce compute). Returns the
     MSF flags assembled from the ranks' own slices (each rank writes only [e_lo, e_hi)) and every
@@ -175,14 +175,19 @@ def _emulate_ranks(e, world, cfg=None):
         done = False
         while not done:
             counts = [s.minedge() for s in steppers]
-            while counts[0] is None:  # a level opened: OR-combine the fragment flags (emulated MAX)
+            while counts[0] is None:  # a level opened: OR-combine the fragment flags
                 assert all(c is None for c in counts)
-                bufs = [s.exchange_buffer() for s in steppers]
-                red = bufs[0].clone()
-                for b in bufs[1:]:
-                    red = torch.maximum(red, b)
-                for b in bufs:
-                    b.copy_(red)
+                if bitmaps:  # packed bitmaps, all-gathered (emulated: concatenated), OR-ed on device
+                    gathered = torch.cat([s.flag_bits().clone() for s in steppers])
+                    for s in steppers:
+                        s.merge_flag_bits(gathered, world)
+                else:  # the n + 1 flag bytes, all-reduced with MAX (emulated)
+                    bufs = [s.exchange_buffer() for s in steppers]
+                    red = bufs[0].clone()
+                    for b in bufs[1:]:
+                        red = torch.maximum(red, b)
+                    for b in bufs:
+                        b.copy_(red)
                 counts = [s.minedge() for s in steppers]
             assert len(set(counts)) == 1
             if counts[0]:
@@ -222,9 +227,10 @@ def _emulate_ranks(e, world, cfg=None):
             s.close()
 
 
-@pytest.mark.parametrize("world,graph", [(2, "rmat"), (3, "rmat"), (8, "rmat"), (8, "grid"), (5, "grid-gradient"),
-                                         (8, "readme"), (4, "ties")])
-def test_partitioned_ranks_emulated_on_one_gpu(world, graph, torch_cuda):
+@pytest.mark.parametrize("world,graph,bitmaps", [(2, "rmat", True), (3, "rmat", False), (8, "rmat", True),
+                                                 (8, "grid", True), (5, "grid-gradient", True), (8, "readme", True),
+                                                 (8, "readme", False), (4, "ties", True), (4, "ties", False)])
+def test_partitioned_ranks_emulated_on_one_gpu(world, graph, bitmaps, torch_cuda):
     """`world` edge-range engines on one GPU, all-reduces emulated: the OR of the ranks' flags is
     canonical Kruskal's MSF (oracle) and every rank reports the oracle's totals."""
     from distributed_ghs_implementation_amd import canonicalize
@@ -242,7 +248,7 @@ def test_partitioned_ranks_emulated_on_one_gpu(world, graph, torch_cuda):
                                                w=rng.integers(0, 3, m)))
     else:
         e = generate_grid(257, 1 if graph == "grid-gradient" else 0)
-    flags, totals = _emulate_ranks(e, world)
+    flags, totals = _emulate_ranks(e, world, bitmaps=bitmaps)
     g = e.to_host()
     ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
     assert np.array_equal(flags.cpu().numpy().astype(bool), ref_in.astype(bool))

@@ -80,13 +80,16 @@ def main():
                 counts.append(c)
                 ms[r] += t
             while counts[0] is None:
-                bufs = [s.exchange_buffer() for s in steppers]
-                red = bufs[0].clone()
-                for b in bufs[1:]:
-                    red = torch.maximum(red, b)
-                for b in bufs:
-                    b.copy_(red)
-                coll.append(("allreduce_max_u8", int(red.numel())))
+                bits = []
+                for r, s in enumerate(steppers):
+                    b, t = timed(r, lambda: s.flag_bits().clone())
+                    bits.append(b)
+                    ms[r] += t
+                gathered = torch.cat(bits)
+                for r, s in enumerate(steppers):
+                    _, t = timed(r, lambda: s.merge_flag_bits(gathered, W))
+                    ms[r] += t
+                coll.append(("allgather_bits", int(bits[0].numel()) * 8))
                 counts = []
                 for r, s in enumerate(steppers):
                     c, t = timed(r, s.minedge)
@@ -144,8 +147,10 @@ def main():
             assert all(r.total_weight == rres.total_weight for r in res)
         compute = sum(r["max_rank_ms"] for r in rounds)
         payload = sum(b for r in rounds for _, b in r["collectives"])
-        # ring all-reduce: every rank sends (and receives) 2 (N-1)/N of the buffer
-        wire = sum(2.0 * (W - 1) / W * b for r in rounds for _, b in r["collectives"])
+        # ring all-reduce: every rank sends (and receives) 2 (N-1)/N of the buffer; all-gather of
+        # a b-byte contribution per rank: (N-1) b
+        wire = sum((W - 1) * b if k.startswith("allgather") else 2.0 * (W - 1) / W * b
+                   for r in rounds for k, b in r["collectives"])
         ncoll = sum(len(r["collectives"]) for r in rounds)
         print(json.dumps({"scale": args.scale, "world": W, "rep": rep, "m": e.m, "n": e.n,
                           "single_gpu_ms": one_ms and round(one_ms, 3), "rounds": len(rounds),
