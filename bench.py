@@ -103,11 +103,16 @@ def launch_bytes(rec, stats, res, n):
         return 16.0 * live  # a 4 + b 4 + key 8 (roots: no gathers)
     if k == "k_minedge<COMPACT>":
         return 24.0 * live + 16.0 * _next_live(stats, r)  # + lab[a], lab[b]; survivors out
+    # rounds >= 1 of one rank with >= 1M active fragments launch both CONNECT forms and the
+    # device runs one (boruvka.hip k_win / k_hook guards: edge form while the survivors are
+    # fewer than 4x the active fragments)
+    edge_form = (not _first_round(stats, r)) and act >= (1 << 20) and _next_live(stats, r) < 4 * act
     if k == "k_win":
-        e = live if _first_round(stats, r) else _next_live(stats, r)
-        return 32.0 * e  # a, b, key + best[a], best[b]
+        if _first_round(stats, r):
+            return 32.0 * live  # a, b, key + best[a], best[b]
+        return 32.0 * _next_live(stats, r) if edge_form else 0.0
     if k == "k_hook":
-        return 40.0 * act  # act, best, eu/ev, lab x2, best[other], par
+        return 0.0 if edge_form else 40.0 * act  # act, best, eu/ev, lab x2, best[other], par
     if k == "k_jump":
         return 21.0 * act  # act, par, lab, best, keep flag
     if k == "k_select_lb":
