@@ -79,7 +79,10 @@ constexpr int FIND_LAB_MAX_HOPS = 256;
 // per-fragment gathers of the canonical endpoints dominate; fragment form (k_hook) otherwise.
 // Chosen on the device from the exact counts; the host enqueues both only while its bound on the
 // active fragments is at least EDGE_HOOK_MIN_BOUND.
-constexpr uint64_t EDGE_HOOK_RATIO = 4;
+#ifndef GHS_EDGE_HOOK_RATIO
+#define GHS_EDGE_HOOK_RATIO 4
+#endif
+constexpr uint64_t EDGE_HOOK_RATIO = GHS_EDGE_HOOK_RATIO;
 constexpr uint32_t HOOK_G = 2048;  // grid cap of the kernels ending in per-block total atomics
 constexpr uint64_t EDGE_HOOK_MIN_BOUND = 1u << 20;
 constexpr uint32_t JUMP_MAX_STEPS = 1u << 26;
