@@ -12,8 +12,8 @@ for f in $(git -C "$ROOT" ls-tree --name-only "$REV" distributed_ghs_implementat
 done
 cd "$T/x/csrc"
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950"
-for s in boruvka ingest host; do /opt/rocm/bin/hipcc $F -c -o $s.o $s.hip 2>&1 | grep -v hip-link || true; done
+for s in boruvka ingest host multi; do [ -f $s.hip ] && { /opt/rocm/bin/hipcc $F -c -o $s.o $s.hip 2>&1 | grep -v hip-link || true; }; done
 mkdir -p "$ROOT/distributed_ghs_implementation_amd/lib/exp"
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$ROOT/distributed_ghs_implementation_amd/lib/exp/$NAME.so" boruvka.o ingest.o host.o
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$ROOT/distributed_ghs_implementation_amd/lib/exp/$NAME.so" *.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -rf "$T"
 echo "built $NAME.so from $REV"
