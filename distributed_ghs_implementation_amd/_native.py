@@ -42,6 +42,7 @@ EXPORTED_SYMBOLS = (
     "ghs_solver_hook_local", "ghs_solver_unpack_hook",
     "ghs_rmat_temp_bytes", "ghs_rmat_generate", "ghs_rmat_tuples", "ghs_grid_generate",
     "ghs_profile_enable", "ghs_profile_read", "ghs_kernel_name",
+    "ghs_comm_unique_id", "ghs_comm_init", "ghs_comm_destroy", "ghs_solver_run", "ghs_mst_emulated",
 )
 
 
@@ -94,7 +95,7 @@ class RoundStatsList(collections.abc.Sequence):
         return repr(list(self))
 
 
-ABI_VERSION = 3  # include/ghs_mst.h GHS_MST_ABI_VERSION
+ABI_VERSION = 4  # include/ghs_mst.h GHS_MST_ABI_VERSION
 
 
 class Result(ctypes.Structure):
@@ -225,6 +226,11 @@ def load():
             "ghs_profile_read": (i32, [vp, u32, P(u32)]),
             "ghs_kernel_name": (ctypes.c_char_p, [u32]),
             "ghs_grid_generate": (i32, [u32, u32, u64, vp, vp, vp, vp]),
+            "ghs_comm_unique_id": (i32, [vp]),
+            "ghs_comm_init": (i32, [i32, i32, vp, P(vp)]),
+            "ghs_comm_destroy": (i32, [vp]),
+            "ghs_solver_run": (i32, [vp, vp]),
+            "ghs_mst_emulated": (i32, [u32, u64, vp, vp, vp, i32, P(Config), vp, P(Result), P(RoundStats)]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(L, name)
@@ -242,6 +248,40 @@ def check(rc):
         msg = load().ghs_last_error()
         raise GHSError(rc, msg.decode() if msg else "")
     return rc
+
+
+GHS_COMM_ID_BYTES = 128  # include/ghs_mst.h
+
+
+def comm_unique_id():
+    """Rank 0's RCCL unique id (bytes) for ghs_comm_init on every rank."""
+    buf = (ctypes.c_uint8 * GHS_COMM_ID_BYTES)()
+    check(load().ghs_comm_unique_id(buf))
+    return bytes(buf)
+
+
+class Comm:
+    """ghs_comm_t: one rank's RCCL communicator for ghs_solver_run (bound to the current device)."""
+
+    def __init__(self, nranks, rank, uid):
+        if len(uid) != GHS_COMM_ID_BYTES:
+            raise ValueError("the unique id must be GHS_COMM_ID_BYTES bytes")
+        buf = (ctypes.c_uint8 * GHS_COMM_ID_BYTES).from_buffer_copy(uid)
+        h = ctypes.c_void_p(0)
+        check(load().ghs_comm_init(int(nranks), int(rank), buf, ctypes.byref(h)))
+        self.h = h
+        self.nranks, self.rank = int(nranks), int(rank)
+
+    def close(self):
+        if self.h:
+            load().ghs_comm_destroy(self.h)
+            self.h = ctypes.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def device_count():

@@ -2396,6 +2396,11 @@ struct ghs_solver {
 // per-kernel durations (and the dominant kernel of its roofline line) come from these. The
 // events add idle time between launches (~5.7 us each), so the bench times its steps without
 // them and profiles one extra step.
+// internal accessors for the round loop of multi.hip (common.h)
+hipStream_t ghs_solver_stream_of(const ghs_solver *s) { return s->stream; }
+uint32_t ghs_solver_n_of(const ghs_solver *s) { return s->n; }
+uint32_t ghs_solver_ranks_of(const ghs_solver *s) { return s->cfg.num_ranks; }
+
 static std::mutex g_prof_mutex;
 static bool g_prof_on = false;
 static std::vector<ghs_kernel_record_t> g_prof;

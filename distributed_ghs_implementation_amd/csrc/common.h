@@ -58,6 +58,11 @@ __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 
 }  // namespace ghs
 
+// solver fields for the round loop of multi.hip (defined in boruvka.hip)
+hipStream_t ghs_solver_stream_of(const ghs_solver *s);
+uint32_t ghs_solver_n_of(const ghs_solver *s);
+uint32_t ghs_solver_ranks_of(const ghs_solver *s);
+
 #define GHS_HIP_CHECK(expr)                                                                     \
   do {                                                                                          \
     hipError_t _e = (expr);                                                                     \

@@ -1,160 +1,359 @@
-// Single-process multi-GPU solve: one call drives N devices of one node as an RCCL clique
-// (ncclCommInitAll), one host thread per device. This is the library form of the reference's
-// MPI path (ghs_implementation_mpi.py:884-954: mpiexec -n <vertices> ranks exchanging pickled
-// point-to-point messages, then Barrier + gather of the BRANCH edges to rank 0, :760-779) with
-// one rank per GPU and the collectives of include/ghs_mst.h's stepwise protocol:
-//   level open   flags (n fragment bits + error bit)     all-gather, OR on the device
-//   every round  best keys of the active fragments       all-reduce MIN  (int64, key ^ 2^63)
+// The multi-rank round loop in the library, and its drivers.
+//
+//   ghs_solver_run     one rank's whole solve: the stepwise protocol of include/ghs_mst.h with the
+//                      collectives of a ghs_comm enqueued on the solver's own stream — the round
+//                      loop that distributed.py run_rounds drives from Python, in one host call
+//   ghs_comm_*         an RCCL communicator per rank (ncclCommInitRank from a unique id the caller
+//                      broadcasts: one process per GPU, e.g. under torch.distributed)
+//   ghs_mst_multi      one process driving N devices: an RCCL clique (ncclCommInitAll), one host
+//                      thread per device, each running ghs_solver_run
+//   ghs_mst_emulated   N ranks on ONE device with in-process collectives of the same semantics
+//                      (test / diagnostic: the exact N-rank loop, checkable on one GPU)
+//
+// This is the library form of the reference's MPI path (ghs_implementation_mpi.py:884-954:
+// mpiexec -n <vertices> ranks exchanging pickled point-to-point messages, then Barrier + gather of
+// the BRANCH edges to rank 0, :760-779) with one rank per GPU and these collectives:
+//   level open    flags (n fragment bits + error bit)     all-gather, OR on the device
+//   every round   best keys of the active fragments       all-reduce MIN  (int64, key ^ 2^63)
 //   level round 0 owner-computed hooks (par ^ fragment)  all-reduce MAX  (int32)
-// Each device holds the replicated canonical list and owns the contiguous canonical-edge range
-// [r*m/N, (r+1)*m/N) (4-aligned) — the same partition as the Python driver (distributed.py).
-// Every device writes the MSF flags of its own range only; the result is their concatenation.
+// Each rank holds the replicated canonical list and owns the contiguous canonical-edge range
+// [r*m/N, (r+1)*m/N) (4-aligned) — the same partition as the Python driver (device.py edge_range).
+// Every rank writes the MSF flags of its own range only; the result is their concatenation.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "common.h"
 
-namespace {
+namespace ghs {
 
-struct DevRes {
-  int dev = 0;
-  hipStream_t stream = nullptr;
-  void *canon = nullptr;       // u, v, w (replicated)
-  void *ws = nullptr;          // solver workspace
-  uint8_t *in_mst = nullptr;   // m flags (own range written)
-  int64_t *dense = nullptr;    // all-reduce slots (<= n)
-  int32_t *dense_hook = nullptr;
-  uint64_t *gathered = nullptr;  // num_gpus x the level-open flag bitmap
-  ghs_solver_t *solver = nullptr;
-  ncclComm_t comm = nullptr;
-  int rc = GHS_OK;
-  std::string err;
-  ghs_result_t result{};
-  std::vector<ghs_round_stats_t> stats;
+// In-process collectives of ghs_mst_emulated: every rank's buffers live on the same device. A
+// generation barrier; a rank that fails aborts the group so the others leave instead of waiting.
+struct EmuGroup {
+  explicit EmuGroup(int n) : nranks(n), ptrs(n, nullptr) {}
+  int nranks;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  bool aborted = false;
+  std::vector<const void *> ptrs;
+  bool barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    if (aborted) return false;
+    const uint64_t g = gen;
+    if (++arrived == nranks) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+      return true;
+    }
+    cv.wait(lk, [&] { return gen != g || aborted; });
+    return !aborted;
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(mu);
+    aborted = true;
+    cv.notify_all();
+  }
 };
 
-inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+}  // namespace ghs
+
+namespace {
+
+__global__ void k_emu_min_i64(int64_t *__restrict__ dst, const int64_t *__restrict__ src, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i] < dst[i] ? src[i] : dst[i];
+}
+__global__ void k_emu_max_i32(int32_t *__restrict__ dst, const int32_t *__restrict__ src, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i] > dst[i] ? src[i] : dst[i];
+}
+
+inline unsigned emu_grid(uint64_t n) {
+  const uint64_t g = (n + 255) / 256;
+  return (unsigned)(g < 4096 ? (g ? g : 1) : 4096);
+}
+
+}  // namespace
+
+struct ghs_comm {
+  int nranks = 1, rank = 0, dev = 0;
+  ncclComm_t nccl = nullptr;
+  bool own_nccl = false;
+  ghs::EmuGroup *emu = nullptr;
+  // device scratch of the loop (grown on demand)
+  int64_t *dense = nullptr;
+  int32_t *hook = nullptr;
+  uint64_t *gathered = nullptr;
+  size_t dense_cap = 0, gathered_cap = 0;
+};
+
+namespace {
+
+#define COMM_NCCL(expr)                                                                            \
+  do {                                                                                             \
+    ncclResult_t _r = (expr);                                                                      \
+    if (_r != ncclSuccess) GHS_FAIL(GHS_E_HIP, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+  } while (0)
+#define COMM_BARRIER(c)                                                                            \
+  do {                                                                                             \
+    if (!(c)->emu->barrier()) GHS_FAIL(GHS_E_STATE, "another rank of the emulated group failed");  \
+  } while (0)
+
+int comm_scratch(ghs_comm *c, uint32_t n) {
+  const size_t slots = (size_t)n + 1, words = ((size_t)n + 1 + 63) / 64;
+  if (c->dense_cap < slots) {
+    if (c->dense) (void)hipFree(c->dense);
+    if (c->hook) (void)hipFree(c->hook);
+    c->dense = nullptr;
+    c->hook = nullptr;
+    c->dense_cap = 0;
+    GHS_HIP_CHECK(hipMalloc((void **)&c->dense, slots * 8));
+    GHS_HIP_CHECK(hipMalloc((void **)&c->hook, slots * 4));
+    c->dense_cap = slots;
+  }
+  if (c->gathered_cap < words * c->nranks) {
+    if (c->gathered) (void)hipFree(c->gathered);
+    c->gathered = nullptr;
+    c->gathered_cap = 0;
+    GHS_HIP_CHECK(hipMalloc((void **)&c->gathered, words * c->nranks * 8));
+    c->gathered_cap = words * c->nranks;
+  }
+  return GHS_OK;
+}
+
+int coll_allgather_u64(ghs_comm *c, const uint64_t *send, uint64_t *recv, size_t count, hipStream_t st) {
+  if (c->nccl) {
+    COMM_NCCL(ncclAllGather(send, recv, count, ncclUint64, c->nccl, st));
+    return GHS_OK;
+  }
+  GHS_HIP_CHECK(hipStreamSynchronize(st));
+  c->emu->ptrs[c->rank] = send;
+  COMM_BARRIER(c);
+  for (int r = 0; r < c->nranks; ++r)
+    GHS_HIP_CHECK(hipMemcpyAsync(recv + (size_t)r * count, c->emu->ptrs[r], count * 8, hipMemcpyDeviceToDevice, st));
+  GHS_HIP_CHECK(hipStreamSynchronize(st));
+  COMM_BARRIER(c);  // every rank has read every send buffer
+  return GHS_OK;
+}
+
+// in-place all-reduce: MIN over int64 or MAX over int32
+template <typename T>
+int coll_allreduce(ghs_comm *c, T *buf, size_t count, hipStream_t st) {
+  constexpr bool is_min = sizeof(T) == 8;
+  if (c->nccl) {
+    COMM_NCCL(ncclAllReduce(buf, buf, count, is_min ? ncclInt64 : ncclInt32, is_min ? ncclMin : ncclMax, c->nccl, st));
+    return GHS_OK;
+  }
+  GHS_HIP_CHECK(hipStreamSynchronize(st));
+  c->emu->ptrs[c->rank] = buf;
+  COMM_BARRIER(c);
+  if (c->rank == 0) {  // rank 0 reduces every buffer into its own
+    for (int r = 1; r < c->nranks; ++r) {
+      if (is_min)
+        k_emu_min_i64<<<emu_grid(count), 256, 0, st>>>((int64_t *)buf, (const int64_t *)c->emu->ptrs[r], count);
+      else
+        k_emu_max_i32<<<emu_grid(count), 256, 0, st>>>((int32_t *)buf, (const int32_t *)c->emu->ptrs[r], count);
+    }
+    GHS_HIP_CHECK(hipGetLastError());
+    GHS_HIP_CHECK(hipStreamSynchronize(st));
+  }
+  COMM_BARRIER(c);
+  if (c->rank != 0) {
+    GHS_HIP_CHECK(hipMemcpyAsync(buf, c->emu->ptrs[0], count * sizeof(T), hipMemcpyDeviceToDevice, st));
+    GHS_HIP_CHECK(hipStreamSynchronize(st));
+  }
+  COMM_BARRIER(c);  // rank 0's buffer is free again
+  return GHS_OK;
+}
+
+#define LOOP_CHECK(expr)          \
+  do {                            \
+    const int _rc = (expr);       \
+    if (_rc < 0) return _rc;      \
+  } while (0)
+
+int run_loop(ghs_solver_t *s, ghs_comm *c) {
+  const uint32_t nr = ghs_solver_ranks_of(s);
+  const bool multi = nr > 1;
+  hipStream_t st = ghs_solver_stream_of(s);
+  if (multi) {
+    GHS_HIP_CHECK(hipSetDevice(c->dev));
+    LOOP_CHECK(comm_scratch(c, ghs_solver_n_of(s)));
+  }
+  for (uint32_t guard = 0;; ++guard) {
+    if (guard > 16 * GHS_MAX_ROUND_STATS) GHS_FAIL(GHS_E_ROUNDCAP, "round cap exceeded");
+    uint64_t count = 0;
+    int rc = ghs_solver_minedge(s, &count);
+    while (rc == GHS_NEED_EXCHANGE) {  // a level opened: OR its fragment flags (+ error bit)
+      uint64_t *bits = nullptr;
+      uint64_t words = 0;
+      LOOP_CHECK(ghs_solver_flag_bits(s, &bits, &words));
+      LOOP_CHECK(coll_allgather_u64(c, bits, c->gathered, words, st));
+      LOOP_CHECK(ghs_solver_merge_flag_bits(s, c->gathered, nr));
+      rc = ghs_solver_minedge(s, &count);
+    }
+    LOOP_CHECK(rc);
+    if (multi && count) {
+      LOOP_CHECK(ghs_solver_pack_best(s, c->dense));
+      LOOP_CHECK(coll_allreduce<int64_t>(c, c->dense, count, st));
+      LOOP_CHECK(ghs_solver_unpack_best(s, c->dense));
+      uint64_t hooks = 0;
+      LOOP_CHECK(ghs_solver_hook_local(s, c->hook, &hooks));
+      if (hooks) {
+        LOOP_CHECK(coll_allreduce<int32_t>(c, c->hook, hooks, st));
+        LOOP_CHECK(ghs_solver_unpack_hook(s, c->hook));
+      }
+    }
+    int done = 0;
+    LOOP_CHECK(ghs_solver_contract(s, &done));
+    if (done) return GHS_OK;
+  }
+}
+
+void comm_free(ghs_comm *c) {
+  if (!c) return;
+  if (hipSetDevice(c->dev) == hipSuccess) {
+    for (void *p : {(void *)c->dense, (void *)c->hook, (void *)c->gathered})
+      if (p) (void)hipFree(p);
+  }
+  if (c->nccl && c->own_nccl) ncclCommDestroy(c->nccl);
+  delete c;
+}
 
 void edge_range(uint64_t m, int r, int N, uint64_t *lo, uint64_t *hi) {
   *lo = ((m * (uint64_t)r) / (uint64_t)N) & ~3ull;
   *hi = (r == N - 1) ? m : (((m * (uint64_t)(r + 1)) / (uint64_t)N) & ~3ull);
 }
 
-#define MULTI_HIP(expr)                                                                            \
-  do {                                                                                             \
-    hipError_t _e = (expr);                                                                        \
-    if (_e != hipSuccess) {                                                                        \
-      d.err = std::string(#expr) + ": " + hipGetErrorString(_e);                                   \
-      return GHS_E_HIP;                                                                            \
-    }                                                                                              \
-  } while (0)
-#define MULTI_NCCL(expr)                                                                           \
-  do {                                                                                             \
-    ncclResult_t _r = (expr);                                                                      \
-    if (_r != ncclSuccess) {                                                                       \
-      d.err = std::string(#expr) + ": " + ncclGetErrorString(_r);                                  \
-      return GHS_E_HIP;                                                                            \
-    }                                                                                              \
-  } while (0)
-#define MULTI_GHS(expr)                                                                            \
-  do {                                                                                             \
-    int _rc = (expr);                                                                              \
-    if (_rc < 0) {                                                                                 \
-      d.err = ghs_last_error();                                                                    \
-      return _rc;                                                                                  \
-    }                                                                                              \
-  } while (0)
+inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// setup on the device's thread: buffers, H2D copies of the canonical list, the solver
-int setup(DevRes &d, int r, int N, uint32_t n, uint64_t m, const uint32_t *u, const uint32_t *v, const uint32_t *w,
-          const ghs_config_t *cfg) {
-  MULTI_HIP(hipSetDevice(d.dev));
-  MULTI_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+// one rank of a driver below: its stream, canonical copy (ghs_mst_multi), workspace, solver
+struct Rank {
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  void *canon = nullptr;       // u, v, w (ghs_mst_multi: replicated per device)
+  void *ws = nullptr;
+  uint8_t *in_mst = nullptr;   // ghs_mst_multi: m flags per device (own range written)
+  ghs_solver_t *solver = nullptr;
+  ghs_comm *comm = nullptr;
+  int rc = GHS_OK;
+  std::string err;
+  ghs_result_t result{};
+  std::vector<ghs_round_stats_t> stats;
+};
+
+int rank_fail(Rank &d, int rc) {
+  d.rc = rc;
+  d.err = ghs_last_error();
+  if (d.comm && d.comm->emu) d.comm->emu->abort();
+  return rc;
+}
+
+// create the rank's solver over device-resident u/v/w and run it to completion
+int rank_solve(Rank &d, int r, int N, uint32_t n, uint64_t m, const uint32_t *du, const uint32_t *dv,
+               const uint32_t *dw, uint8_t *d_in_mst, const ghs_config_t *cfg) {
+  if (hipSetDevice(d.dev) != hipSuccess) return rank_fail(d, GHS_E_HIP);
   uint64_t lo, hi;
   edge_range(m, r, N, &lo, &hi);
-  const size_t cb = al256(m * 4);
-  MULTI_HIP(hipMalloc(&d.canon, 3 * cb + 256));
-  char *c = (char *)d.canon;
-  if (m) {
-    MULTI_HIP(hipMemcpyAsync(c, u, m * 4, hipMemcpyHostToDevice, d.stream));
-    MULTI_HIP(hipMemcpyAsync(c + cb, v, m * 4, hipMemcpyHostToDevice, d.stream));
-    MULTI_HIP(hipMemcpyAsync(c + 2 * cb, w, m * 4, hipMemcpyHostToDevice, d.stream));
-  }
   const size_t wsb = ghs_workspace_bytes(n, m, hi - lo);
-  MULTI_HIP(hipMalloc(&d.ws, wsb));
-  MULTI_HIP(hipMalloc((void **)&d.in_mst, m ? m : 1));
-  MULTI_HIP(hipMalloc((void **)&d.dense, ((size_t)n + 1) * 8));
-  MULTI_HIP(hipMalloc((void **)&d.dense_hook, ((size_t)n + 1) * 4));
-  MULTI_HIP(hipMalloc((void **)&d.gathered, (size_t)N * (((size_t)n + 1 + 63) / 64) * 8));
+  if (hipMalloc(&d.ws, wsb) != hipSuccess) {
+    ghs::set_error("hipMalloc of a rank workspace failed");
+    return rank_fail(d, GHS_E_HIP);
+  }
   ghs_config_t c2;
   if (cfg) c2 = *cfg; else ghs_default_config(&c2);
   c2.num_ranks = (uint32_t)N;
-  MULTI_GHS(ghs_solver_create(n, m, (const uint32_t *)c, (const uint32_t *)(c + cb), (const uint32_t *)(c + 2 * cb),
-                              lo, hi, &c2, d.ws, wsb, d.in_mst, d.stream, &d.solver));
-  return GHS_OK;
-}
-
-// the round loop of one device (distributed.py run_rounds, in C++): every device makes the same
-// sequence of collective calls because every device sees the same counts
-int run(DevRes &d, uint64_t m, int r, int N, uint8_t *in_mst_out) {
-  MULTI_HIP(hipSetDevice(d.dev));
-  for (uint32_t guard = 0;; ++guard) {
-    if (guard > 16 * GHS_MAX_ROUND_STATS) {
-      d.err = "round cap exceeded";
-      return GHS_E_ROUNDCAP;
-    }
-    uint64_t count = 0;
-    int rc = ghs_solver_minedge(d.solver, &count);
-    while (rc == GHS_NEED_EXCHANGE) {  // a level opened: OR its fragment flags (+ error bit)
-      uint64_t *bits = nullptr;
-      uint64_t words = 0;
-      MULTI_GHS(ghs_solver_flag_bits(d.solver, &bits, &words));
-      MULTI_NCCL(ncclAllGather(bits, d.gathered, words, ncclUint64, d.comm, d.stream));
-      MULTI_GHS(ghs_solver_merge_flag_bits(d.solver, d.gathered, (uint32_t)N));
-      rc = ghs_solver_minedge(d.solver, &count);
-    }
-    MULTI_GHS(rc);
-    if (count) {
-      MULTI_GHS(ghs_solver_pack_best(d.solver, d.dense));
-      MULTI_NCCL(ncclAllReduce(d.dense, d.dense, count, ncclInt64, ncclMin, d.comm, d.stream));
-      MULTI_GHS(ghs_solver_unpack_best(d.solver, d.dense));
-      uint64_t hooks = 0;
-      MULTI_GHS(ghs_solver_hook_local(d.solver, d.dense_hook, &hooks));
-      if (hooks) {
-        MULTI_NCCL(ncclAllReduce(d.dense_hook, d.dense_hook, hooks, ncclInt32, ncclMax, d.comm, d.stream));
-        MULTI_GHS(ghs_solver_unpack_hook(d.solver, d.dense_hook));
-      }
-    }
-    int done = 0;
-    MULTI_GHS(ghs_solver_contract(d.solver, &done));
-    if (done) break;
-  }
+  int rc = ghs_solver_create(n, m, du, dv, dw, lo, hi, &c2, d.ws, wsb, d_in_mst, d.stream, &d.solver);
+  if (rc < 0) return rank_fail(d, rc);
+  rc = ghs_solver_run(d.solver, d.comm);
+  if (rc < 0) return rank_fail(d, rc);
   d.stats.assign(GHS_MAX_ROUND_STATS, ghs_round_stats_t{});
-  MULTI_GHS(ghs_solver_finish(d.solver, &d.result, d.stats.data()));
-  uint64_t lo, hi;
-  edge_range(m, r, N, &lo, &hi);
-  if (in_mst_out && hi > lo) {
-    MULTI_HIP(hipMemcpyAsync(in_mst_out + lo, d.in_mst + lo, hi - lo, hipMemcpyDeviceToHost, d.stream));
-    MULTI_HIP(hipStreamSynchronize(d.stream));
-  }
+  rc = ghs_solver_finish(d.solver, &d.result, d.stats.data());
+  if (rc < 0) return rank_fail(d, rc);
   return GHS_OK;
 }
 
-void release(DevRes &d) {
+void rank_release(Rank &d) {
   if (hipSetDevice(d.dev) != hipSuccess) return;
   if (d.solver) ghs_solver_destroy(d.solver);
-  if (d.comm) ncclCommDestroy(d.comm);
   if (d.stream) (void)hipStreamSynchronize(d.stream);
-  for (void *p : {d.canon, d.ws, (void *)d.in_mst, (void *)d.dense, (void *)d.dense_hook, (void *)d.gathered})
+  for (void *p : {d.canon, d.ws, (void *)d.in_mst})
     if (p) (void)hipFree(p);
   if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
+// first failing rank's error, then the totals agree on every rank
+int collect(std::vector<Rank> &d, ghs_result_t *result, ghs_round_stats_t *stats, std::string *err) {
+  for (auto &x : d)
+    if (x.rc) {
+      *err = x.err;
+      return x.rc;
+    }
+  for (size_t i = 1; i < d.size(); ++i)
+    if (d[i].result.total_weight != d[0].result.total_weight || d[i].result.num_mst_edges != d[0].result.num_mst_edges) {
+      *err = "ranks disagree on the MSF totals";
+      return GHS_E_STATE;
+    }
+  if (result) *result = d[0].result;
+  if (stats)
+    for (uint32_t i = 0; i < d[0].result.num_stats; ++i) stats[i] = d[0].stats[i];
+  return GHS_OK;
+}
+
 }  // namespace
+
+extern "C" int ghs_comm_unique_id(uint8_t *id) {
+  if (!id) GHS_FAIL(GHS_E_ARG, "id is NULL");
+  static_assert(sizeof(ncclUniqueId) == GHS_COMM_ID_BYTES, "RCCL unique id size");
+  ncclUniqueId u;
+  COMM_NCCL(ncclGetUniqueId(&u));
+  memcpy(id, &u, GHS_COMM_ID_BYTES);
+  return GHS_OK;
+}
+
+extern "C" int ghs_comm_init(int nranks, int rank, const uint8_t *id, ghs_comm_t **out) {
+  if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks) GHS_FAIL(GHS_E_ARG, "bad communicator arguments");
+  *out = nullptr;
+  ghs_comm *c = new ghs_comm;
+  c->nranks = nranks;
+  c->rank = rank;
+  if (hipGetDevice(&c->dev) != hipSuccess) {
+    delete c;
+    GHS_FAIL(GHS_E_NODEVICE, "no current HIP device");
+  }
+  ncclUniqueId u;
+  memcpy(&u, id, GHS_COMM_ID_BYTES);
+  const ncclResult_t r = ncclCommInitRank(&c->nccl, nranks, u, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    GHS_FAIL(GHS_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  c->own_nccl = true;
+  *out = c;
+  return GHS_OK;
+}
+
+extern "C" int ghs_comm_destroy(ghs_comm_t *comm) {
+  comm_free(comm);
+  return GHS_OK;
+}
+
+extern "C" int ghs_solver_run(ghs_solver_t *s, ghs_comm_t *comm) {
+  if (!s) GHS_FAIL(GHS_E_ARG, "solver is NULL");
+  const uint32_t nr = ghs_solver_ranks_of(s);
+  if (nr > 1 && (!comm || comm->nranks != (int)nr))
+    GHS_FAIL(GHS_E_ARG, "a solver of " + std::to_string(nr) + " ranks needs a communicator of as many ranks");
+  return run_loop(s, comm);
+}
 
 extern "C" int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t *v, const uint32_t *w,
                              int num_gpus, const int *devices, const ghs_config_t *cfg, uint8_t *in_mst,
@@ -173,12 +372,13 @@ extern "C" int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const ui
   }
   int prev = 0;
   (void)hipGetDevice(&prev);
-  std::vector<DevRes> d(num_gpus);
-  std::vector<ncclComm_t> comms(num_gpus);
+  std::vector<Rank> d(num_gpus);
+  std::vector<ghs_comm> comms(num_gpus);
+  std::vector<ncclComm_t> nc(num_gpus);
   int rc = GHS_OK;
   std::string err;
   {
-    const ncclResult_t nr = ncclCommInitAll(comms.data(), num_gpus, devs.data());
+    const ncclResult_t nr = ncclCommInitAll(nc.data(), num_gpus, devs.data());
     if (nr != ncclSuccess) {
       rc = GHS_E_HIP;
       err = std::string("ncclCommInitAll: ") + ncclGetErrorString(nr);
@@ -186,44 +386,110 @@ extern "C" int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const ui
   }
   for (int i = 0; i < num_gpus; ++i) {
     d[i].dev = devs[i];
-    d[i].comm = rc == GHS_OK ? comms[i] : nullptr;
+    comms[i].nranks = num_gpus;
+    comms[i].rank = i;
+    comms[i].dev = devs[i];
+    comms[i].nccl = rc == GHS_OK ? nc[i] : nullptr;
+    comms[i].own_nccl = false;
+    d[i].comm = &comms[i];
   }
-  // setup (threads: the H2D copies of the replicated list proceed in parallel)
   if (rc == GHS_OK) {
+    // one thread per device: stream, H2D copies of the replicated list, then the solve (the
+    // collectives in lock step); the copies of the devices proceed in parallel
     std::vector<std::thread> th;
     for (int i = 0; i < num_gpus; ++i)
-      th.emplace_back([&, i] { d[i].rc = setup(d[i], i, num_gpus, n, m, u, v, w, cfg); });
+      th.emplace_back([&, i] {
+        Rank &x = d[i];
+        if (hipSetDevice(x.dev) != hipSuccess || hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking) != hipSuccess) {
+          ghs::set_error("device setup failed");
+          rank_fail(x, GHS_E_HIP);
+          return;
+        }
+        const size_t cb = al256(m * 4);
+        if (hipMalloc(&x.canon, 3 * cb + 256) != hipSuccess || hipMalloc((void **)&x.in_mst, m ? m : 1) != hipSuccess) {
+          ghs::set_error("hipMalloc of the device's canonical copy failed");
+          rank_fail(x, GHS_E_HIP);
+          return;
+        }
+        char *c = (char *)x.canon;
+        if (m && (hipMemcpyAsync(c, u, m * 4, hipMemcpyHostToDevice, x.stream) != hipSuccess ||
+                  hipMemcpyAsync(c + cb, v, m * 4, hipMemcpyHostToDevice, x.stream) != hipSuccess ||
+                  hipMemcpyAsync(c + 2 * cb, w, m * 4, hipMemcpyHostToDevice, x.stream) != hipSuccess)) {
+          ghs::set_error("H2D copy of the canonical list failed");
+          rank_fail(x, GHS_E_HIP);
+          return;
+        }
+        if (rank_solve(x, i, num_gpus, n, m, (const uint32_t *)c, (const uint32_t *)(c + cb),
+                       (const uint32_t *)(c + 2 * cb), x.in_mst, cfg))
+          return;
+        uint64_t lo, hi;
+        edge_range(m, i, num_gpus, &lo, &hi);
+        if (hi > lo && (hipMemcpyAsync(in_mst + lo, x.in_mst + lo, hi - lo, hipMemcpyDeviceToHost, x.stream) != hipSuccess ||
+                        hipStreamSynchronize(x.stream) != hipSuccess)) {
+          ghs::set_error("D2H copy of the flags failed");
+          rank_fail(x, GHS_E_HIP);
+        }
+      });
     for (auto &t : th) t.join();
-    for (auto &x : d)
-      if (x.rc && rc == GHS_OK) {
-        rc = x.rc;
-        err = x.err;
-      }
+    rc = collect(d, result, stats, &err);
   }
-  // the solve: one thread per device, collectives in lock step
-  if (rc == GHS_OK) {
-    std::vector<std::thread> th;
-    for (int i = 0; i < num_gpus; ++i) th.emplace_back([&, i] { d[i].rc = run(d[i], m, i, num_gpus, in_mst); });
-    for (auto &t : th) t.join();
-    for (auto &x : d)
-      if (x.rc && rc == GHS_OK) {
-        rc = x.rc;
-        err = x.err;
-      }
+  for (auto &x : d) rank_release(x);
+  for (int i = 0; i < num_gpus; ++i) {
+    if (comms[i].nccl) {
+      (void)hipSetDevice(devs[i]);
+      ncclCommDestroy(comms[i].nccl);
+      comms[i].nccl = nullptr;
+    }
+    for (void *p : {(void *)comms[i].dense, (void *)comms[i].hook, (void *)comms[i].gathered})
+      if (p) (void)hipFree(p);
   }
-  if (rc == GHS_OK) {
-    for (int i = 1; i < num_gpus; ++i)
-      if (d[i].result.total_weight != d[0].result.total_weight || d[i].result.num_mst_edges != d[0].result.num_mst_edges) {
-        rc = GHS_E_STATE;
-        err = "devices disagree on the MSF totals";
-      }
-  }
-  if (rc == GHS_OK) {
-    if (result) *result = d[0].result;
-    if (stats) for (uint32_t i = 0; i < d[0].result.num_stats; ++i) stats[i] = d[0].stats[i];
-  }
-  for (auto &x : d) release(x);
   (void)hipSetDevice(prev);
+  if (rc) GHS_FAIL(rc, err);
+  return GHS_OK;
+}
+
+extern "C" int ghs_mst_emulated(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
+                                int num_ranks, const ghs_config_t *cfg, uint8_t *d_in_mst, ghs_result_t *result,
+                                ghs_round_stats_t *stats) {
+  if (num_ranks < 1 || num_ranks > 64) GHS_FAIL(GHS_E_ARG, "num_ranks must be in [1, 64]");
+  if (m && (!d_u || !d_v || !d_w || !d_in_mst)) GHS_FAIL(GHS_E_ARG, "NULL device pointer");
+  if (m >= (1ull << 31)) GHS_FAIL(GHS_E_ARG, "m must be < 2^31");
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) GHS_FAIL(GHS_E_NODEVICE, "no current HIP device");
+  ghs::EmuGroup group(num_ranks);
+  std::vector<Rank> d(num_ranks);
+  std::vector<ghs_comm> comms(num_ranks);
+  for (int i = 0; i < num_ranks; ++i) {
+    comms[i].nranks = num_ranks;
+    comms[i].rank = i;
+    comms[i].dev = dev;
+    comms[i].emu = &group;
+    d[i].dev = dev;
+    d[i].comm = &comms[i];
+  }
+  std::vector<std::thread> th;
+  for (int i = 0; i < num_ranks; ++i)
+    th.emplace_back([&, i] {
+      Rank &x = d[i];
+      if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking) != hipSuccess) {
+        ghs::set_error("stream creation failed");
+        rank_fail(x, GHS_E_HIP);
+        return;
+      }
+      if (rank_solve(x, i, num_ranks, n, m, d_u, d_v, d_w, d_in_mst, cfg)) return;
+      if (hipStreamSynchronize(x.stream) != hipSuccess) {
+        ghs::set_error("stream sync failed");
+        rank_fail(x, GHS_E_HIP);
+      }
+    });
+  for (auto &t : th) t.join();
+  std::string err;
+  const int rc = collect(d, result, stats, &err);
+  for (auto &x : d) rank_release(x);
+  for (auto &c : comms)
+    for (void *p : {(void *)c.dense, (void *)c.hook, (void *)c.gathered})
+      if (p) (void)hipFree(p);
+  (void)hipSetDevice(dev);
   if (rc) GHS_FAIL(rc, err);
   return GHS_OK;
 }

@@ -122,3 +122,20 @@ class DeviceMST:
 
     def in_mst_host(self):
         return self.in_mst[: self.edges.m].cpu().numpy().astype(bool)
+
+
+def emulated_mst(edges, num_ranks, config=None):
+    """The multi-rank loop of an N-GPU solve (ghs_solver_run, every rank its own solver, stream
+    and host thread over its edge range) with all N ranks on THIS device and in-process
+    collectives (ghs_mst_emulated) — the N-rank protocol checked on one GPU. Returns
+    (Result, [round stats], in_mst uint8 tensor of m flags)."""
+    L = _native.load()
+    _native.require_gpu()
+    cfg = config if config is not None else _native.make_config()
+    in_mst = torch.zeros(max(edges.m, 1), dtype=torch.uint8, device=edges.device)
+    torch.cuda.synchronize(edges.device)  # the rank streams read u/v/w written on torch's stream
+    res = _native.Result()
+    stats = (_native.RoundStats * _native.GHS_MAX_ROUND_STATS)()
+    _native.check(L.ghs_mst_emulated(edges.n, edges.m, _ptr(edges.u), _ptr(edges.v), _ptr(edges.w), int(num_ranks),
+                                     ctypes.byref(cfg), _ptr(in_mst), ctypes.byref(res), stats))
+    return res, _native.RoundStatsList(stats, res.num_stats), in_mst[: edges.m]

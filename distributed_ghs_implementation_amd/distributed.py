@@ -26,6 +26,7 @@ orchestration can be exercised on CPU with the gloo backend in tests (tests inje
 stepper from oracle/); the product stepper is `HipStepper` (libghs_mst.so).
 """
 import ctypes
+import os
 
 import torch
 import torch.distributed as dist
@@ -100,6 +101,11 @@ class HipStepper:
         d = ctypes.c_int(0)
         _native.check(self.L.ghs_solver_contract(self.h, ctypes.byref(d)))
         return bool(d.value)
+
+    def run_native(self, comm):
+        """The whole round loop in the library (ghs_solver_run): collectives over `comm` (a
+        _native.Comm, RCCL on the solver's stream), one host call per solve."""
+        _native.check(self.L.ghs_solver_run(self.h, comm.h if comm is not None else None))
 
     def finish(self):
         res = _native.Result()
@@ -202,9 +208,15 @@ def _device_u8_view(ptr, nbytes, device, owner):
 
 
 class DistributedMST:
-    """One rank's share of a multi-GPU MST over a replicated DeviceEdges graph."""
+    """One rank's share of a multi-GPU MST over a replicated DeviceEdges graph.
 
-    def __init__(self, edges, rank=None, world=None, group=None, config=None):
+    native (default: on when the process group's backend is nccl and world > 1): the round loop
+    runs inside the library (ghs_solver_run) over the library's own RCCL communicator — created
+    once from a unique id that rank 0 broadcasts through the process group — with the collectives
+    on the solver's stream: one host call per solve. Off: `run_rounds` drives the same protocol
+    from Python through torch.distributed (any backend)."""
+
+    def __init__(self, edges, rank=None, world=None, group=None, config=None, native=None):
         self.rank = dist.get_rank(group) if rank is None else rank
         self.world = dist.get_world_size(group) if world is None else world
         self.group = group
@@ -215,6 +227,20 @@ class DistributedMST:
         self.engine = DeviceMST(edges, lo, hi, config)
         self.edges = edges
         self.stepper = None
+        if native is None:
+            native = (self.world > 1 and dist.is_initialized() and dist.get_backend(group) == "nccl"
+                      and os.environ.get("GHS_DIST_NATIVE", "1") != "0")
+        self.native = bool(native)
+        self.comm = self._make_comm() if self.native and self.world > 1 else None
+
+    def _make_comm(self):
+        """The library's RCCL communicator: rank 0's unique id broadcast over the process group."""
+        uid = torch.zeros(_native.GHS_COMM_ID_BYTES, dtype=torch.uint8, device=self.edges.device)
+        if self.rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(_native.comm_unique_id()), dtype=torch.uint8))
+        src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
+        dist.broadcast(uid, src=src, group=self.group)
+        return _native.Comm(self.world, self.rank, bytes(uid.cpu().numpy().tobytes()))
 
     def run(self):
         """The level/round loop over the owned edge range. Returns (Result, stats). The solver
@@ -224,7 +250,10 @@ class DistributedMST:
         else:
             self.stepper.reset()
         try:
-            run_rounds(self.stepper, torch_allreduce_min(self.group))
+            if self.native:
+                self.stepper.run_native(self.comm)
+            else:
+                run_rounds(self.stepper, torch_allreduce_min(self.group))
             return self.stepper.finish()
         except BaseException:
             self.close()
@@ -234,6 +263,9 @@ class DistributedMST:
         if self.stepper is not None:
             self.stepper.close()
             self.stepper = None
+        if self.comm is not None:
+            self.comm.close()
+            self.comm = None
 
     def gather_in_mst(self):
         """Assemble the MSF flags from every rank's own slice [e_lo, e_hi) (collective: every rank

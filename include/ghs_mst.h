@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GHS_MST_ABI_VERSION 3
+#define GHS_MST_ABI_VERSION 4
 
 #define GHS_OK 0
 #define GHS_NEED_EXCHANGE 1   /* ghs_solver_minedge on a multi-rank solver opened a level: OR-combine
@@ -202,6 +202,31 @@ int ghs_solver_finish(ghs_solver_t *h, ghs_result_t *result, ghs_round_stats_t *
  * pinned host resources: a multi-GPU caller's per-solve create/destroy becomes one reset) */
 int ghs_solver_reset(ghs_solver_t *h);
 int ghs_solver_destroy(ghs_solver_t *h);
+
+/* ---- the round loop in the library --------------------------------------------------------
+ * ghs_solver_run drives the loop above to completion on the solver's stream — minedge, the
+ * level-flag bitmap all-gather, pack / int64 MIN / unpack, the owner-computed hooks' int32 MAX,
+ * contract — with the collectives of `comm` enqueued on that same stream (RCCL): one host call
+ * per solve instead of ~6 library calls + 2-3 collective launches per round from the caller.
+ * comm: one per rank from ghs_comm_init, after rank 0's ghs_comm_unique_id has reached every
+ * rank (torch.distributed / MPI broadcast of GHS_COMM_ID_BYTES bytes); NULL for a single-rank
+ * solver. Collective: every rank calls it; then ghs_solver_finish as usual. The communicator is
+ * bound to the device current at ghs_comm_init and keeps its own device scratch (grown on demand,
+ * n-sized). */
+#define GHS_COMM_ID_BYTES 128
+typedef struct ghs_comm ghs_comm_t;
+int ghs_comm_unique_id(uint8_t *id);
+int ghs_comm_init(int nranks, int rank, const uint8_t *id, ghs_comm_t **out);
+int ghs_comm_destroy(ghs_comm_t *comm);
+int ghs_solver_run(ghs_solver_t *h, ghs_comm_t *comm);
+/* Test / diagnostic entry: the ghs_solver_run loop of a num_ranks-GPU solve, every rank on the
+ * CURRENT device (one host thread and stream per rank, in-process collectives with the same
+ * semantics as RCCL's) — exercises the exact multi-rank loop on one GPU. Device pointers; every
+ * rank writes its own range of d_in_mst (m flags). result/stats: rank 0's (checked equal on every
+ * rank). */
+int ghs_mst_emulated(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
+                     int num_ranks, const ghs_config_t *cfg, uint8_t *d_in_mst, ghs_result_t *result,
+                     ghs_round_stats_t *stats);
 
 /* ---- per-launch profile ------------------------------------------------------------------
  * The reference measured only wall time (time.time(), ghs_implementation.py:453-464,

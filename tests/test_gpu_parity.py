@@ -329,6 +329,107 @@ def test_partitioned_s26_emulated(world, rmat_s26_reference, torch_cuda):
     torch.cuda.empty_cache()
 
 
+def _test_graph(graph):
+    from distributed_ghs_implementation_amd import canonicalize
+    from distributed_ghs_implementation_amd.device import DeviceEdges, generate_grid, generate_rmat
+    if graph == "rmat":
+        return generate_rmat(15, 16, seed=3, wseed=4)
+    if graph == "readme":  # 9 edges: most of 8 ranks own no edge at all
+        return DeviceEdges.from_host(canonicalize(6, edges=[(0, 1, 1), (0, 2, 4), (1, 2, 2), (1, 3, 5), (2, 3, 3),
+                                                            (2, 4, 7), (3, 4, 6), (3, 5, 8), (4, 5, 9)]))
+    if graph == "ties":
+        rng = np.random.default_rng(12)
+        n, m = 3000, 20000
+        return DeviceEdges.from_host(canonicalize(n, u=rng.integers(0, n, m), v=rng.integers(0, n, m),
+                                                  w=rng.integers(0, 3, m)))
+    if graph == "forest":  # many components, isolated vertices
+        rng = np.random.default_rng(13)
+        n, m = 50000, 20000
+        return DeviceEdges.from_host(canonicalize(n, u=rng.integers(0, n, m), v=rng.integers(0, n, m),
+                                                  w=rng.integers(0, 50, m)))
+    return generate_grid(257, 1 if graph == "grid-gradient" else 0)
+
+
+@pytest.mark.parametrize("world,graph", [(2, "rmat"), (3, "ties"), (8, "rmat"), (8, "grid"), (5, "grid-gradient"),
+                                         (8, "readme"), (4, "forest"), (1, "rmat")])
+def test_native_loop_emulated_vs_oracle(world, graph, torch_cuda):
+    """ghs_solver_run — the library's own multi-rank round loop, the one DistributedMST runs over
+    RCCL — with `world` rank solvers on this GPU (ghs_mst_emulated: a host thread and a stream per
+    rank, in-process collectives): the assembled own-range flags and every rank's totals equal
+    oracle Kruskal."""
+    from distributed_ghs_implementation_amd.device import emulated_mst
+    ora = _oracle()
+    e = _test_graph(graph)
+    res, stats, flags = emulated_mst(e, world)
+    g = e.to_host()
+    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    assert np.array_equal(flags.cpu().numpy().astype(bool), ref_in.astype(bool))
+    assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
+    assert len(stats) == res.num_stats
+
+
+def test_native_loop_emulated_noncanonical_fails_together(torch_cuda):
+    """A non-canonical edge in one rank's range: ghs_mst_emulated returns GHS_E_NONCANON (every
+    rank leaves the loop at the same step — no rank left waiting in a collective)."""
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import DeviceEdges, edge_range, emulated_mst, generate_rmat
+    e = generate_rmat(12, 16, seed=1, wseed=2)
+    lo, hi = edge_range(e.m, 1, 4)
+    v = e.v.clone()
+    v[(lo + hi) // 2] = e.u[(lo + hi) // 2]
+    with pytest.raises(_native.GHSError) as ei:
+        emulated_mst(DeviceEdges(e.n, e.u, v, e.w), 4)
+    assert ei.value.code == _native.GHS_E_NONCANON
+
+
+def test_native_loop_rccl_comm_one_rank(torch_cuda):
+    """ghs_comm_unique_id / ghs_comm_init (ncclCommInitRank, 1 rank on this GPU) + ghs_solver_run
+    on a solver handle, twice (reset between solves): the oracle's MSF; a 2-rank solver refuses a
+    1-rank communicator."""
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import DeviceMST, generate_rmat
+    from distributed_ghs_implementation_amd.distributed import HipStepper
+    ora = _oracle()
+    e = generate_rmat(14, 16, seed=7, wseed=8)
+    g = e.to_host()
+    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    comm = _native.Comm(1, 0, _native.comm_unique_id())
+    eng = DeviceMST(e)
+    st = HipStepper(eng)
+    try:
+        for _ in range(2):
+            st.run_native(comm)
+            res, _ = st.finish()
+            assert np.array_equal(eng.in_mst_host(), ref_in.astype(bool))
+            assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
+            st.reset()
+    finally:
+        st.close()
+    two = DeviceMST(e, 0, e.m // 2 & ~3, _native.make_config(num_ranks=2))
+    st2 = HipStepper(two)
+    try:
+        with pytest.raises(_native.GHSError) as ei:
+            st2.run_native(comm)
+        assert ei.value.code == _native.GHS_E_ARG
+    finally:
+        st2.close()
+        comm.close()
+
+
+@pytest.mark.parametrize("world", [8])
+def test_native_loop_s26_emulated(world, rmat_s26_reference, torch_cuda):
+    """BASELINE config 4 through the library's round loop (ghs_mst_emulated, 8 ranks on this
+    GPU): the s26 MSF of the single-GPU solve (== torch Boruvka checker)."""
+    torch = torch_cuda
+    from distributed_ghs_implementation_amd.device import emulated_mst
+    e, ref_flags, ref_tot = rmat_s26_reference
+    res, _, flags = emulated_mst(e, world)
+    assert torch.equal(flags, ref_flags)
+    assert (res.total_weight, res.num_mst_edges) == ref_tot
+    del flags
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("scale,ef,seed,wseed", [(12, 16, 1, 2), (16, 16, 1, 2), (18, 16, 3, 4), (14, 8, 9, 0)])
 def test_rmat_generator_matches_oracle(scale, ef, seed, wseed, torch_cuda):
     """Generator parity: the raw GPU tuples equal oracle/generators.c tuple for
