@@ -121,9 +121,16 @@ __device__ __forceinline__ void flush_min(uint64_t *__restrict__ best, uint32_t 
 #define GHS_FILTER_GATED 1
 #endif
 #ifndef GHS_HOT_BITS
-#define GHS_HOT_BITS 8
+#define GHS_HOT_BITS 9
 #endif
 constexpr int HOT_BITS = GHS_HOT_BITS;
+// the compacting min-edge's parallel-edge filter: LDS pair slots per block,
+// linear probes, and the host's bound on the active fragments below which the filtering variant
+// is launched (it filters when the exact count is <= the solver's dedup_max: env GHS_DEDUP_MAX,
+// default 0 = off — measured to cost about what it saves, DESIGN.md "Measured and rejected")
+constexpr int DEDUP_SLOTS = 1024;
+constexpr int DEDUP_PROBES = 16;
+constexpr uint64_t DEDUP_BOUND_FACTOR = 32;
 constexpr int HOT_SLOTS = 1 << HOT_BITS;
 
 __device__ __forceinline__ void hot_init(uint32_t *s_hl, unsigned long long *s_hk) {
@@ -470,19 +477,32 @@ __device__ __forceinline__ void tile_load(EdgeTile &t, const uint32_t *__restric
 // COMPACT: survivors (inter-fragment edges) are written relabelled to this block's output
 // region (padded to a multiple of 4 with dead entries).
 // ------------------------------------------------------------------------------------------
-template <bool IDENT, bool COMPACT>
+template <bool IDENT, bool COMPACT, bool DEDUP = false>
 GHS_STREAM_KERNEL_6 void k_minedge(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
                                  const uint64_t *__restrict__ key, SegView in, const uint32_t *__restrict__ lab,
                                  uint64_t *__restrict__ best, uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
                                  uint64_t *__restrict__ okey, uint64_t *__restrict__ oseg_start,
                                  uint64_t *__restrict__ oseg_count, bool aside,
-                                 const unsigned long long *__restrict__ guard_nact) {
+                                 const unsigned long long *__restrict__ guard_nact,
+                                 const unsigned long long *__restrict__ dedup_nact = nullptr, uint32_t dedup_max = 0) {
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
   __shared__ uint32_t s_seg[2];
   __shared__ uint32_t s_hl[HOT_SLOTS];
   __shared__ unsigned long long s_hk[HOT_SLOTS];
   __shared__ WaveStage s_stage[COMPACT ? BLOCK / WAVE : 1];
+  __shared__ unsigned long long s_dp[DEDUP ? DEDUP_SLOTS : 1];  // fragment pair lo << 32 | hi
+  __shared__ unsigned long long s_dk[DEDUP ? DEDUP_SLOTS : 1];  // its minimum key in this block
   const int lane = threadIdx.x & (WAVE - 1);
+  // parallel-edge filter (DEDUP, few active fragments): survivors between the same two fragments
+  // keep only their minimum key per block (the heavier ones close a cycle with it: never in the
+  // MSF); the pairs live in an LDS hash and are emitted once at the end of the block
+  const bool dd = DEDUP && *dedup_nact <= dedup_max;
+  if (DEDUP) {
+    for (int i = threadIdx.x; i < DEDUP_SLOTS; i += BLOCK) {
+      s_dp[i] = ~0ull;
+      s_dk[i] = KEY_NONE;
+    }
+  }
   // a pipelined single-rank level runs one round ahead of the host's termination check: a round
   // that starts with <= 1 active fragment is such a discarded lookahead round (the level is
   // complete) — its blocks write empty regions instead of streaming every remaining edge
@@ -597,6 +617,29 @@ GHS_STREAM_KERNEL_6 void k_minedge(const uint32_t *__restrict__ src, const uint3
     }  // aside
 
     if (COMPACT) {
+      if (DEDUP && dd) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (smask & (1u << j)) {
+            const uint32_t lo = L[j] < D[j] ? L[j] : D[j], hi = L[j] < D[j] ? D[j] : L[j];
+            const unsigned long long pk = ((unsigned long long)lo << 32) | hi;
+            uint32_t slot = mix32(lo ^ (hi * 0x9E3779B1u)) & (DEDUP_SLOTS - 1);
+            for (int t = 0; t < DEDUP_PROBES; ++t) {
+              unsigned long long cur = s_dp[slot];
+              if (cur == ~0ull) {
+                cur = atomicCAS(&s_dp[slot], ~0ull, pk);
+                if (cur == ~0ull) cur = pk;
+              }
+              if (cur == pk) {  // a plain read first: few pairs means many lanes on one slot
+                if ((unsigned long long)K[j] < s_dk[slot]) atomicMin(&s_dk[slot], (unsigned long long)K[j]);
+                smask &= ~(1u << j);  // absorbed; a full neighbourhood leaves it to the stream
+                break;
+              }
+              slot = (slot + 1) & (DEDUP_SLOTS - 1);
+            }
+          }
+        }
+      }
       uint32_t lane_excl, wave_before, wave_cnt, total;
       block_offsets_w((uint32_t)__popc(smask), s_wcnt, &lane_excl, &wave_before, &wave_cnt, &total);
       stage_write(s_stage[threadIdx.x / WAVE], L, D, K, smask, lane_excl, wave_cnt, osrc, odst, okey,
@@ -608,6 +651,26 @@ GHS_STREAM_KERNEL_6 void k_minedge(const uint32_t *__restrict__ src, const uint3
   if (lane == 0 && carry_l != LABEL_NONE) hot_min(s_hl, s_hk, best, carry_l, carry_v);
   __syncthreads();
   hot_flush(s_hl, s_hk, best);
+  if (DEDUP && dd) {  // the block's pair minima join its survivors (4 slots per lane per pass)
+    for (int base = 0; base < DEDUP_SLOTS; base += BLOCK * 4) {
+      uint32_t L[4], D[4], dmask = 0;
+      uint64_t K[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = base + threadIdx.x * 4 + j;
+        const unsigned long long pk = i < DEDUP_SLOTS ? s_dp[i] : ~0ull;
+        L[j] = (uint32_t)(pk >> 32);
+        D[j] = (uint32_t)pk;
+        K[j] = i < DEDUP_SLOTS ? s_dk[i] : KEY_NONE;
+        dmask |= (pk != ~0ull) ? (1u << j) : 0u;
+      }
+      uint32_t lane_excl, wave_before, wave_cnt, total;
+      block_offsets_w((uint32_t)__popc(dmask), s_wcnt, &lane_excl, &wave_before, &wave_cnt, &total);
+      stage_write(s_stage[threadIdx.x / WAVE], L, D, K, dmask, lane_excl, wave_cnt, osrc, odst, okey,
+                  vb + out_n + wave_before);
+      out_n += total;
+    }
+  }
   if (COMPACT) {
     // pad to a multiple of 4 with dead entries; stays inside [vb, vb + Q) and below the capacity
     // (the workspace reserves 4 * SEG_MAX spare entries)
@@ -2372,6 +2435,7 @@ struct ghs_solver {
   std::chrono::steady_clock::time_point t0;
   char *ws_base = nullptr;      // the caller's workspace (carved by workspace_layout)
   bool seed_runs = true;        // level 0 round 0: a-side runs by k_seed_runs (GHS_SEED_RUNS=0: off)
+  uint32_t dedup_max = 0;       // parallel-edge filter at <= this many active fragments (GHS_DEDUP_MAX)
   // dense levels (several ranks, see k_dense_open): the dense arrays, the vertex arrays they stand
   // in for while a level runs, and the level's fragment count
   uint32_t *dlab = nullptr, *dpar = nullptr, *dpos = nullptr, *dvtx = nullptr;
@@ -2919,9 +2983,14 @@ static int enqueue_minedge(ghs_solver *s) {
   } else {
     // fixed grid: every one of the seg_g blocks writes its region's count
     KT(GHS_K_MINEDGE_COMPACT, 0);
-    k_minedge<false, true><<<s->cmp_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, O.src, O.dst,
-                                                          O.key, O.seg_start, O.seg_count, true,
-                                                          s->cfg.num_ranks <= 1 ? cur_act_count(s) : nullptr);
+    const unsigned long long *guard = s->cfg.num_ranks <= 1 ? cur_act_count(s) : nullptr;
+    if (s->dedup_max && s->nact <= DEDUP_BOUND_FACTOR * s->dedup_max)  // few fragments left: the parallel-edge filter
+      k_minedge<false, true, true><<<s->cmp_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, O.src,
+                                                                 O.dst, O.key, O.seg_start, O.seg_count, true, guard,
+                                                                 cur_act_count(s), s->dedup_max);
+    else
+      k_minedge<false, true><<<s->cmp_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, O.src, O.dst,
+                                                            O.key, O.seg_start, O.seg_count, true, guard);
     // the regions' prefix scan is left to the round's hook kernel (or a scan launch before the
     // next consumer): s->scan_pending
     s->scan_pending = true;
@@ -3246,6 +3315,7 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   };
   grid_env("GHS_MINEDGE_G", &s->cmp_g);
   if (const char *sr = getenv("GHS_SEED_RUNS")) s->seed_runs = sr[0] != '0';
+  if (const char *dm = getenv("GHS_DEDUP_MAX")) s->dedup_max = (uint32_t)strtoul(dm, nullptr, 10);
   grid_env("GHS_IDENT_G", &s->ident_g);
   grid_env("GHS_WIN_G", &s->win_g);
   grid_env("GHS_LP_G", &s->lp_g);
@@ -3507,7 +3577,7 @@ int ghs_solver_reset(ghs_solver_t *s) {
   t.n = s->n; t.m = s->m; t.e_lo = s->e_lo; t.e_hi = s->e_hi;
   t.eu = s->eu; t.ev = s->ev; t.ew = s->ew;
   t.in_mst = s->in_mst; t.stream = s->stream; t.cfg = s->cfg;
-  t.debug = s->debug; t.lookahead = s->lookahead; t.seed_runs = s->seed_runs;
+  t.debug = s->debug; t.lookahead = s->lookahead; t.seed_runs = s->seed_runs; t.dedup_max = s->dedup_max;
   { const char *det = getenv("GHS_DETAIL"); t.detail = det && det[0] == '1'; }
   { const char *tr = getenv("GHS_TIME_ROUNDS"); t.time_rounds = tr && tr[0] == '1'; }
   { std::lock_guard<std::mutex> lock(g_prof_mutex); t.prof = g_prof_on; }

@@ -368,6 +368,30 @@ def test_native_loop_emulated_vs_oracle(world, graph, torch_cuda):
     assert len(stats) == res.num_stats
 
 
+@pytest.mark.parametrize("dedup_max", ["128", "1000000000"])
+@pytest.mark.parametrize("graph,world", [("rmat", 1), ("ties", 1), ("forest", 1), ("grid", 1), ("rmat", 4),
+                                         ("ties", 3)])
+def test_parallel_edge_filter_vs_oracle(graph, world, dedup_max, monkeypatch, torch_cuda):
+    """The compacting min-edge's parallel-edge filter (GHS_DEDUP_MAX: per block, survivors between
+    the same two fragments keep only their minimum key) at <= 128 active fragments and in every
+    compacting round: the oracle's MSF, single GPU and through the multi-rank loop."""
+    from distributed_ghs_implementation_amd.device import DeviceMST, emulated_mst
+    monkeypatch.setenv("GHS_DEDUP_MAX", dedup_max)
+    ora = _oracle()
+    e = _test_graph(graph)
+    g = e.to_host()
+    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    if world == 1:
+        eng = DeviceMST(e)
+        res, _ = eng.run()
+        flags = eng.in_mst_host()
+    else:
+        res, _, f = emulated_mst(e, world)
+        flags = f.cpu().numpy().astype(bool)
+    assert np.array_equal(flags, ref_in.astype(bool))
+    assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
+
+
 def test_native_loop_emulated_noncanonical_fails_together(torch_cuda):
     """A non-canonical edge in one rank's range: ghs_mst_emulated returns GHS_E_NONCANON (every
     rank leaves the loop at the same step — no rank left waiting in a collective)."""
