@@ -2669,8 +2669,16 @@ static double level1_auto(const ghs_config_t &c, uint32_t n, uint64_t m) {
 // On the device (k_sample_weights -> k_plan -> d_thr, read by the passes), so the first pass
 // starts without a host round trip; the host's copy (pinned, behind plan_ev) is read only when
 // it needs the number of levels — at the end of level 0 at the earliest.
+// With several ranks every level costs each rank n-sized passes (resolve, select, flag exchange,
+// dense open/close) while its edge work is divided by the ranks: once a rank's share of the list
+// is below 3n edges, two levels (the first as planned, then everything heavier) beat three.
+// R-MAT s26 (n = 2^26), emulated ranks (profiles/r02/plan_s26_*.jsonl): N = 8 (m/N = 2n): 8.29 ->
+// 7.85 ms max-rank compute, 884 -> 825 MB wire per rank; N = 4 (3.9n): 10.85 -> 11.47 ms and
+// N = 2: 16.5 -> 18.6 ms — kept at three there.
 static uint32_t plan_levels_count(const ghs_solver *s) {
-  return std::max<uint32_t>(1, std::min<uint32_t>(s->cfg.max_levels, 32));
+  uint32_t L = std::max<uint32_t>(1, std::min<uint32_t>(s->cfg.max_levels, 32));
+  if (s->cfg.num_ranks > 1 && s->m / s->cfg.num_ranks < 3ull * s->n) L = std::min<uint32_t>(L, 2);
+  return L;
 }
 
 static int plan_levels_enqueue(ghs_solver *s) {
@@ -3392,6 +3400,16 @@ int ghs_solver_exchange_buffer(ghs_solver_t *s, uint8_t **d_flags, uint64_t *byt
 }
 
 int ghs_solver_flag_bits(ghs_solver_t *s, uint64_t **d_bits, uint64_t *words) {
+  if (int rc = ghs_solver_flag_bits_async(s, d_bits, words)) return rc;
+  GHS_HIP_CHECK(hipStreamSynchronize(s->stream));  // complete before the caller's collective reads it
+  return GHS_OK;
+}
+
+}  // extern "C"
+
+// the pack without the trailing sync: for a caller whose collective is enqueued on the solver's
+// own stream (ghs_solver_run)
+int ghs_solver_flag_bits_async(ghs_solver *s, uint64_t **d_bits, uint64_t *words) {
   if (!s || !d_bits || !words) GHS_FAIL(GHS_E_ARG, "solver/d_bits/words is NULL");
   if (!s->pending_exchange) GHS_FAIL(GHS_E_STATE, "no exchange pending");
   const uint64_t nf = (uint64_t)s->n + 1, nw = (nf + 63) / 64;
@@ -3400,11 +3418,12 @@ int ghs_solver_flag_bits(ghs_solver_t *s, uint64_t **d_bits, uint64_t *words) {
     k_pack_flag_bits<<<grid_for(nw, 256, 16384), 256, 0, s->stream>>>(s->flags, nf, s->flag_bits);
   }
   GHS_HIP_CHECK(hipGetLastError());
-  GHS_HIP_CHECK(hipStreamSynchronize(s->stream));  // complete before the caller's collective reads it
   *d_bits = s->flag_bits;
   *words = nw;
   return GHS_OK;
 }
+
+extern "C" {
 
 int ghs_solver_merge_flag_bits(ghs_solver_t *s, const uint64_t *d_all, uint32_t nranks) {
   if (!s || !d_all || nranks == 0) GHS_FAIL(GHS_E_ARG, "solver/d_all is NULL or nranks is 0");

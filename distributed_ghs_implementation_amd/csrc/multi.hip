@@ -196,7 +196,7 @@ int run_loop(ghs_solver_t *s, ghs_comm *c) {
     while (rc == GHS_NEED_EXCHANGE) {  // a level opened: OR its fragment flags (+ error bit)
       uint64_t *bits = nullptr;
       uint64_t words = 0;
-      LOOP_CHECK(ghs_solver_flag_bits(s, &bits, &words));
+      LOOP_CHECK(c->nccl ? ghs_solver_flag_bits_async(s, &bits, &words) : ghs_solver_flag_bits(s, &bits, &words));
       LOOP_CHECK(coll_allgather_u64(c, bits, c->gathered, words, st));
       LOOP_CHECK(ghs_solver_merge_flag_bits(s, c->gathered, nr));
       rc = ghs_solver_minedge(s, &count);

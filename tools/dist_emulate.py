@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--no-ref", action="store_true", help="skip the single-GPU reference (profiling)")
     ap.add_argument("--profile", action="store_true",
                     help="per-launch HIP-event profile of the last rep: kernel ms per round of the max rank")
+    ap.add_argument("--max-levels", type=int, default=None)
+    ap.add_argument("--level-growth", type=float, default=None)
+    ap.add_argument("--level1", type=float, default=None, help="level-1 edges per vertex")
     args = ap.parse_args()
     import torch
     from distributed_ghs_implementation_amd import _native
@@ -47,7 +50,8 @@ def main():
         torch.cuda.empty_cache()
 
     W = args.world
-    cfg = _native.make_config(num_ranks=W)
+    cfg = _native.make_config(num_ranks=W, max_levels=args.max_levels, level_growth=args.level_growth,
+                              level1_edges_per_vertex=args.level1)
     engines = [DeviceMST(e, *edge_range(e.m, r, W), config=cfg) for r in range(W)]
     steppers = [HipStepper(x) for x in engines]
 
