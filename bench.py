@@ -82,10 +82,14 @@ def _first_round(stats, r):
 
 def launch_bytes(rec, stats, res, n):
     k = rec["kernel"]
+    # bucketed heavy edges (pass_flags bit 0): k_select also writes the heavy copy (12 B per edge
+    # not in level 0) and k_filter streams that copy instead of the canonical list
+    heavy = max(res.canon_edges - res.select_out, 0) if res.pass_flags & 1 else 0
     if k == "k_select":
-        return 12.0 * res.canon_edges + 16.0 * res.select_out  # u, v, w stream + level-0 edges out
+        return 12.0 * res.canon_edges + 16.0 * res.select_out + 12.0 * heavy  # u, v, w in; level-0 edges out
     if k == "k_filter":
-        return 12.0 * res.canon_edges + 16.0 * res.filter_out  # stream + level-1 and pending edges out
+        src = heavy if res.pass_flags & 1 else res.canon_edges
+        return 12.0 * src + 16.0 * res.filter_out  # stream + level-1 and pending edges out
     if k == "k_resolve":
         return 8.0 * n + n / 8.0  # lab read + write, giant bitmap
     if k == "k_jump_ident":

@@ -105,7 +105,7 @@ class Result(ctypes.Structure):
         ("rounds", ctypes.c_uint32),
         ("num_stats", ctypes.c_uint32),
         ("levels", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("pass_flags", ctypes.c_uint32),
         ("ms_total", ctypes.c_double),
         ("ms_select", ctypes.c_float),
         ("ms_filter", ctypes.c_float),

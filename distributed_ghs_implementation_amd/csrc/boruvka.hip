@@ -1924,6 +1924,328 @@ GHS_STREAM_KERNEL_6 void k_level_pass(const uint32_t *__restrict__ ru, const uin
 }
 
 // ------------------------------------------------------------------------------------------
+// Heavy-edge buckets (hv). k_filter's cost is its random b-probes of the giant bitmap: one L2
+// request per heavy edge, served at the L2 request rate (~265 G/s from a 2-MiB bitmap, ~121 G/s
+// once the bitmap outgrows an XCD's 4-MiB L2 — s26), and they do not overlap the stream, so the
+// pass costs stream + probes. With the heavy edges grouped by b, every b-probe of a group of
+// blocks falls in one slice of the bitmap: 2^sb vertices (sb <= 20: 128 KiB) held in LDS.
+//  - k_select_hv (opens level 0, the first stream) additionally writes every heavy edge
+//    (w >= level 0's bound) to a heavy copy. A block streams Qb edges (a multiple of HV_GS =
+//    2048), each of its 4 waves a contiguous quarter of them — so the level-0 edges leave in
+//    canonical order, one wave-private segment per quarter, exactly as k_select writes them
+//    (k_seed_runs relies on it). Sort group g of a block = the g-th 512 edges of every quarter:
+//    the group's heavy edges sorted by bucket (b >> sb) through LDS and written contiguously at
+//    the group's own position (no compaction across groups: position = block start + g * HV_GS),
+//    with a table of nb + 1 u16 bucket offsets per group. An entry is 12 B: a,
+//    (b - bucket base) << 11 | (quarter << 9 | offset in the quarter's 512), w.
+//  - k_filter_hv (opens level 1) reads the copy bucket by bucket: the block loads slice k of the
+//    bitmap into LDS, its waves stream the bucket-k sub-runs of their groups, probe b in LDS and
+//    a (sorted within a group's quarter: a few lines) in the L2-resident bitmap.
+// The copy costs one more write of the heavy edges during the first stream; k_filter then reads
+// the copy instead of the canonical list (the same 12 B per edge) with no L2 probes for b.
+// Positions run to the last block's end (< T + Qb): the workspace reserves that slack.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t HV_GS = 2048;        // edges per sort group: 512 from each wave's quarter
+constexpr uint32_t HV_IDX_BITS = 11;    // an entry's quarter and offset in its group
+constexpr uint32_t HV_SB_MAX = 20;      // vertices per bucket <= 2^20 (a 128-KiB bitmap slice)
+constexpr uint32_t HV_NB_MAX = 64;      // buckets
+constexpr uint32_t HV_FBLOCK = 1024;    // k_filter_hv block: 16 waves share one LDS slice
+#ifndef GHS_HV_DEFAULT
+#define GHS_HV_DEFAULT 0
+#endif
+constexpr bool HV_DEFAULT = GHS_HV_DEFAULT != 0;  // env GHS_HV overrides
+static_assert(HV_SB_MAX + HV_IDX_BITS <= 32, "hv entry packing");
+
+// a block's range of k_select_hv (and the decoding in k_filter_hv): gsel blocks, Qb edges each
+__device__ __forceinline__ uint64_t hv_block_edges(uint64_t T, uint32_t gsel) {
+  const uint64_t per = (T + gsel - 1) / gsel;
+  return ((per + HV_GS - 1) / HV_GS) * HV_GS;
+}
+
+__global__ __launch_bounds__(BLOCK, 3) void k_select_hv(uint32_t n, uint64_t e_lo, uint64_t e_hi,
+                                                       const uint32_t *__restrict__ eu, const uint32_t *__restrict__ ev,
+                                                       const uint32_t *__restrict__ ew, const uint64_t *__restrict__ w_hi_p,
+                                                       uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
+                                                       uint64_t *__restrict__ okey, uint64_t *__restrict__ ostart,
+                                                       uint64_t *__restrict__ ocount, uint8_t *__restrict__ mark,
+                                                       unsigned long long *__restrict__ err, uint32_t sb, uint32_t nb,
+                                                       uint32_t *__restrict__ ha, uint32_t *__restrict__ hb,
+                                                       uint32_t *__restrict__ hw, uint16_t *__restrict__ htab) {
+  const uint64_t w_hi = *w_hi_p;
+  __shared__ WaveStage s_stage[BLOCK / WAVE];
+  __shared__ uint32_t s_ha[HV_GS], s_hb[HV_GS], s_hw[HV_GS];
+  __shared__ uint32_t s_cnt[2][HV_NB_MAX + 1];  // bucket counts -> bases, alternating per group
+  const uint32_t lane = threadIdx.x & (WAVE - 1), wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+  const uint64_t E0 = e_lo & ~3ull;
+  const uint64_t T = e_hi - E0;
+  const uint64_t Qb = hv_block_edges(T, gridDim.x);
+  const uint64_t Qw = Qb / 4;                 // a wave's quarter (a multiple of 512)
+  const uint32_t gpb = (uint32_t)(Qb / HV_GS);  // sort groups per block
+  const uint64_t vb = Qb * blockIdx.x;
+  const uint64_t wb = vb + (uint64_t)wid * Qw;  // this wave's quarter [wb, we)
+  const uint64_t we = (wb + Qw < T) ? wb + Qw : (wb < T ? T : wb);
+  const uint64_t eb = E0 + wb;
+  const uint64_t nbytes = (we - wb) * 4;
+  const __amdgpu_buffer_rsrc_t ru = make_rsrc(eu + eb, nbytes);
+  const __amdgpu_buffer_rsrc_t rv = make_rsrc(ev + eb, nbytes);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(ew + eb, nbytes);
+  uint32_t bpa = 0, bpb = 0;  // the edge before the quarter's first (offset -4 is outside the resource)
+  if (eb > 0 && we > wb) {
+    bpa = eu[eb - 1];
+    bpb = ev[eb - 1];
+  }
+  WaveOut wo;  // level-0 edges: the quarter's wave-private segment
+  wo.pos = wb;
+  bool bad = false;
+  for (uint32_t i = threadIdx.x; i < 2 * (HV_NB_MAX + 1); i += BLOCK) (&s_cnt[0][0])[i] = 0;
+  __syncthreads();
+  uint32_t par = 0;
+  const uint32_t ngroups = vb < T ? gpb : 0u;  // every group of a block with edges gets its table row
+  for (uint32_t g = 0; g < ngroups; ++g, par ^= 1) {
+    uint32_t xa[8], xb[8], xw[8], xr[8];  // the lane's heavy edges: a, packed b | idx, w, rank << 8 | bucket
+    uint32_t hmask = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t q = g * 512u + h * 256u + lane * 4u;  // offset in the quarter
+      const uint64_t v = wb + q;  // relative to E0
+      const uint64_t e0 = E0 + v;
+      const uint32_t off = q * 4u;
+      const uint4 ca = ld_b128(ru, off), cb = ld_b128(rv, off), cw = ld_b128(rw, off);
+      uint32_t pa = ld_b32(ru, off - 4), pb = ld_b32(rv, off - 4);
+      if (q == 0) {
+        pa = bpa;
+        pb = bpb;
+      }
+      const uint32_t a[4] = {ca.x, ca.y, ca.z, ca.w}, b[4] = {cb.x, cb.y, cb.z, cb.w}, w[4] = {cw.x, cw.y, cw.z, cw.w};
+      const uint32_t nv = v < we ? (uint32_t)((we - v) < 4 ? (we - v) : 4) : 0u;
+      const uint32_t nskip = e0 < e_lo ? (uint32_t)(e_lo - e0) : 0u;
+      const uint32_t first = (e0 == 0) ? 1u : 0u;
+      bool out[4];
+      uint64_t key[4];
+      uint32_t omask = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bool live = ((uint32_t)j < nv) & ((uint32_t)j >= nskip);
+        const uint32_t ordered = (j == 0 ? first : 0u) | (uint32_t)(pa < a[j]) | ((uint32_t)(pa == a[j]) & (uint32_t)(pb < b[j]));
+        const uint32_t ok = (uint32_t)(a[j] < b[j]) & (uint32_t)(b[j] < n) & ordered;
+        bad |= live & (ok == 0u);
+        live = live & (ok != 0u);  // never index with an unchecked id
+        pa = a[j];
+        pb = b[j];
+        out[j] = live & ((uint64_t)w[j] < w_hi);
+        const bool heavy = live & ((uint64_t)w[j] >= w_hi);
+        omask |= out[j] ? (1u << j) : 0u;
+        key[j] = ((uint64_t)w[j] << 32) | (uint32_t)(e0 + j);
+        if (mark && out[j]) {
+          mark[a[j]] = 1;
+          mark[b[j]] = 1;
+        }
+        const uint32_t k = b[j] >> sb;
+        uint32_t r = 0;
+        if (heavy) r = atomicAdd(&s_cnt[par][k], 1u);
+        xa[h * 4 + j] = a[j];
+        xb[h * 4 + j] = ((b[j] - (k << sb)) << HV_IDX_BITS) | (wid << 9) | (h * 256u + lane * 4u + (uint32_t)j);
+        xw[h * 4 + j] = w[j];
+        xr[h * 4 + j] = (r << 8) | k;
+        hmask |= heavy ? (1u << (h * 4 + j)) : 0u;
+      }
+      wave_append(s_stage[wid], wo, a, b, key, omask, osrc, odst, okey);
+    }
+    __syncthreads();
+    // bucket bases: exclusive scan of the nb counts by wave 0; the group's table row
+    if (wid == 0) {
+      const uint32_t c = lane < nb ? s_cnt[par][lane] : 0u;
+      uint32_t tot;
+      const uint32_t ex = wave_excl_scan(c, &tot);
+      if (lane < nb) s_cnt[par][lane] = ex;
+      if (lane == 0) s_cnt[par][nb] = tot;
+      uint16_t *row = htab + ((uint64_t)blockIdx.x * gpb + g) * (nb + 1);
+      if (lane < nb) row[lane] = (uint16_t)ex;
+      if (lane == WAVE - 1) row[nb] = (uint16_t)tot;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (hmask & (1u << e)) {
+        const uint32_t pos = s_cnt[par][xr[e] & 255u] + (xr[e] >> 8);
+        s_ha[pos] = xa[e];
+        s_hb[pos] = xb[e];
+        s_hw[pos] = xw[e];
+      }
+    }
+    // the other parity's counters were last read before this group's first barrier
+    if (threadIdx.x <= nb) s_cnt[par ^ 1][threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t tot = s_cnt[par][nb];
+    const uint64_t gpos = vb + (uint64_t)g * HV_GS;
+    for (uint32_t i = threadIdx.x; i < tot; i += BLOCK) {
+      ha[gpos + i] = s_ha[i];
+      hb[gpos + i] = s_hb[i];
+      hw[gpos + i] = s_hw[i];
+    }
+  }
+  if (bad) atomicOr(err, 8ull);
+  wave_finish(s_stage[wid], wo, osrc, odst, okey, wb, wb < T, ostart, ocount, blockIdx.x * (BLOCK / WAVE) + wid);
+}
+
+// FILTER over the heavy copy (see above): same decisions and outputs as k_filter (level-1 edges
+// relabelled, heavier survivors pending as u, v, key), one output segment per wave (its groups'
+// positions), segments ordered by bucket within a wave.
+__global__ __launch_bounds__(HV_FBLOCK) void k_filter_hv(
+    uint64_t e_lo, uint64_t e_hi, uint32_t sb, uint32_t nb, const uint32_t *__restrict__ ha,
+    const uint32_t *__restrict__ hb, const uint32_t *__restrict__ hw, const uint16_t *__restrict__ htab,
+    uint32_t gsel, const uint64_t *__restrict__ w_range, const uint64_t *__restrict__ giant_bits, uint64_t bits_words,
+    const uint32_t *__restrict__ giant_ptr, const uint32_t *__restrict__ lab, uint32_t *__restrict__ lsrc,
+    uint32_t *__restrict__ ldst, uint64_t *__restrict__ lkey, uint64_t *__restrict__ lstart,
+    uint64_t *__restrict__ lcount, uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
+    uint64_t *__restrict__ okey, uint64_t *__restrict__ ostart, uint64_t *__restrict__ ocount,
+    uint8_t *__restrict__ mark) {
+  __shared__ uint32_t s_bits[1u << (HV_SB_MAX - 5)];
+  const uint64_t w_hi = w_range[1];
+  const uint32_t lane = threadIdx.x & (WAVE - 1), wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+  const uint64_t E0 = e_lo & ~3ull;
+  const uint64_t T = e_hi - E0;
+  const uint64_t Qb = hv_block_edges(T, gsel), Qw = Qb / 4;  // k_select_hv's blocks
+  const uint64_t gpb = Qb / HV_GS;
+  const uint64_t NG = ((T + Qb - 1) / Qb) * gpb;  // the groups of every block with edges
+  const uint64_t W = (uint64_t)gridDim.x * (HV_FBLOCK / WAVE);
+  const uint64_t gw = (uint64_t)blockIdx.x * (HV_FBLOCK / WAVE) + wid;
+  const uint64_t gA = NG * gw / W, gB = NG * (gw + 1) / W;  // this wave's groups
+  const uint64_t seg_begin = gA * HV_GS;
+  const uint32_t *bits32 = reinterpret_cast<const uint32_t *>(giant_bits);
+  const uint32_t giant = giant_ptr[0];
+  const uint32_t swords = 1u << (sb - 5);
+  bool touch_giant = false;
+  uint64_t nlev = 0, nrem = 0;
+  for (uint32_t k = 0; k < nb; ++k) {
+    __syncthreads();  // every wave is done with the previous slice
+    const uint64_t w0 = (uint64_t)k * swords;
+    for (uint32_t i = threadIdx.x; i < swords; i += HV_FBLOCK) s_bits[i] = (w0 + i < bits_words) ? bits32[w0 + i] : 0u;
+    __syncthreads();
+    for (uint64_t gc = gA; gc < gB; gc += WAVE) {
+      // lane i: group gc + i's bucket-k sub-run [st, st + len); c = its start in the wave's
+      // virtual stream of sub-runs
+      const uint64_t gl = gc + lane;
+      const bool ing = gl < gB;
+      const uint32_t o0 = ing ? htab[gl * (nb + 1) + k] : 0u, o1 = ing ? htab[gl * (nb + 1) + k + 1] : 0u;
+      uint32_t E;
+      const uint32_t c = wave_excl_scan(o1 - o0, &E);
+      const uint32_t st = (uint32_t)(gl * HV_GS) + o0;
+      // eid of a group's entry = its quarter's first edge + the offset: E0 + block * Qb +
+      // quarter * Qw + g * 512 + offset
+      const uint64_t ebase = E0 + (gl / gpb) * Qb + (gl % gpb) * 512u;
+      for (uint32_t x0 = 0; x0 < E; x0 += 4 * WAVE) {
+        uint32_t p[4];
+        uint64_t eb[4];
+        bool val[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t x = x0 + lane + WAVE * j;
+          val[j] = x < E;
+          int lo = 0;  // the last sub-run starting at or before x (non-empty: the next starts after x)
+#pragma unroll
+          for (int s = 32; s >= 1; s >>= 1) {
+            const int cand = lo + s;
+            const uint32_t cv = __shfl(c, cand & (WAVE - 1));
+            if (cand < WAVE && cv <= x) lo = cand;
+          }
+          // every lane shuffles (a bpermute from a lane switched off by a branch reads 0)
+          const uint32_t sp = __shfl(st, lo), cp = __shfl(c, lo);
+          p[j] = val[j] ? sp + (x - cp) : 0u;
+          eb[j] = __shfl(ebase, lo);
+        }
+        uint32_t A[4], Bp[4], Wt[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          A[j] = ha[p[j]];
+          Bp[j] = hb[p[j]];
+          Wt[j] = hw[p[j]];
+        }
+        uint32_t abw[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) abw[j] = bits32[val[j] ? (A[j] >> 5) : 0u];
+        uint32_t b[4], ga[4], gb[4], la[4], lb[4];
+        uint64_t key[4];
+        bool lev[4], rem[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t bl = Bp[j] >> HV_IDX_BITS;
+          b[j] = (k << sb) + bl;
+          ga[j] = (abw[j] >> (A[j] & 31)) & 1u;
+          const uint32_t blv = val[j] ? bl : 0u;  // a dead lane's entry is not read
+          gb[j] = (s_bits[blv >> 5] >> (blv & 31)) & 1u;
+          const bool keep = val[j] & ((ga[j] & gb[j]) == 0u);
+          const uint32_t idx = Bp[j] & ((1u << HV_IDX_BITS) - 1);
+          const uint64_t eid = eb[j] + (idx >> 9) * Qw + (idx & 511u);
+          key[j] = ((uint64_t)Wt[j] << 32) | (uint32_t)eid;
+          lev[j] = keep & ((uint64_t)Wt[j] < w_hi);
+          rem[j] = keep & !lev[j];
+          la[j] = lab[(lev[j] & (ga[j] == 0u)) ? A[j] : 0u];
+          lb[j] = lab[(lev[j] & (gb[j] == 0u)) ? b[j] : 0u];
+          la[j] = ga[j] ? giant : la[j];
+          lb[j] = gb[j] ? giant : lb[j];
+        }
+        uint32_t lmask = 0, rmask = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          lev[j] = lev[j] & (la[j] != lb[j]);
+          lmask |= lev[j] ? (1u << j) : 0u;
+          rmask |= rem[j] ? (1u << j) : 0u;
+          if (lev[j] && mark) {
+            if (!ga[j]) mark[la[j]] = 1;
+            if (!gb[j]) mark[lb[j]] = 1;
+            touch_giant |= (ga[j] | gb[j]) != 0u;
+          }
+        }
+        // wave-private appends: both counts from one packed scan
+        uint32_t tot;
+        const uint32_t ex = wave_excl_scan((uint32_t)__popc(lmask) | ((uint32_t)__popc(rmask) << 16), &tot);
+        uint64_t pl = seg_begin + nlev + (ex & 0xffffu), pr = seg_begin + nrem + (ex >> 16);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (lmask & (1u << j)) {
+            lsrc[pl] = la[j];
+            ldst[pl] = lb[j];
+            lkey[pl] = key[j];
+            ++pl;
+          }
+          if (rmask & (1u << j)) {
+            osrc[pr] = A[j];
+            odst[pr] = b[j];
+            okey[pr] = key[j];
+            ++pr;
+          }
+        }
+        nlev += tot & 0xffffu;
+        nrem += tot >> 16;
+      }
+    }
+  }
+  if (__syncthreads_or(touch_giant ? 1 : 0) && threadIdx.x == 0 && mark) mark[giant] = 1;
+  // both outputs padded to a multiple of 4 with dead entries (a = LABEL_NONE); the segment's
+  // span (its groups' positions) always leaves room (a multiple of 4 >= its entries)
+  const uint64_t padded = (nrem + 3) & ~3ull, lpadded = (nlev + 3) & ~3ull;
+  if (lane < padded - nrem) {
+    const uint64_t pos = seg_begin + nrem + lane;
+    osrc[pos] = LABEL_NONE;
+    odst[pos] = 0;
+    okey[pos] = KEY_NONE;
+  }
+  if (lane < lpadded - nlev) {
+    const uint64_t pos = seg_begin + nlev + lane;
+    lsrc[pos] = LABEL_NONE;
+    ldst[pos] = 0;
+    lkey[pos] = KEY_NONE;
+  }
+  if (lane == 0) {
+    lstart[gw] = seg_begin;
+    lcount[gw] = lpadded;
+    ostart[gw] = seg_begin;
+    ocount[gw] = padded;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Dense levels (several ranks). Once a level's active list A (nact0 fragment roots, identical on
 // every rank) is selected, the level runs in a dense label space 0..nact0-1: pos[A[i]] = i, the
 // rank's level edges are relabelled through pos, and best / lab / par become nact0-sized arrays.
@@ -2436,6 +2758,12 @@ struct ghs_solver {
   char *ws_base = nullptr;      // the caller's workspace (carved by workspace_layout)
   bool seed_runs = true;        // level 0 round 0: a-side runs by k_seed_runs (GHS_SEED_RUNS=0: off)
   uint32_t dedup_max = 0;       // parallel-edge filter at <= this many active fragments (GHS_DEDUP_MAX)
+  // heavy-edge buckets (k_select_hv / k_filter_hv): on when the plan has >= 2 levels and the
+  // vertices span 2..HV_NB_MAX buckets of 2^hv_sb (GHS_HV=0: off; GHS_HV_SB: bucket size, tests)
+  bool hv = false;
+  bool hv_env = HV_DEFAULT;
+  uint32_t hv_sb = HV_SB_MAX, hv_nb = 0;
+  uint32_t hv_gsel = 1;         // k_select_hv's grid (k_filter_hv decodes the eids from it)
   // dense levels (several ranks, see k_dense_open): the dense arrays, the vertex arrays they stand
   // in for while a level runs, and the level's fragment count
   uint32_t *dlab = nullptr, *dpar = nullptr, *dpos = nullptr, *dvtx = nullptr;
@@ -2551,7 +2879,8 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
     return p;
   };
   const size_t N = (size_t)n;
-  const uint64_t cap = local_edges + 4 * SEG_MAX;  // a level's edges (+ padding of the regions)
+  // a level's edges (+ padding of the regions, + the heavy copy's last block: < T/256 + 2 groups)
+  const uint64_t cap = local_edges + 4 * SEG_MAX + local_edges / 256 + 2 * 2048;
   char *p;
   p = carve(N * 4); if (s) s->lab = (uint32_t *)p;
   p = carve(N * 4); if (s) s->par = (uint32_t *)p;
@@ -2715,6 +3044,15 @@ static bool levels_done(ghs_solver *s) {
   return s->level + 1 >= s->thresholds.size();
 }
 
+// the heavy copy (k_select_hv -> k_filter_hv) lives in the pending buffer rem[0], unused until
+// k_filter writes the pending edges to rem[1]: a -> src, packed b | idx -> dst, w -> the first
+// half of key (as u32), the groups' bucket tables after it
+constexpr uint32_t HV_FILTER_G = 256;  // k_filter_hv blocks: one per CU (128-KiB LDS slice each)
+static inline uint32_t *hv_w(ghs_solver *s) { return reinterpret_cast<uint32_t *>(s->rem[0].key); }
+static inline uint16_t *hv_tab(ghs_solver *s) {
+  return reinterpret_cast<uint16_t *>(reinterpret_cast<uint32_t *>(s->rem[0].key) + s->cap_arcs);
+}
+
 static int fail_counters(ghs_solver *s, unsigned long long err, const char *where) {
   s->phase = 2;
   if (err & 8) GHS_FAIL(GHS_E_NONCANON, "edge list is not canonical (need u < v < n, strictly ascending (u, v))");
@@ -2771,8 +3109,14 @@ static int open_level(ghs_solver *s, bool async_open = false) {
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[0], st));
       {
         KT(GHS_K_SELECT, TC);
-        k_select<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range + 1, Y.src, Y.dst, Y.key,
-                                      Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR);
+        s->hv_gsel = G;
+        if (s->hv)  // + the heavy copy, grouped by bucket of b, into rem[0] (read by k_filter_hv)
+          k_select_hv<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range + 1, Y.src, Y.dst,
+                                           Y.key, Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR, s->hv_sb, s->hv_nb,
+                                           s->rem[0].src, s->rem[0].dst, hv_w(s), hv_tab(s));
+        else
+          k_select<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range + 1, Y.src, Y.dst, Y.key,
+                                        Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR);
       }
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[1], st));
       GHS_HIP_CHECK(hipGetLastError());
@@ -2790,14 +3134,23 @@ static int open_level(ghs_solver *s, bool async_open = false) {
     if (!s->pending_built) {
       // FILTER + level split over the canonical list once level 0 is complete: level-1 edges
       // not inside one fragment -> Y; heavier edges not inside the giant -> pending (rem[rout])
-      G = grid_for(TC, ARCS_PER_BLOCK, s->seg_g);
+      G = s->hv ? HV_FILTER_G * (HV_FBLOCK / WAVE) : grid_for(TC, ARCS_PER_BLOCK, s->seg_g);
       if (TC) {
         GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[2], st));
         {
         KT(GHS_K_FILTER, TC);
-        k_filter<<<G, BLOCK, 0, st>>>(s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range, s->bits, s->giant, s->lab,
-                                      Y.src, Y.dst, Y.key, Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key,
-                                      RO.seg_start, RO.seg_count, mark);
+        if (s->hv) {  // the heavy copy of k_select_hv (rem[0]); one output region per wave
+          if (rin != 0) GHS_FAIL(GHS_E_STATE, "heavy copy: pending buffers in use");
+          k_filter_hv<<<HV_FILTER_G, HV_FBLOCK, 0, st>>>(s->e_lo, s->e_hi, s->hv_sb, s->hv_nb, s->rem[0].src, s->rem[0].dst,
+                                                        hv_w(s), hv_tab(s), s->hv_gsel, d_range, s->bits,
+                                                        ((uint64_t)s->n + 127) / 128 * 4, s->giant, s->lab, Y.src,
+                                                        Y.dst, Y.key, Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key,
+                                                        RO.seg_start, RO.seg_count, mark);
+        } else {
+          k_filter<<<G, BLOCK, 0, st>>>(s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range, s->bits, s->giant, s->lab,
+                                        Y.src, Y.dst, Y.key, Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key,
+                                        RO.seg_start, RO.seg_count, mark);
+        }
         }
         GHS_HIP_CHECK(hipGetLastError());
         GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[3], st));
@@ -3276,6 +3629,8 @@ static int solver_begin(ghs_solver *s) {
   if ((e = hipMemsetAsync(s->lb_state, 0, LB_MAX_TILES * 8, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset select state: ") + hipGetErrorString(e));
   k_init_counters<<<1, 64, 0, s->stream>>>(s->cnt, n);
   if ((e = hipGetLastError()) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("init kernels: ") + hipGetErrorString(e));
+  s->hv_nb = (uint32_t)(((uint64_t)n + (1ull << s->hv_sb) - 1) >> s->hv_sb);
+  s->hv = s->hv_env && s->hv_nb >= 2 && s->hv_nb <= HV_NB_MAX && plan_levels_count(s) >= 2 && s->e_hi > s->e_lo;
   s->level = 0;
   s->level_open = false;
   s->phase = n ? 0 : 2;
@@ -3324,6 +3679,11 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   grid_env("GHS_MINEDGE_G", &s->cmp_g);
   if (const char *sr = getenv("GHS_SEED_RUNS")) s->seed_runs = sr[0] != '0';
   if (const char *dm = getenv("GHS_DEDUP_MAX")) s->dedup_max = (uint32_t)strtoul(dm, nullptr, 10);
+  if (const char *h = getenv("GHS_HV")) s->hv_env = h[0] != '0';
+  if (const char *h = getenv("GHS_HV_SB")) {
+    const long v = strtol(h, nullptr, 10);
+    s->hv_sb = (uint32_t)(v < 5 ? 5 : (v > (long)HV_SB_MAX ? HV_SB_MAX : v));
+  }
   grid_env("GHS_IDENT_G", &s->ident_g);
   grid_env("GHS_WIN_G", &s->win_g);
   grid_env("GHS_LP_G", &s->lp_g);
@@ -3585,6 +3945,7 @@ int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *
     result->canon_edges = s->e_hi - s->e_lo;
     result->select_out = s->select_out;
     result->filter_out = s->filter_out;
+    result->pass_flags = s->hv ? 1u : 0u;
   }
   return GHS_OK;
 }
@@ -3597,6 +3958,7 @@ int ghs_solver_reset(ghs_solver_t *s) {
   t.eu = s->eu; t.ev = s->ev; t.ew = s->ew;
   t.in_mst = s->in_mst; t.stream = s->stream; t.cfg = s->cfg;
   t.debug = s->debug; t.lookahead = s->lookahead; t.seed_runs = s->seed_runs; t.dedup_max = s->dedup_max;
+  t.hv_env = s->hv_env; t.hv_sb = s->hv_sb;
   { const char *det = getenv("GHS_DETAIL"); t.detail = det && det[0] == '1'; }
   { const char *tr = getenv("GHS_TIME_ROUNDS"); t.time_rounds = tr && tr[0] == '1'; }
   { std::lock_guard<std::mutex> lock(g_prof_mutex); t.prof = g_prof_on; }

@@ -68,7 +68,8 @@ typedef struct ghs_result {
   uint32_t rounds;            /* Boruvka rounds executed (all levels) */
   uint32_t num_stats;         /* entries filled in the stats array (<= GHS_MAX_ROUND_STATS) */
   uint32_t levels;            /* weight levels planned */
-  uint32_t reserved;
+  uint32_t pass_flags;        /* bit 0: the heavy edges went through the bucketed passes
+                                 (k_select_hv writes them grouped by b, k_filter_hv reads them) */
   double ms_total;            /* host wall time of the solve (device-resident input -> flags) */
   /* The two full streams over the canonical list (HIP events on the solve's stream). */
   float ms_select;            /* k_select: validation + level-0 split */

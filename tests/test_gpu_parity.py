@@ -334,6 +334,8 @@ def _test_graph(graph):
     from distributed_ghs_implementation_amd.device import DeviceEdges, generate_grid, generate_rmat
     if graph == "rmat":
         return generate_rmat(15, 16, seed=3, wseed=4)
+    if graph == "rmat20":  # the bucketed filter's waves hold several groups each
+        return generate_rmat(20, 24, seed=5, wseed=6)
     if graph == "readme":  # 9 edges: most of 8 ranks own no edge at all
         return DeviceEdges.from_host(canonicalize(6, edges=[(0, 1, 1), (0, 2, 4), (1, 2, 2), (1, 3, 5), (2, 3, 3),
                                                             (2, 4, 7), (3, 4, 6), (3, 5, 8), (4, 5, 9)]))
@@ -390,6 +392,56 @@ def test_parallel_edge_filter_vs_oracle(graph, world, dedup_max, monkeypatch, to
         flags = f.cpu().numpy().astype(bool)
     assert np.array_equal(flags, ref_in.astype(bool))
     assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
+
+
+@pytest.mark.parametrize("graph,world", [("rmat", 1), ("ties", 1), ("forest", 1), ("grid", 1), ("grid-gradient", 1),
+                                         ("rmat", 4), ("ties", 3), ("forest", 2), ("rmat20", 1), ("rmat20", 3)])
+def test_heavy_buckets_vs_oracle(graph, world, monkeypatch, torch_cuda):
+    """The bucketed heavy-edge passes (k_select_hv writes the heavy edges grouped by bucket of b,
+    k_filter_hv probes b in an LDS slice of the giant bitmap), forced onto small graphs by a small
+    bucket (GHS_HV_SB: ~32 buckets): the oracle's MSF, single GPU and through the multi-rank loop,
+    and the same flags as the unbucketed passes."""
+    from distributed_ghs_implementation_amd.device import DeviceMST, emulated_mst
+    ora = _oracle()
+    e = _test_graph(graph)
+    g = e.to_host()
+    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    sb = max(5, int(np.ceil(np.log2(max(g.n, 2) / 32.0))))
+    assert 2 <= -(-g.n // (1 << sb)) <= 64
+
+    def solve():
+        if world == 1:
+            eng = DeviceMST(e)
+            res, _ = eng.run()
+            return res, eng.in_mst_host()
+        res, _, f = emulated_mst(e, world)
+        return res, f.cpu().numpy().astype(bool)
+
+    monkeypatch.setenv("GHS_HV", "1")
+    monkeypatch.setenv("GHS_HV_SB", str(sb))
+    res, flags = solve()
+    assert res.pass_flags & 1, "the bucketed passes did not run"
+    assert np.array_equal(flags, ref_in.astype(bool))
+    assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
+    monkeypatch.setenv("GHS_HV", "0")
+    res0, flags0 = solve()
+    assert not res0.pass_flags & 1
+    assert np.array_equal(flags0, flags) and res0.total_weight == res.total_weight
+
+
+def test_heavy_buckets_noncanonical_rejected(monkeypatch, torch_cuda):
+    """k_select_hv validates the list like k_select: a non-canonical edge fails the solve."""
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import DeviceEdges, DeviceMST, generate_rmat
+    monkeypatch.setenv("GHS_HV", "1")
+    monkeypatch.setenv("GHS_HV_SB", "10")
+    e = generate_rmat(15, 16, seed=3, wseed=4)
+    for pos in (0, e.m // 2, e.m - 1):
+        v = e.v.clone()
+        v[pos] = e.u[pos]  # u == v
+        with pytest.raises(_native.GHSError) as ei:
+            DeviceMST(DeviceEdges(e.n, e.u, v, e.w)).run()
+        assert ei.value.code == _native.GHS_E_NONCANON
 
 
 def test_native_loop_emulated_noncanonical_fails_together(torch_cuda):
