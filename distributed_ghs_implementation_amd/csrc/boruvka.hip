@@ -2001,17 +2001,38 @@ __global__ __launch_bounds__(BLOCK, 3) void k_select_hv(uint32_t n, uint64_t e_l
   __syncthreads();
   uint32_t par = 0;
   const uint32_t ngroups = vb < T ? gpb : 0u;  // every group of a block with edges gets its table row
+  // the group's two tiles per wave, prefetched one group ahead (past the quarter: reads 0)
+  uint4 fa[2], fb[2], fw[2];
+  uint32_t fpa[2], fpb[2];
+  auto fetch = [&](uint32_t g) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t off = (g * 512u + h * 256u + lane * 4u) * 4u;
+      fa[h] = ld_b128(ru, off);
+      fb[h] = ld_b128(rv, off);
+      fw[h] = ld_b128(rw, off);
+      fpa[h] = ld_b32(ru, off - 4);
+      fpb[h] = ld_b32(rv, off - 4);
+    }
+  };
+  fetch(0);
   for (uint32_t g = 0; g < ngroups; ++g, par ^= 1) {
     uint32_t xa[8], xb[8], xw[8], xr[8];  // the lane's heavy edges: a, packed b | idx, w, rank << 8 | bucket
     uint32_t hmask = 0;
+    uint4 ta[2], tb[2], tw[2];
+    uint32_t tpa[2], tpb[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      ta[h] = fa[h]; tb[h] = fb[h]; tw[h] = fw[h]; tpa[h] = fpa[h]; tpb[h] = fpb[h];
+    }
+    fetch(g + 1);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const uint32_t q = g * 512u + h * 256u + lane * 4u;  // offset in the quarter
       const uint64_t v = wb + q;  // relative to E0
       const uint64_t e0 = E0 + v;
-      const uint32_t off = q * 4u;
-      const uint4 ca = ld_b128(ru, off), cb = ld_b128(rv, off), cw = ld_b128(rw, off);
-      uint32_t pa = ld_b32(ru, off - 4), pb = ld_b32(rv, off - 4);
+      const uint4 ca = ta[h], cb = tb[h], cw = tw[h];
+      uint32_t pa = tpa[h], pb = tpb[h];
       if (q == 0) {
         pa = bpa;
         pb = bpb;
@@ -2083,6 +2104,9 @@ __global__ __launch_bounds__(BLOCK, 3) void k_select_hv(uint32_t n, uint64_t e_l
       hb[gpos + i] = s_hb[i];
       hw[gpos + i] = s_hw[i];
     }
+    // the prefetched group has landed by now (waited here, not at the loop head)
+    asm volatile("" ::"v"(fa[0].x), "v"(fb[0].x), "v"(fw[0].x), "v"(fa[1].x), "v"(fb[1].x), "v"(fw[1].x), "v"(fpa[0]),
+                 "v"(fpb[0]), "v"(fpa[1]), "v"(fpb[1]));
   }
   if (bad) atomicOr(err, 8ull);
   wave_finish(s_stage[wid], wo, osrc, odst, okey, wb, wb < T, ostart, ocount, blockIdx.x * (BLOCK / WAVE) + wid);
@@ -2090,7 +2114,15 @@ __global__ __launch_bounds__(BLOCK, 3) void k_select_hv(uint32_t n, uint64_t e_l
 
 // FILTER over the heavy copy (see above): same decisions and outputs as k_filter (level-1 edges
 // relabelled, heavier survivors pending as u, v, key), one output segment per wave (its groups'
-// positions), segments ordered by bucket within a wave.
+// positions), ordered by bucket within a wave. A wave streams its groups' bucket-k sub-runs as
+// one virtual stream (lane i holds group i's sub-run start c_i; an entry finds its group by a
+// binary search over the lanes), HV_EPL entries per lane per iteration, software-pipelined: the
+// a-probes and label gathers of iteration i are issued before the loads of iteration i + 1, so
+// waiting for them leaves those loads in flight.
+#ifndef GHS_HV_EPL
+#define GHS_HV_EPL 4
+#endif
+constexpr int HV_EPL = GHS_HV_EPL;
 __global__ __launch_bounds__(HV_FBLOCK) void k_filter_hv(
     uint64_t e_lo, uint64_t e_hi, uint32_t sb, uint32_t nb, const uint32_t *__restrict__ ha,
     const uint32_t *__restrict__ hb, const uint32_t *__restrict__ hw, const uint16_t *__restrict__ htab,
@@ -2100,7 +2132,7 @@ __global__ __launch_bounds__(HV_FBLOCK) void k_filter_hv(
     uint64_t *__restrict__ lcount, uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
     uint64_t *__restrict__ okey, uint64_t *__restrict__ ostart, uint64_t *__restrict__ ocount,
     uint8_t *__restrict__ mark) {
-  __shared__ uint32_t s_bits[1u << (HV_SB_MAX - 5)];
+  __shared__ __attribute__((aligned(16))) uint32_t s_bits[1u << (HV_SB_MAX - 5)];
   const uint64_t w_hi = w_range[1];
   const uint32_t lane = threadIdx.x & (WAVE - 1), wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const uint64_t E0 = e_lo & ~3ull;
@@ -2115,109 +2147,193 @@ __global__ __launch_bounds__(HV_FBLOCK) void k_filter_hv(
   const uint32_t *bits32 = reinterpret_cast<const uint32_t *>(giant_bits);
   const uint32_t giant = giant_ptr[0];
   const uint32_t swords = 1u << (sb - 5);
+  // the wave's output segments (its groups' positions) as buffer resources: masked lanes store
+  // to ST_DROP, so every output store is issued every iteration
+  const uint64_t span = (gB - gA) * HV_GS;
+  const __amdgpu_buffer_rsrc_t rls = make_rsrc_u32(lsrc + seg_begin, span * 4), rld = make_rsrc_u32(ldst + seg_begin, span * 4);
+  const __amdgpu_buffer_rsrc_t rlk = make_rsrc_u32(lkey + seg_begin, span * 8);
+  const __amdgpu_buffer_rsrc_t ros = make_rsrc_u32(osrc + seg_begin, span * 4), rod = make_rsrc_u32(odst + seg_begin, span * 4);
+  const __amdgpu_buffer_rsrc_t rok = make_rsrc_u32(okey + seg_begin, span * 8);
+  const __amdgpu_buffer_rsrc_t rmark = make_rsrc_u32(mark, mark ? bits_words * 32 : 0);  // labels < n
   bool touch_giant = false;
   uint64_t nlev = 0, nrem = 0;
   for (uint32_t k = 0; k < nb; ++k) {
     __syncthreads();  // every wave is done with the previous slice
-    const uint64_t w0 = (uint64_t)k * swords;
-    for (uint32_t i = threadIdx.x; i < swords; i += HV_FBLOCK) s_bits[i] = (w0 + i < bits_words) ? bits32[w0 + i] : 0u;
+    {
+      // slice k: 16-B loads, all of a thread's issued before any is stored (one round trip; the
+      // bitmap buffer is 16-B aligned and padded to whole 16-B words)
+      const uint4 *src4 = reinterpret_cast<const uint4 *>(bits32 + (uint64_t)k * swords);
+      const uint64_t avail4 = bits_words > (uint64_t)k * swords ? (bits_words - (uint64_t)k * swords) / 4 : 0;
+      uint4 *dst4 = reinterpret_cast<uint4 *>(s_bits);
+      constexpr uint32_t PER = (1u << (HV_SB_MAX - 5)) / 4 / HV_FBLOCK;  // 8 at the largest slice
+      uint4 t[PER];
+#pragma unroll
+      for (uint32_t r = 0; r < PER; ++r) {
+        const uint32_t i = threadIdx.x + r * HV_FBLOCK;
+        t[r] = (i < swords / 4 && i < avail4) ? src4[i] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (uint32_t r = 0; r < PER; ++r) {
+        const uint32_t i = threadIdx.x + r * HV_FBLOCK;
+        if (i < swords / 4) dst4[i] = t[r];
+      }
+    }
     __syncthreads();
     for (uint64_t gc = gA; gc < gB; gc += WAVE) {
-      // lane i: group gc + i's bucket-k sub-run [st, st + len); c = its start in the wave's
-      // virtual stream of sub-runs
+      // lane i: group gc + i's bucket-k sub-run [st, st + len), its start c in the wave's virtual
+      // stream, and the eid of its quarter-0 edge 0 (eid = ebase + quarter * Qw + offset)
       const uint64_t gl = gc + lane;
       const bool ing = gl < gB;
       const uint32_t o0 = ing ? htab[gl * (nb + 1) + k] : 0u, o1 = ing ? htab[gl * (nb + 1) + k + 1] : 0u;
       uint32_t E;
       const uint32_t c = wave_excl_scan(o1 - o0, &E);
       const uint32_t st = (uint32_t)(gl * HV_GS) + o0;
-      // eid of a group's entry = its quarter's first edge + the offset: E0 + block * Qb +
-      // quarter * Qw + g * 512 + offset
-      const uint64_t ebase = E0 + (gl / gpb) * Qb + (gl % gpb) * 512u;
-      for (uint32_t x0 = 0; x0 < E; x0 += 4 * WAVE) {
-        uint32_t p[4];
-        uint64_t eb[4];
-        bool val[4];
+      const uint32_t ebase = (uint32_t)(E0 + (gl / gpb) * Qb + (gl % gpb) * 512u);  // m < 2^31
+      // entry x = x0 + lane + 64 j of the virtual stream -> position p, eid base eb (every lane
+      // runs every shuffle: a bpermute from a lane switched off by a branch reads 0)
+      // the next sub-run's start (c of lane i + 1; E past the last) and the position offset
+      const uint32_t cnext = lane == WAVE - 1 ? E : __shfl_down(c, 1);
+      const uint32_t delta = st - c;  // position = x + delta within the sub-run
+      auto locate = [&](uint32_t x0, uint32_t *p, uint32_t *eb) {
+        int lo = 0;  // the last sub-run starting at or before x (non-empty: the next starts after x)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < HV_EPL; ++j) {
           const uint32_t x = x0 + lane + WAVE * j;
-          val[j] = x < E;
-          int lo = 0;  // the last sub-run starting at or before x (non-empty: the next starts after x)
+          if (j == 0) {
 #pragma unroll
-          for (int s = 32; s >= 1; s >>= 1) {
-            const int cand = lo + s;
-            const uint32_t cv = __shfl(c, cand & (WAVE - 1));
-            if (cand < WAVE && cv <= x) lo = cand;
+            for (int s = 32; s >= 1; s >>= 1) {
+              const int cand = lo + s;
+              const uint32_t cv = __shfl(c, cand & (WAVE - 1));
+              if (cand < WAVE && cv <= x) lo = cand;
+            }
+          } else {
+            // 64 entries later: one or two sub-runs further on (sub-runs of >= 32 entries), else
+            // a fresh search from here
+            const uint32_t n1 = __shfl(cnext, lo);
+            if (n1 <= x && lo < WAVE - 1) ++lo;
+            const uint32_t n2 = __shfl(cnext, lo);
+            if (n2 <= x && lo < WAVE - 1) ++lo;
+            const uint32_t n3 = __shfl(cnext, lo);
+            if (__any(n3 <= x && lo < WAVE - 1)) {
+              int l2 = 0;
+#pragma unroll
+              for (int s = 32; s >= 1; s >>= 1) {
+                const int cand = l2 + s;
+                const uint32_t cv = __shfl(c, cand & (WAVE - 1));
+                if (cand < WAVE && cv <= x) l2 = cand;
+              }
+              lo = l2;
+            }
           }
-          // every lane shuffles (a bpermute from a lane switched off by a branch reads 0)
-          const uint32_t sp = __shfl(st, lo), cp = __shfl(c, lo);
-          p[j] = val[j] ? sp + (x - cp) : 0u;
-          eb[j] = __shfl(ebase, lo);
+          const uint32_t dp = __shfl(delta, lo), ep = __shfl(ebase, lo);
+          p[j] = x < E ? x + dp : 0u;
+          eb[j] = ep;
         }
-        uint32_t A[4], Bp[4], Wt[4];
+      };
+      // Three-stage pipeline over chunks of HV_EPL x 64 entries; iteration `it` stores chunk it-2
+      // (its label gathers landed), decides chunk it-1 (its a-probes landed) and issues its label
+      // gathers, issues chunk it's a-probes (its loads landed) and chunk it+1's loads. Every stage
+      // runs every iteration (dead lanes read index 0, stores to a dropped offset), so the number
+      // of memory instructions per iteration is fixed and each wait is a counted vmcnt that leaves
+      // the later stages' requests in flight.
+      constexpr uint32_t CH = HV_EPL * WAVE;
+      const uint32_t niter = (E + CH - 1) / CH;
+      uint32_t dA[HV_EPL], dB[HV_EPL], dW[HV_EPL], dE[HV_EPL];                 // chunk it: loads
+      uint32_t rA[HV_EPL], rB[HV_EPL], rW[HV_EPL], rE[HV_EPL], rP[HV_EPL];     // it-1: a-probes
+      uint32_t qA[HV_EPL], qB[HV_EPL], qW[HV_EPL], qE[HV_EPL], qla[HV_EPL], qlb[HV_EPL];  // it-2: gathers
+      uint32_t dv = 0, rv = 0, qlev = 0, qrem = 0, qga = 0, qgb = 0;  // per-entry bits (j)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          A[j] = ha[p[j]];
-          Bp[j] = hb[p[j]];
-          Wt[j] = hw[p[j]];
+      for (int j = 0; j < HV_EPL; ++j) {
+        rA[j] = rB[j] = rW[j] = rE[j] = rP[j] = 0u;
+        qA[j] = qB[j] = qW[j] = qE[j] = qla[j] = qlb[j] = 0u;
+      }
+      auto load_chunk = [&](uint32_t it) {
+        uint32_t p[HV_EPL];
+        locate(it * CH, p, dE);
+        dv = 0;
+#pragma unroll
+        for (int j = 0; j < HV_EPL; ++j) {
+          dA[j] = ha[p[j]];
+          dB[j] = hb[p[j]];
+          dW[j] = hw[p[j]];
+          dv |= (it * CH + lane + WAVE * j < E) ? (1u << j) : 0u;
         }
-        uint32_t abw[4];
+      };
+      load_chunk(0);
+      for (uint32_t it = 0; it < niter + 2; ++it) {
+        {  // O: chunk it-2
+          uint32_t lmask = qlev, rmask = qrem;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) abw[j] = bits32[val[j] ? (A[j] >> 5) : 0u];
-        uint32_t b[4], ga[4], gb[4], la[4], lb[4];
-        uint64_t key[4];
-        bool lev[4], rem[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t bl = Bp[j] >> HV_IDX_BITS;
-          b[j] = (k << sb) + bl;
-          ga[j] = (abw[j] >> (A[j] & 31)) & 1u;
-          const uint32_t blv = val[j] ? bl : 0u;  // a dead lane's entry is not read
-          gb[j] = (s_bits[blv >> 5] >> (blv & 31)) & 1u;
-          const bool keep = val[j] & ((ga[j] & gb[j]) == 0u);
-          const uint32_t idx = Bp[j] & ((1u << HV_IDX_BITS) - 1);
-          const uint64_t eid = eb[j] + (idx >> 9) * Qw + (idx & 511u);
-          key[j] = ((uint64_t)Wt[j] << 32) | (uint32_t)eid;
-          lev[j] = keep & ((uint64_t)Wt[j] < w_hi);
-          rem[j] = keep & !lev[j];
-          la[j] = lab[(lev[j] & (ga[j] == 0u)) ? A[j] : 0u];
-          lb[j] = lab[(lev[j] & (gb[j] == 0u)) ? b[j] : 0u];
-          la[j] = ga[j] ? giant : la[j];
-          lb[j] = gb[j] ? giant : lb[j];
-        }
-        uint32_t lmask = 0, rmask = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          lev[j] = lev[j] & (la[j] != lb[j]);
-          lmask |= lev[j] ? (1u << j) : 0u;
-          rmask |= rem[j] ? (1u << j) : 0u;
-          if (lev[j] && mark) {
-            if (!ga[j]) mark[la[j]] = 1;
-            if (!gb[j]) mark[lb[j]] = 1;
-            touch_giant |= (ga[j] | gb[j]) != 0u;
+          for (int j = 0; j < HV_EPL; ++j) {
+            qla[j] = (qga >> j) & 1u ? giant : qla[j];
+            qlb[j] = (qgb >> j) & 1u ? giant : qlb[j];
+            if (qla[j] == qlb[j]) lmask &= ~(1u << j);
+            const bool mk = (lmask >> j) & 1u;
+            st_b8(1, rmark, (mk && !((qga >> j) & 1u)) ? qla[j] : ST_DROP);
+            st_b8(1, rmark, (mk && !((qgb >> j) & 1u)) ? qlb[j] : ST_DROP);
           }
-        }
-        // wave-private appends: both counts from one packed scan
-        uint32_t tot;
-        const uint32_t ex = wave_excl_scan((uint32_t)__popc(lmask) | ((uint32_t)__popc(rmask) << 16), &tot);
-        uint64_t pl = seg_begin + nlev + (ex & 0xffffu), pr = seg_begin + nrem + (ex >> 16);
+          touch_giant |= (lmask & (qga | qgb)) != 0u;
+          uint32_t tot;
+          const uint32_t ex = wave_excl_scan((uint32_t)__popc(lmask) | ((uint32_t)__popc(rmask) << 16), &tot);
+          uint32_t pl = (uint32_t)nlev + (ex & 0xffffu), pr = (uint32_t)nrem + (ex >> 16);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (lmask & (1u << j)) {
-            lsrc[pl] = la[j];
-            ldst[pl] = lb[j];
-            lkey[pl] = key[j];
-            ++pl;
+          for (int j = 0; j < HV_EPL; ++j) {
+            const uint32_t idx = qB[j] & ((1u << HV_IDX_BITS) - 1);
+            const uint32_t eid = qE[j] + (idx >> 9) * (uint32_t)Qw + (idx & 511u);
+            const uint64_t key = ((uint64_t)qW[j] << 32) | eid;
+            const bool l = (lmask >> j) & 1u, r = (rmask >> j) & 1u;
+            st_b32(qla[j], rls, l ? pl * 4u : ST_DROP);
+            st_b32(qlb[j], rld, l ? pl * 4u : ST_DROP);
+            st_b64(key, rlk, l ? pl * 8u : ST_DROP);
+            st_b32(qA[j], ros, r ? pr * 4u : ST_DROP);
+            st_b32((k << sb) + (qB[j] >> HV_IDX_BITS), rod, r ? pr * 4u : ST_DROP);
+            st_b64(key, rok, r ? pr * 8u : ST_DROP);
+            pl += l ? 1u : 0u;
+            pr += r ? 1u : 0u;
           }
-          if (rmask & (1u << j)) {
-            osrc[pr] = A[j];
-            odst[pr] = b[j];
-            okey[pr] = key[j];
-            ++pr;
-          }
+          nlev += tot & 0xffffu;
+          nrem += tot >> 16;
         }
-        nlev += tot & 0xffffu;
-        nrem += tot >> 16;
+        {  // G: chunk it-1 — decisions, label gathers
+          uint32_t nlv = 0, nrm = 0, nga = 0, ngb = 0;
+#pragma unroll
+          for (int j = 0; j < HV_EPL; ++j) {
+            const bool valid = (rv >> j) & 1u;
+            const uint32_t bl = valid ? rB[j] >> HV_IDX_BITS : 0u;  // a dead lane's entry is not read
+            const uint32_t b = (k << sb) + bl;
+            const uint32_t ga = valid ? (rP[j] >> (rA[j] & 31)) & 1u : 0u;
+            const uint32_t gb = (s_bits[bl >> 5] >> (bl & 31)) & 1u;
+            const bool keep = valid & ((ga & gb) == 0u);
+            const bool lev = keep & ((uint64_t)rW[j] < w_hi);
+            const bool rem = keep & !lev;
+            qla[j] = lab[(lev & (ga == 0u)) ? rA[j] : 0u];
+            qlb[j] = lab[(lev & (gb == 0u)) ? b : 0u];
+            nlv |= lev ? (1u << j) : 0u;
+            nrm |= rem ? (1u << j) : 0u;
+            nga |= ga << j;
+            ngb |= gb << j;
+            qA[j] = rA[j];
+            qB[j] = rB[j];
+            qW[j] = rW[j];
+            qE[j] = rE[j];
+          }
+          qlev = nlv;
+          qrem = nrm;
+          qga = nga;
+          qgb = ngb;
+        }
+        {  // P: chunk it — a-probes (a group's quarter holds sorted a ends: few lines)
+#pragma unroll
+          for (int j = 0; j < HV_EPL; ++j) {
+            rA[j] = dA[j];
+            rB[j] = dB[j];
+            rW[j] = dW[j];
+            rE[j] = dE[j];
+            rP[j] = bits32[((dv >> j) & 1u) ? (dA[j] >> 5) : 0u];
+          }
+          rv = dv;
+        }
+        load_chunk(it + 1);  // L: chunk it+1 (past the end: index 0, no valid bits)
       }
     }
   }
@@ -3048,6 +3164,7 @@ static bool levels_done(ghs_solver *s) {
 // k_filter writes the pending edges to rem[1]: a -> src, packed b | idx -> dst, w -> the first
 // half of key (as u32), the groups' bucket tables after it
 constexpr uint32_t HV_FILTER_G = 256;  // k_filter_hv blocks: one per CU (128-KiB LDS slice each)
+constexpr uint32_t HV_SELECT_G = 768;  // k_select_hv blocks: 3 per CU (41 KiB of LDS each)
 static inline uint32_t *hv_w(ghs_solver *s) { return reinterpret_cast<uint32_t *>(s->rem[0].key); }
 static inline uint16_t *hv_tab(ghs_solver *s) {
   return reinterpret_cast<uint16_t *>(reinterpret_cast<uint32_t *>(s->rem[0].key) + s->cap_arcs);
@@ -3109,6 +3226,7 @@ static int open_level(ghs_solver *s, bool async_open = false) {
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[0], st));
       {
         KT(GHS_K_SELECT, TC);
+        if (s->hv) G = std::min<unsigned>(G, HV_SELECT_G);  // co-resident: 3 blocks per CU (LDS)
         s->hv_gsel = G;
         if (s->hv)  // + the heavy copy, grouped by bucket of b, into rem[0] (read by k_filter_hv)
           k_select_hv<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range + 1, Y.src, Y.dst,
@@ -3682,7 +3800,7 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   if (const char *h = getenv("GHS_HV")) s->hv_env = h[0] != '0';
   if (const char *h = getenv("GHS_HV_SB")) {
     const long v = strtol(h, nullptr, 10);
-    s->hv_sb = (uint32_t)(v < 5 ? 5 : (v > (long)HV_SB_MAX ? HV_SB_MAX : v));
+    s->hv_sb = (uint32_t)(v < 7 ? 7 : (v > (long)HV_SB_MAX ? HV_SB_MAX : v));  // >= 4 words per slice
   }
   grid_env("GHS_IDENT_G", &s->ident_g);
   grid_env("GHS_WIN_G", &s->win_g);

@@ -406,7 +406,7 @@ def test_heavy_buckets_vs_oracle(graph, world, monkeypatch, torch_cuda):
     e = _test_graph(graph)
     g = e.to_host()
     ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
-    sb = max(5, int(np.ceil(np.log2(max(g.n, 2) / 32.0))))
+    sb = max(7, int(np.ceil(np.log2(max(g.n, 2) / 32.0))))
     assert 2 <= -(-g.n // (1 << sb)) <= 64
 
     def solve():
