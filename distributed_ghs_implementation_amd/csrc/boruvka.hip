@@ -3738,9 +3738,14 @@ static int solver_begin(ghs_solver *s) {
   if (int rc = plan_levels_enqueue(s)) return rc;
   KT(GHS_K_INIT, n);
   if (n) {
-    if ((e = hipMemsetAsync(s->best, 0xff, (size_t)n * 8, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset best: ") + hipGetErrorString(e));
+    // several ranks with dense levels: every level runs on the dense arrays (k_dense_open sets
+    // them up), so the vertex-sized best / par are never read — only lab is (s26: 805 MB of
+    // writes per rank saved)
+    if (!s->dense_mode) {
+      if ((e = hipMemsetAsync(s->best, 0xff, (size_t)n * 8, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset best: ") + hipGetErrorString(e));
+      k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->par, n);  // every root: par[r] == r
+    }
     k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->lab, n);
-    k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->par, n);  // every root: par[r] == r
   }
   // only the solver's own edge range: it never writes a flag outside [e_lo, e_hi)
   if (s->e_hi > s->e_lo && (e = hipMemsetAsync(s->in_mst + s->e_lo, 0, s->e_hi - s->e_lo, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset in_mst: ") + hipGetErrorString(e));

@@ -70,7 +70,7 @@ def main():
         if args.profile and rep == args.reps - 1:
             _native.profile_enable(True)
             kprof = []
-        if rep:
+        if rep or args.profile:  # a reset also picks up the profile switch
             for s in steppers:
                 s.reset()
         rounds = []
