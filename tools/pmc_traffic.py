@@ -45,6 +45,9 @@ def main():
         wb = 1024.0 * sum(w) / len(w) if w else None
         kernels[k] = {
             "launches_fetch_pass": len(f), "launches_write_pass": len(w),
+            # one workload per profile: a kernel launched once per step must show equal launches
+            # (the s26 scaling leg of bench.py is excluded by --no-scaling-base)
+            "fetch_raw_min_max": [1024.0 * min(f), 1024.0 * max(f)] if f else None,
             "fetch_bytes_per_launch_raw": fb, "write_bytes_per_launch": wb,
             "fetch_bytes_per_launch": 2 * fb if fb is not None else None,
             "traffic_bytes_per_launch": (2 * fb if fb is not None else 0) + (wb or 0),
