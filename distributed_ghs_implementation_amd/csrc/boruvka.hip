@@ -811,6 +811,20 @@ __global__ __launch_bounds__(1024) void k_scan_counts(const uint64_t *__restrict
   }
 }
 
+// Dense label of an active root x (several ranks, dense levels): its rank among the level's
+// active flags = chunk prefix + word prefix + the flags below x in its 64-bit word. The three
+// tables (12 B per 64 vertices: 12 MB at s26) replace a vertex-sized position map (268 MB) whose
+// random reads went to HBM.
+struct DenseRank {
+  const uint64_t *bits = nullptr;  // active flags, 64 vertices per word
+  const uint32_t *wpre = nullptr;  // flags below the word, within its chunk of 256 words
+  const uint32_t *cpre = nullptr;  // flags below the chunk
+};
+__device__ __forceinline__ uint32_t dense_rank(const DenseRank &r, uint32_t x) {
+  const uint32_t w = x >> 6;
+  return r.cpre[w >> 8] + r.wpre[w] + (uint32_t)__popcll(r.bits[w] & ((1ull << (x & 63)) - 1));
+}
+
 __device__ __forceinline__ uint32_t find_lab(const uint32_t *__restrict__ lab, uint32_t x,
                                              unsigned long long *__restrict__ err) {
   uint32_t y = lab[x];
@@ -872,7 +886,7 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
                                                 uint64_t *__restrict__ scan_prefix, unsigned long long *__restrict__ scan_total,
                                                 bool resolved, const unsigned long long *__restrict__ guard_live,
                                                 uint32_t own_lo, uint32_t own_hi,
-                                                const uint32_t *__restrict__ vlab, const uint32_t *__restrict__ dpos) {
+                                                const uint32_t *__restrict__ vlab, DenseRank dr) {
   __shared__ unsigned long long s_w[BLOCK / WAVE], s_c[BLOCK / WAVE];
   unsigned long long wsum = 0, cnt = 0;
   const uint64_t nact = *d_nact;
@@ -885,11 +899,11 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
       const uint32_t eid = (uint32_t)k;
       // a level's first round: k_resolve left every label a root (one read, no walk). A dense level
       // (several ranks): an endpoint's level-open root vlab[x] (resolved), its dense label
-      // dpos[vlab[x]], then the walk through the dense labels
+      // dense_rank(vlab[x]), then the walk through the dense labels
       uint32_t xa = eu[eid], xb = ev[eid];
-      if (dpos) {
-        xa = dpos[vlab[xa]];
-        xb = dpos[vlab[xb]];
+      if (dr.bits) {
+        xa = dense_rank(dr, vlab[xa]);
+        xb = dense_rank(dr, vlab[xb]);
       }
       const uint32_t la = resolved ? lab[xa] : find_lab(lab, xa, err);
       const uint32_t lb = resolved ? lab[xb] : find_lab(lab, xb, err);
@@ -2372,7 +2386,7 @@ __global__ __launch_bounds__(HV_FBLOCK) void k_filter_hv(
 // of live components" — the per-rank volume the vertex-indexed multi-rank rounds paid.
 // ------------------------------------------------------------------------------------------
 __global__ void k_dense_open(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
-                             uint32_t *__restrict__ pos, uint32_t *__restrict__ vtx, uint32_t *__restrict__ dlab,
+                             uint32_t *__restrict__ vtx, uint32_t *__restrict__ dlab,
                              uint32_t *__restrict__ dpar, uint64_t *__restrict__ dbest,
                              unsigned long long *__restrict__ dense_count) {
   const uint64_t nact = *d_nact;
@@ -2380,7 +2394,6 @@ __global__ void k_dense_open(const uint32_t *__restrict__ act, const unsigned lo
   if (t0 == 0) *dense_count = nact;
   for (uint64_t i = t0; i < nact; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t c = act[i];
-    pos[c] = (uint32_t)i;
     vtx[i] = c;
     dlab[i] = (uint32_t)i;
     dpar[i] = (uint32_t)i;
@@ -2390,8 +2403,60 @@ __global__ void k_dense_open(const uint32_t *__restrict__ act, const unsigned lo
 
 // the rank's level edges (a, b: vertex labels of active roots) -> dense labels, in place; the
 // regions' 4-entry tiles as in k_minedge (one region lookup per block range, 16-B accesses)
+__device__ __forceinline__ uint32_t nz_bits16(uint4 f);  // bit k = byte k of the 16 is nonzero (below)
+
+// the rank tables from the level's active flags (n bytes): one thread per 64-vertex word, a block
+// (256 words) scans its counts; then one block scans the chunk totals
+__global__ __launch_bounds__(BLOCK) void k_rank_words(const uint8_t *__restrict__ flags, uint64_t nf,
+                                                      uint64_t *__restrict__ bits, uint32_t *__restrict__ wpre,
+                                                      uint32_t *__restrict__ csum) {
+  __shared__ uint32_t s_wcnt[BLOCK / WAVE];
+  const uint64_t words = (nf + 63) / 64;
+  const uint64_t wd = blockIdx.x * (uint64_t)BLOCK + threadIdx.x;
+  uint64_t b = 0;
+  if (wd < words) {
+    const uint64_t i0 = wd * 64;
+    if (i0 + 64 <= nf) {
+      const uint4 *f = reinterpret_cast<const uint4 *>(flags + i0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b |= (uint64_t)nz_bits16(f[q]) << (16 * q);
+    } else {
+      for (uint64_t i = i0; i < nf; ++i) b |= (uint64_t)(flags[i] != 0) << (i - i0);
+    }
+  }
+  uint32_t total;
+  const uint32_t ex = block_offsets((uint32_t)__popcll(b), s_wcnt, &total);
+  if (wd < words) {
+    bits[wd] = b;
+    wpre[wd] = ex;
+  }
+  if (threadIdx.x == 0) csum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(1024) void k_rank_chunks(uint32_t *__restrict__ csum, uint32_t nchunks) {
+  __shared__ uint32_t s_part[1024];
+  const uint32_t per = (nchunks + 1023) / 1024;
+  const uint32_t b = threadIdx.x * per;
+  uint32_t sum = 0;
+  for (uint32_t i = 0; i < per && b + i < nchunks; ++i) sum += csum[b + i];
+  s_part[threadIdx.x] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const uint32_t o = threadIdx.x >= (unsigned)d ? s_part[threadIdx.x - d] : 0;
+    __syncthreads();
+    s_part[threadIdx.x] += o;
+    __syncthreads();
+  }
+  uint32_t run = s_part[threadIdx.x] - sum;  // exclusive, in place
+  for (uint32_t i = 0; i < per && b + i < nchunks; ++i) {
+    const uint32_t c = csum[b + i];
+    csum[b + i] = run;
+    run += c;
+  }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_relabel_dense(uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
-                                                         SegView in, const uint32_t *__restrict__ pos) {
+                                                         SegView in, DenseRank dr) {
   __shared__ uint32_t s_seg[2];
   const uint64_t T = in.prefix[in.nseg];
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
@@ -2411,7 +2476,7 @@ __global__ __launch_bounds__(BLOCK) void k_relabel_dense(uint32_t *__restrict__ 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {  // region padding (a == LABEL_NONE) stays dead
       const bool live = A[j] != LABEL_NONE;
-      const uint32_t pa = pos[live ? A[j] : 0u], pb = pos[live ? B[j] : 0u];
+      const uint32_t pa = dense_rank(dr, live ? A[j] : 0u), pb = dense_rank(dr, live ? B[j] : 0u);
       A[j] = live ? pa : LABEL_NONE;
       B[j] = live ? pb : B[j];
     }
@@ -2882,7 +2947,9 @@ struct ghs_solver {
   uint32_t hv_gsel = 1;         // k_select_hv's grid (k_filter_hv decodes the eids from it)
   // dense levels (several ranks, see k_dense_open): the dense arrays, the vertex arrays they stand
   // in for while a level runs, and the level's fragment count
-  uint32_t *dlab = nullptr, *dpar = nullptr, *dpos = nullptr, *dvtx = nullptr;
+  uint32_t *dlab = nullptr, *dpar = nullptr, *dvtx = nullptr;
+  uint64_t *drank_bits = nullptr;                  // dense labels by rank (DenseRank)
+  uint32_t *drank_wpre = nullptr, *drank_cpre = nullptr;
   uint64_t *dbest = nullptr;
   uint32_t *vlab = nullptr, *vpar = nullptr;
   uint64_t *flag_bits = nullptr;  // the packed level-open flags (ghs_solver_flag_bits)
@@ -3007,7 +3074,10 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
     p = carve(N * 4); if (s) s->dlab = (uint32_t *)p;
     p = carve(N * 4); if (s) s->dpar = (uint32_t *)p;
     p = carve(N * 8); if (s) s->dbest = (uint64_t *)p;
-    p = carve(N * 4); if (s) s->dpos = (uint32_t *)p;
+    const size_t W = (N + 63) / 64;
+    p = carve(W * 8); if (s) s->drank_bits = (uint64_t *)p;
+    p = carve(W * 4); if (s) s->drank_wpre = (uint32_t *)p;
+    p = carve(((W + BLOCK - 1) / BLOCK) * 4 + 4); if (s) s->drank_cpre = (uint32_t *)p;
     p = carve(N * 4); if (s) s->dvtx = (uint32_t *)p;
   }
   p = carve(N + 1); if (s) s->flags = (uint8_t *)p;  // + the multi-rank error byte flags[n]
@@ -3317,17 +3387,29 @@ static int open_level(ghs_solver *s, bool async_open = false) {
 }
 
 // ---- dense levels (several ranks; kernels at k_dense_open) ------------------------------------
+static DenseRank dense_rank_of(const ghs_solver *s) {
+  DenseRank r;
+  r.bits = s->drank_bits;
+  r.wpre = s->drank_wpre;
+  r.cpre = s->drank_cpre;
+  return r;
+}
+
 static int dense_open(ghs_solver *s) {
   hipStream_t st = s->stream;
   const uint64_t nact = s->nact;
   {
     KT(GHS_K_DENSE, nact);
-    k_dense_open<<<grid_for(nact, 256, 16384), 256, 0, st>>>(s->act[0], s->cnt + C_ACT, s->dpos, s->dvtx, s->dlab,
+    const uint64_t words = ((uint64_t)s->n + 63) / 64;
+    const uint32_t chunks = (uint32_t)((words + BLOCK - 1) / BLOCK);
+    k_rank_words<<<chunks, BLOCK, 0, st>>>(s->flags, s->n, s->drank_bits, s->drank_wpre, s->drank_cpre);
+    k_rank_chunks<<<1, 1024, 0, st>>>(s->drank_cpre, chunks);
+    k_dense_open<<<grid_for(nact, 256, 16384), 256, 0, st>>>(s->act[0], s->cnt + C_ACT, s->dvtx, s->dlab,
                                                              s->dpar, s->dbest, s->cnt + C_NDENSE);
     const ArcBuf &Y = s->buf[s->cur];
     SegView in{Y.seg_start, Y.seg_prefix, s->cur_nseg};
     if (s->cur_arcs)
-      k_relabel_dense<<<grid_for(s->cur_arcs, ARCS_PER_BLOCK, SEG_G), BLOCK, 0, st>>>(Y.src, Y.dst, in, s->dpos);
+      k_relabel_dense<<<grid_for(s->cur_arcs, ARCS_PER_BLOCK, SEG_G), BLOCK, 0, st>>>(Y.src, Y.dst, in, dense_rank_of(s));
   }
   GHS_HIP_CHECK(hipGetLastError());
   s->vlab = s->lab; s->vpar = s->par; s->vbest = s->best;
@@ -3521,7 +3603,7 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
       KT(GHS_K_HOOK, 0);
       k_hook<<<gh, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
                                          s->cnt + C_WEIGHT, s->cnt + C_ERR, nullptr, 0, nullptr, nullptr, false,
-                                         s->cnt + C_LIVE, (uint32_t)s->e_lo, (uint32_t)s->e_hi, nullptr, nullptr);
+                                         s->cnt + C_LIVE, (uint32_t)s->e_lo, (uint32_t)s->e_hi, nullptr, DenseRank());
     } else {
       const ArcBuf *sb = s->scan_pending ? s->scan_buf : nullptr;
       KT(GHS_K_HOOK, 0);
@@ -3529,7 +3611,7 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
                                          s->cnt + C_WEIGHT, s->cnt + C_ERR, sb ? sb->seg_count : nullptr, s->cmp_g,
                                          sb ? sb->seg_prefix : nullptr, s->cnt + C_LIVE, s->level_round == 0, nullptr,
                                          (uint32_t)s->e_lo, (uint32_t)s->e_hi, s->level_dense ? s->vlab : nullptr,
-                                         s->level_dense ? s->dpos : nullptr);
+                                         s->level_dense ? dense_rank_of(s) : DenseRank());
       s->scan_pending = false;
     }
     GHS_HIP_CHECK(hipGetLastError());
