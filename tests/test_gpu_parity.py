@@ -654,6 +654,19 @@ def test_rmat_s24_full_size(torch_cuda):
     _full_size_checks(e, eng, res, torch)
 
 
+def test_rmat_s24_full_size_heavy_buckets(monkeypatch, torch_cuda):
+    """The opt-in bucketed heavy-edge passes (GHS_HV=1: 16 buckets of 2^20 vertices, ~3 sort
+    groups per k_filter_hv wave) at BASELINE config 3's full size: the same checks."""
+    torch = torch_cuda
+    from distributed_ghs_implementation_amd.device import DeviceMST, generate_rmat
+    monkeypatch.setenv("GHS_HV", "1")
+    e = generate_rmat(24, 16, seed=1, wseed=2)
+    eng = DeviceMST(e)
+    res, _ = eng.run()
+    assert res.pass_flags & 1 and res.levels >= 2
+    _full_size_checks(e, eng, res, torch)
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_grid_16k_full_size(mode, torch_cuda):
     """BASELINE config 5 (16384^2 grid, 537M edges; mode 1 = gradient weights) at full size:
