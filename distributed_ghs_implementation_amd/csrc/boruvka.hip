@@ -2409,12 +2409,14 @@ __device__ __forceinline__ uint32_t nz_bits16(uint4 f);  // bit k = byte k of th
 // (256 words) scans its counts; then one block scans the chunk totals
 __global__ __launch_bounds__(BLOCK) void k_rank_words(const uint8_t *__restrict__ flags, uint64_t nf,
                                                       uint64_t *__restrict__ bits, uint32_t *__restrict__ wpre,
-                                                      uint32_t *__restrict__ csum) {
+                                                      uint32_t *__restrict__ csum, bool from_words) {
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
   const uint64_t words = (nf + 63) / 64;
   const uint64_t wd = blockIdx.x * (uint64_t)BLOCK + threadIdx.x;
   uint64_t b = 0;
-  if (wd < words) {
+  if (from_words) {  // the merged words of the bitmap exchange are already in bits (k_merge_flag_words)
+    if (wd < words) b = bits[wd];
+  } else if (wd < words) {
     const uint64_t i0 = wd * 64;
     if (i0 + 64 <= nf) {
       const uint4 *f = reinterpret_cast<const uint4 *>(flags + i0);
@@ -2427,13 +2429,55 @@ __global__ __launch_bounds__(BLOCK) void k_rank_words(const uint8_t *__restrict_
   uint32_t total;
   const uint32_t ex = block_offsets((uint32_t)__popcll(b), s_wcnt, &total);
   if (wd < words) {
-    bits[wd] = b;
+    if (!from_words) bits[wd] = b;
     wpre[wd] = ex;
   }
   if (threadIdx.x == 0) csum[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(1024) void k_rank_chunks(uint32_t *__restrict__ csum, uint32_t nchunks) {
+// merged level-open flags as words (several ranks, dense levels): the OR of the gathered
+// bitmaps straight into the rank tables' word array (flags below n; bit n, the error byte, to its
+// byte) — no flag bytes written, no select over n bytes
+__global__ void k_merge_flag_words(const uint64_t *__restrict__ all, uint32_t nranks, uint64_t words, uint64_t n,
+                                   uint64_t *__restrict__ out, uint8_t *__restrict__ err_byte) {
+  const uint64_t nw = (n + 63) / 64;
+  for (uint64_t wd = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; wd < words; wd += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t b = 0;
+    for (uint32_t r = 0; r < nranks; ++r) b |= all[(uint64_t)r * words + wd];
+    if (wd == n / 64) *err_byte = ((b >> (n % 64)) & 1u) ? 2 : 0;
+    if (wd < nw) out[wd] = (wd == n / 64) ? (b & ((1ull << (n % 64)) - 1)) : b;
+  }
+}
+
+// the level's fragments from the rank tables: vtx[rank(x)] = x for every set flag x (a thread per
+// word), then the dense identity state
+__global__ void k_dense_open_words(DenseRank dr, uint64_t words, uint32_t *__restrict__ vtx) {
+  for (uint64_t wd = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; wd < words; wd += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t b = dr.bits[wd];
+    uint32_t r = dr.cpre[wd >> 8] + dr.wpre[wd];
+    while (b) {
+      const int j = __ffsll((unsigned long long)b) - 1;
+      vtx[r++] = (uint32_t)(wd * 64 + j);
+      b &= b - 1;
+    }
+  }
+}
+
+__global__ void k_dense_init(const unsigned long long *__restrict__ d_nact, uint32_t *__restrict__ dlab,
+                             uint32_t *__restrict__ dpar, uint64_t *__restrict__ dbest,
+                             unsigned long long *__restrict__ dense_count) {
+  const uint64_t nact = *d_nact;
+  const uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (t0 == 0) *dense_count = nact;
+  for (uint64_t i = t0; i < nact; i += (uint64_t)gridDim.x * blockDim.x) {
+    dlab[i] = (uint32_t)i;
+    dpar[i] = (uint32_t)i;
+    dbest[i] = KEY_NONE;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_rank_chunks(uint32_t *__restrict__ csum, uint32_t nchunks,
+                                                      unsigned long long *__restrict__ total_out) {
   __shared__ uint32_t s_part[1024];
   const uint32_t per = (nchunks + 1023) / 1024;
   const uint32_t b = threadIdx.x * per;
@@ -2453,6 +2497,7 @@ __global__ __launch_bounds__(1024) void k_rank_chunks(uint32_t *__restrict__ csu
     csum[b + i] = run;
     run += c;
   }
+  if (total_out && threadIdx.x == 1023) *total_out = s_part[1023];
 }
 
 __global__ __launch_bounds__(BLOCK) void k_relabel_dense(uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
@@ -2949,6 +2994,8 @@ struct ghs_solver {
   // in for while a level runs, and the level's fragment count
   uint32_t *dlab = nullptr, *dpar = nullptr, *dvtx = nullptr;
   uint64_t *drank_bits = nullptr;                  // dense labels by rank (DenseRank)
+  bool words_merged = false;                       // this level's flags arrived as merged words
+  bool rank_ready = false;                         // ... and the rank tables are built from them
   uint32_t *drank_wpre = nullptr, *drank_cpre = nullptr;
   uint64_t *dbest = nullptr;
   uint32_t *vlab = nullptr, *vpar = nullptr;
@@ -3402,10 +3449,17 @@ static int dense_open(ghs_solver *s) {
     KT(GHS_K_DENSE, nact);
     const uint64_t words = ((uint64_t)s->n + 63) / 64;
     const uint32_t chunks = (uint32_t)((words + BLOCK - 1) / BLOCK);
-    k_rank_words<<<chunks, BLOCK, 0, st>>>(s->flags, s->n, s->drank_bits, s->drank_wpre, s->drank_cpre);
-    k_rank_chunks<<<1, 1024, 0, st>>>(s->drank_cpre, chunks);
-    k_dense_open<<<grid_for(nact, 256, 16384), 256, 0, st>>>(s->act[0], s->cnt + C_ACT, s->dvtx, s->dlab,
-                                                             s->dpar, s->dbest, s->cnt + C_NDENSE);
+    if (s->rank_ready) {  // rank tables from the merged words (open_level_finish)
+      k_dense_open_words<<<grid_for(words, 256, 16384), 256, 0, st>>>(dense_rank_of(s), words, s->dvtx);
+      k_dense_init<<<grid_for(nact, 256, 16384), 256, 0, st>>>(s->cnt + C_ACT, s->dlab, s->dpar, s->dbest,
+                                                               s->cnt + C_NDENSE);
+    } else {
+      k_rank_words<<<chunks, BLOCK, 0, st>>>(s->flags, s->n, s->drank_bits, s->drank_wpre, s->drank_cpre, false);
+      k_rank_chunks<<<1, 1024, 0, st>>>(s->drank_cpre, chunks, nullptr);
+      k_dense_open<<<grid_for(nact, 256, 16384), 256, 0, st>>>(s->act[0], s->cnt + C_ACT, s->dvtx, s->dlab,
+                                                               s->dpar, s->dbest, s->cnt + C_NDENSE);
+    }
+    s->rank_ready = false;
     const ArcBuf &Y = s->buf[s->cur];
     SegView in{Y.seg_start, Y.seg_prefix, s->cur_nseg};
     if (s->cur_arcs)
@@ -3450,7 +3504,21 @@ static int open_level_finish(ghs_solver *s) {
     GHS_HIP_CHECK(hipGetLastError());
   }
   s->pending_exchange = false;
-  if (int rc = select_lb(s, nullptr, s->cnt + C_N, s->n, s->act[0], s->cnt + C_ACT)) return rc;
+  const bool from_words = s->words_merged;
+  s->words_merged = false;
+  if (from_words) {
+    // dense levels, bitmap exchange: the rank tables (and the count) from the merged words; the
+    // fragment list follows in dense_open
+    KT(GHS_K_DENSE, s->n);
+    const uint64_t words = ((uint64_t)s->n + 63) / 64;
+    const uint32_t chunks = (uint32_t)((words + BLOCK - 1) / BLOCK);
+    k_rank_words<<<chunks, BLOCK, 0, st>>>(s->flags, s->n, s->drank_bits, s->drank_wpre, s->drank_cpre, true);
+    k_rank_chunks<<<1, 1024, 0, st>>>(s->drank_cpre, chunks, s->cnt + C_ACT);
+    GHS_HIP_CHECK(hipGetLastError());
+  } else if (int rc = select_lb(s, nullptr, s->cnt + C_N, s->n, s->act[0], s->cnt + C_ACT)) {
+    return rc;
+  }
+  s->rank_ready = from_words;
   s->act_ident = false;
   s->act_cur = 0;
   GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, C_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
@@ -3996,8 +4064,14 @@ int ghs_solver_merge_flag_bits(ghs_solver_t *s, const uint64_t *d_all, uint32_t 
   const uint64_t nf = (uint64_t)s->n + 1, nw = (nf + 63) / 64;
   {
     KT(GHS_K_FLAG_BITS, nw);
-    k_merge_flag_bits<<<grid_for(nw, 256, 16384), 256, 0, s->stream>>>(d_all, nranks, nw, nf, s->flags,
-                                                                       s->flags + s->n);
+    if (s->dense_mode) {  // the level opens from the merged words (no flag bytes, no select over n)
+      k_merge_flag_words<<<grid_for(nw, 256, 16384), 256, 0, s->stream>>>(d_all, nranks, nw, s->n, s->drank_bits,
+                                                                          s->flags + s->n);
+      s->words_merged = true;
+    } else {
+      k_merge_flag_bits<<<grid_for(nw, 256, 16384), 256, 0, s->stream>>>(d_all, nranks, nw, nf, s->flags,
+                                                                         s->flags + s->n);
+    }
   }
   GHS_HIP_CHECK(hipGetLastError());
   return GHS_OK;
