@@ -4,11 +4,11 @@
 // graph files (create_graph_files.py:43-89 writes every undirected edge once in
 // graph_metadata.json). The reference's generator is networkx's seeded ER G(n, p)
 // (create_graph_files.py:13-40); R-MAT and grids are the BASELINE scales it cannot reach. The
-// canonical sort/dedupe is a rocPRIM radix sort of 64-bit (min << scale | max) keys + unique.
+// canonical sort/dedupe is a rocPRIM radix sort of 64-bit (min << scale | max) keys, then a
+// two-pass unique + decode (k_uniq_*).
 // The CPU restatement of both generators (test infrastructure) is oracle/generators.c.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_select.hpp>
 
 #include <string>
 
@@ -86,14 +86,104 @@ __global__ void k_rmat_tuples(uint64_t T, uint32_t scale, uint64_t seed, uint64_
     keys[t] = rmat_tuple(t, scale, seed);
 }
 
-__global__ void k_rmat_decode(uint64_t m, uint32_t scale, uint64_t wseed, const uint64_t *__restrict__ keys,
-                              uint32_t *__restrict__ u, uint32_t *__restrict__ v, uint32_t *__restrict__ w) {
-  const uint64_t mask = (1ull << scale) - 1ull;
-  for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = keys[e];
-    u[e] = (uint32_t)(k >> scale);
-    v[e] = (uint32_t)(k & mask);
-    w[e] = mix32((uint32_t)e ^ (uint32_t)wseed);
+// Unique + decode of the sorted keys in two passes over them (rocPRIM's unique, a partition
+// over 2 GB of keys at s24, took 8 ms; these are streaming passes): a key is kept when it differs
+// from its predecessor and is not the self-loop marker (which sorts last). Pass 1 counts the kept
+// keys per tile, one block scans the tile counts, pass 2 writes each kept key's (u, v, w) at its
+// rank — the weight hashes the output position, as the canonical list's edge id.
+constexpr int UQ_BLOCK = 256;
+constexpr int UQ_ROWS = 16;  // a tile is UQ_ROWS rows of UQ_BLOCK consecutive keys
+constexpr uint64_t UQ_TILE = (uint64_t)UQ_BLOCK * UQ_ROWS;
+
+__device__ __forceinline__ bool uq_keep(const uint64_t *__restrict__ keys, uint64_t i, uint64_t T, uint64_t marker,
+                                        uint64_t *k_out) {
+  if (i >= T) return false;
+  const uint64_t k = keys[i];
+  *k_out = k;
+  return k != marker && (i == 0 || keys[i - 1] != k);
+}
+
+__global__ __launch_bounds__(UQ_BLOCK) void k_uniq_count(const uint64_t *__restrict__ keys, uint64_t T, uint64_t marker,
+                                                         uint32_t *__restrict__ tile_cnt) {
+  __shared__ uint32_t s_w[UQ_BLOCK / 64];
+  const uint64_t base = blockIdx.x * UQ_TILE;
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < UQ_ROWS; ++j) {
+    uint64_t k;
+    c += uq_keep(keys, base + (uint64_t)j * UQ_BLOCK + threadIdx.x, T, marker, &k) ? 1u : 0u;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x / 64] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < UQ_BLOCK / 64; ++w) t += s_w[w];
+    tile_cnt[blockIdx.x] = t;
+  }
+}
+
+// exclusive scan of the tile counts in place (one block of 1024), total to *total
+__global__ __launch_bounds__(1024) void k_uniq_scan(uint32_t *__restrict__ cnt, uint32_t ntiles,
+                                                    uint64_t *__restrict__ total) {
+  __shared__ uint32_t s_part[1024];
+  const uint32_t per = (ntiles + 1023) / 1024;
+  const uint32_t b = threadIdx.x * per;
+  uint32_t sum = 0;
+  for (uint32_t i = 0; i < per && b + i < ntiles; ++i) sum += cnt[b + i];
+  s_part[threadIdx.x] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const uint32_t o = threadIdx.x >= (unsigned)d ? s_part[threadIdx.x - d] : 0;
+    __syncthreads();
+    s_part[threadIdx.x] += o;
+    __syncthreads();
+  }
+  uint32_t run = s_part[threadIdx.x] - sum;
+  for (uint32_t i = 0; i < per && b + i < ntiles; ++i) {
+    const uint32_t c = cnt[b + i];
+    cnt[b + i] = run;
+    run += c;
+  }
+  if (threadIdx.x == 1023) *total = s_part[1023];
+}
+
+__global__ __launch_bounds__(UQ_BLOCK) void k_uniq_write(const uint64_t *__restrict__ keys, uint64_t T, uint64_t marker,
+                                                         const uint32_t *__restrict__ tile_off, uint32_t scale,
+                                                         uint64_t wseed, uint32_t *__restrict__ u,
+                                                         uint32_t *__restrict__ v, uint32_t *__restrict__ w) {
+  __shared__ uint32_t s_cnt[UQ_ROWS][UQ_BLOCK / 64];
+  const uint64_t base = blockIdx.x * UQ_TILE;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x / 64;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint64_t kk[UQ_ROWS];
+  uint64_t masks[UQ_ROWS];
+#pragma unroll
+  for (int j = 0; j < UQ_ROWS; ++j) {
+    const bool keep = uq_keep(keys, base + (uint64_t)j * UQ_BLOCK + threadIdx.x, T, marker, &kk[j]);
+    masks[j] = __ballot(keep);
+    if (lane == 0) s_cnt[j][wid] = (uint32_t)__popcll(masks[j]);
+  }
+  __syncthreads();
+  const uint64_t vmask = (1ull << scale) - 1ull;
+  uint32_t row_base = tile_off[blockIdx.x];
+#pragma unroll
+  for (int j = 0; j < UQ_ROWS; ++j) {
+    uint32_t before = 0, row = 0;
+#pragma unroll
+    for (int x = 0; x < UQ_BLOCK / 64; ++x) {
+      const uint32_t c = s_cnt[j][x];
+      before += x < wid ? c : 0u;
+      row += c;
+    }
+    if ((masks[j] >> lane) & 1ull) {
+      const uint32_t o = row_base + before + (uint32_t)__popcll(masks[j] & lt);
+      u[o] = (uint32_t)(kk[j] >> scale);
+      v[o] = (uint32_t)(kk[j] & vmask);
+      w[o] = mix32(o ^ (uint32_t)wseed);
+    }
+    row_base += row;
   }
 }
 
@@ -144,12 +234,11 @@ int ghs_check_canonical(uint32_t n, uint64_t m, const uint32_t *d_u, const uint3
 
 size_t ghs_rmat_temp_bytes(uint32_t scale, uint32_t edgefactor) {
   const uint64_t T = (uint64_t)edgefactor << scale;
-  size_t sort_b = 0, uniq_b = 0;
+  size_t sort_b = 0;
   (void)rocprim::radix_sort_keys(nullptr, sort_b, (const uint64_t *)nullptr, (uint64_t *)nullptr, (size_t)T, 0u,
                                  2u * scale);
-  (void)rocprim::unique(nullptr, uniq_b, (const uint64_t *)nullptr, (uint64_t *)nullptr, (uint64_t *)nullptr,
-                        (size_t)T);
-  return 2 * align256(T * 8) + align256(sort_b > uniq_b ? sort_b : uniq_b) + 256;
+  const size_t tiles_b = align256(((T + UQ_TILE - 1) / UQ_TILE) * 4);
+  return 2 * align256(T * 8) + align256(sort_b > tiles_b ? sort_b : tiles_b) + 256;
 }
 
 int ghs_rmat_generate(uint32_t scale, uint32_t edgefactor, uint64_t seed, uint64_t wseed, uint32_t *d_u,
@@ -166,21 +255,20 @@ int ghs_rmat_generate(uint32_t scale, uint32_t edgefactor, uint64_t seed, uint64
   uint64_t *nsel = (uint64_t *)(base + 2 * align256(T * 8));
   void *prim_temp = base + 2 * align256(T * 8) + 256;
   size_t prim_bytes = temp_bytes - (2 * align256(T * 8) + 256);
+  const uint64_t ntiles = (T + UQ_TILE - 1) / UQ_TILE;
+  uint32_t *tiles = (uint32_t *)prim_temp;  // reused after the sort
+  const uint64_t marker = (1ull << (2 * scale)) - 1ull;  // a self-loop's key (sorts last)
 
   k_rmat_tuples<<<grid_cap(T, 256, 16384), 256, 0, st>>>(T, scale, seed, ka);
   GHS_HIP_CHECK(hipGetLastError());
   GHS_HIP_CHECK(rocprim::radix_sort_keys(prim_temp, prim_bytes, ka, kb, (size_t)T, 0u, 2u * scale, st));
-  GHS_HIP_CHECK(rocprim::unique(prim_temp, prim_bytes, kb, ka, nsel, (size_t)T, rocprim::equal_to<uint64_t>(), st));
-  uint64_t cnt = 0, last = 0;
+  k_uniq_count<<<(unsigned)ntiles, UQ_BLOCK, 0, st>>>(kb, T, marker, tiles);
+  k_uniq_scan<<<1, 1024, 0, st>>>(tiles, (uint32_t)ntiles, nsel);
+  k_uniq_write<<<(unsigned)ntiles, UQ_BLOCK, 0, st>>>(kb, T, marker, tiles, scale, wseed, d_u, d_v, d_w);
+  GHS_HIP_CHECK(hipGetLastError());
+  uint64_t cnt = 0;
   GHS_HIP_CHECK(hipMemcpyAsync(&cnt, nsel, 8, hipMemcpyDeviceToHost, st));
   GHS_HIP_CHECK(hipStreamSynchronize(st));
-  if (cnt) {
-    GHS_HIP_CHECK(hipMemcpyAsync(&last, ka + (cnt - 1), 8, hipMemcpyDeviceToHost, st));
-    GHS_HIP_CHECK(hipStreamSynchronize(st));
-    if (last == ((1ull << (2 * scale)) - 1ull)) --cnt;  // the self-loop marker sorts last
-  }
-  k_rmat_decode<<<grid_cap(cnt, 256, 16384), 256, 0, st>>>(cnt, scale, wseed, ka, d_u, d_v, d_w);
-  GHS_HIP_CHECK(hipGetLastError());
   *m_out = cnt;
   return GHS_OK;
 }

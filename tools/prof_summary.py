@@ -7,14 +7,22 @@ import sqlite3
 import sys
 
 
+WIDTH = 90
+
+
 def short(name):
     name = re.sub(r"\(.*\)$", "", name)  # drop the argument list
     name = name.replace("void ", "").replace("ghs::", "")
-    return name[:90]
+    if "rocprim" in name:  # the kernel kind, not the namespace prefix
+        name = re.sub(r"rocprim::ROCPRIM_\w+?_NS::", "", name)
+    return name[:WIDTH]
 
 
 def main():
+    global WIDTH
     path = sys.argv[1]
+    if "--width" in sys.argv:
+        WIDTH = int(sys.argv[sys.argv.index("--width") + 1])
     c = sqlite3.connect(path)
     rows = c.execute("select name, count(*), sum(duration), avg(duration), min(duration), max(duration) "
                      "from kernels group by name order by sum(duration) desc").fetchall()
