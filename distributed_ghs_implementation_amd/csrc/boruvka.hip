@@ -4107,28 +4107,15 @@ int ghs_solver_hook_local(ghs_solver_t *s, int32_t *d_dense, uint64_t *count) {
   if (s->phase != 1) GHS_FAIL(GHS_E_STATE, "hook_local must follow unpack_best");
   // a level's first round with several ranks (its edges carry the current roots); labels and
   // fragment ids must fit the int32 MAX exchange
-  // a level's first round (its edges carry the current roots), or any round of a dense level (the
-  // compaction's survivors carry the roots of the round); labels and fragment ids must fit the
-  // int32 MAX exchange
   if (s->cfg.num_ranks <= 1 || s->level_round != 0 || !s->nact || s->hooked || s->n > (1u << 31)) return GHS_OK;
   if (!d_dense) GHS_FAIL(GHS_E_ARG, "dense is NULL");
   const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
-  if (s->level_round == 0) {
-    if (s->cur_arcs || !s->arcs_known) {
-      const ArcBuf &I = s->buf[s->cur];
-      SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
-      KT(GHS_K_WIN, s->arcs_known ? s->cur_arcs : 0);
-      k_win<<<s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->win_g) : s->win_g, BLOCK, 0, s->stream>>>(
-          I.src, I.dst, I.key, in, s->best, s->par, s->in_mst, nullptr, nullptr);
-    }
-  } else {
-    // this round's compaction output: the surviving (inter-fragment) edges, relabelled to the
-    // round's roots; every fragment's winning edge is one of them, on exactly one rank
-    if (s->scan_pending) flush_scan(s);
-    const ArcBuf &O = s->buf[s->cur ^ 1];
-    SegView in{O.seg_start, O.seg_prefix, s->cmp_g};
-    KT(GHS_K_WIN, 0);
-    k_win<<<s->win_g, BLOCK, 0, s->stream>>>(O.src, O.dst, O.key, in, s->best, s->par, s->in_mst, nullptr, nullptr);
+  if (s->cur_arcs || !s->arcs_known) {
+    const ArcBuf &I = s->buf[s->cur];
+    SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
+    KT(GHS_K_WIN, s->arcs_known ? s->cur_arcs : 0);
+    k_win<<<s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->win_g) : s->win_g, BLOCK, 0, s->stream>>>(
+        I.src, I.dst, I.key, in, s->best, s->par, s->in_mst, nullptr, nullptr);
   }
   KT(GHS_K_PACK_HOOK, s->nact);
   k_pack_hook<<<grid_for(s->nact, 256, 16384), 256, 0, s->stream>>>(act, cur_act_count(s), s->par, d_dense);
