@@ -2378,8 +2378,9 @@ __global__ __launch_bounds__(HV_FBLOCK) void k_filter_hv(
 
 // ------------------------------------------------------------------------------------------
 // Dense levels (several ranks). Once a level's active list A (nact0 fragment roots, identical on
-// every rank) is selected, the level runs in a dense label space 0..nact0-1: pos[A[i]] = i, the
-// rank's level edges are relabelled through pos, and best / lab / par become nact0-sized arrays.
+// every rank) is known, the level runs in a dense label space 0..nact0-1: a root's dense label is
+// its rank among the level's flags (DenseRank: popc over the flag words + word / chunk prefixes),
+// the rank's level edges are relabelled through it, and best / lab / par become nact0-sized arrays.
 // The level-opening round's all-reduce slots are then best itself (sequential pack / unpack, no
 // gathers and scatters over the vertex arrays through A), the jump runs over the dense identity
 // list, and the whole level's state stays in nact0 * 16 B. At the level's end every fragment's
