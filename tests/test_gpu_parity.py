@@ -506,11 +506,15 @@ def test_native_loop_s26_emulated(world, rmat_s26_reference, torch_cuda):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("scale,ef,seed,wseed", [(12, 16, 1, 2), (16, 16, 1, 2), (18, 16, 3, 4), (14, 8, 9, 0)])
+@pytest.mark.parametrize("scale,ef,seed,wseed", [(12, 16, 1, 2), (16, 16, 1, 2), (18, 16, 3, 4), (14, 8, 9, 0),
+                                                 (1, 1, 1, 2), (2, 3, 5, 6), (3, 1, 7, 8), (10, 3, 1, 2),
+                                                 (13, 5, 2, 3)])
 def test_rmat_generator_matches_oracle(scale, ef, seed, wseed, torch_cuda):
     """Generator parity: the raw GPU tuples equal oracle/generators.c tuple for
-    tuple, and the GPU canonical list (rocPRIM sort + unique, self-loops dropped, hashed weights)
-    equals the oracle's canonicalisation of the same tuples, bit-exact."""
+    tuple, and the GPU canonical list (rocPRIM radix sort, then the k_uniq_* unique + decode:
+    self-loops dropped, hashed weights) equals the oracle's canonicalisation of the same tuples,
+    bit-exact. Tiny and ragged sizes cover partial unique tiles (4096 keys) and all-self-loop
+    outcomes."""
     import torch
     from distributed_ghs_implementation_amd import _native
     from distributed_ghs_implementation_amd.device import _ptr, _stream, generate_rmat
