@@ -3024,6 +3024,12 @@ struct ghs_solver {
 hipStream_t ghs_solver_stream_of(const ghs_solver *s) { return s->stream; }
 uint32_t ghs_solver_n_of(const ghs_solver *s) { return s->n; }
 uint32_t ghs_solver_ranks_of(const ghs_solver *s) { return s->cfg.num_ranks; }
+// the round's slots in place: a dense level's identity round (its first) keeps the active
+// fragments' minima contiguous in best[0, nact) — an unsigned MIN all-reduce over best itself
+// replaces pack_best / all-reduce / unpack_best (nullptr: use those)
+uint64_t *ghs_solver_best_slots_of(ghs_solver *s) {
+  return (s->phase == 1 && s->nact && s->act_ident && s->level_dense) ? s->best : nullptr;
+}
 
 static std::mutex g_prof_mutex;
 static bool g_prof_on = false;

@@ -62,6 +62,7 @@ __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 hipStream_t ghs_solver_stream_of(const ghs_solver *s);
 uint32_t ghs_solver_n_of(const ghs_solver *s);
 uint32_t ghs_solver_ranks_of(const ghs_solver *s);
+uint64_t *ghs_solver_best_slots_of(ghs_solver *s);
 int ghs_solver_flag_bits_async(ghs_solver *s, uint64_t **d_bits, uint64_t *words);
 
 #define GHS_HIP_CHECK(expr)                                                                     \

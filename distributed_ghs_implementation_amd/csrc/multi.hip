@@ -26,6 +26,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <thread>
 #include <vector>
 
@@ -69,6 +70,10 @@ struct EmuGroup {
 namespace {
 
 __global__ void k_emu_min_i64(int64_t *__restrict__ dst, const int64_t *__restrict__ src, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i] < dst[i] ? src[i] : dst[i];
+}
+__global__ void k_emu_min_u64(uint64_t *__restrict__ dst, const uint64_t *__restrict__ src, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     dst[i] = src[i] < dst[i] ? src[i] : dst[i];
 }
@@ -145,12 +150,14 @@ int coll_allgather_u64(ghs_comm *c, const uint64_t *send, uint64_t *recv, size_t
   return GHS_OK;
 }
 
-// in-place all-reduce: MIN over int64 or MAX over int32
+// in-place all-reduce: MIN over int64 or uint64, MAX over int32
 template <typename T>
 int coll_allreduce(ghs_comm *c, T *buf, size_t count, hipStream_t st) {
   constexpr bool is_min = sizeof(T) == 8;
+  constexpr bool is_u64 = std::is_same<T, uint64_t>::value;
   if (c->nccl) {
-    COMM_NCCL(ncclAllReduce(buf, buf, count, is_min ? ncclInt64 : ncclInt32, is_min ? ncclMin : ncclMax, c->nccl, st));
+    COMM_NCCL(ncclAllReduce(buf, buf, count, is_u64 ? ncclUint64 : (is_min ? ncclInt64 : ncclInt32),
+                            is_min ? ncclMin : ncclMax, c->nccl, st));
     return GHS_OK;
   }
   GHS_HIP_CHECK(hipStreamSynchronize(st));
@@ -158,7 +165,9 @@ int coll_allreduce(ghs_comm *c, T *buf, size_t count, hipStream_t st) {
   COMM_BARRIER(c);
   if (c->rank == 0) {  // rank 0 reduces every buffer into its own
     for (int r = 1; r < c->nranks; ++r) {
-      if (is_min)
+      if (is_u64)
+        k_emu_min_u64<<<emu_grid(count), 256, 0, st>>>((uint64_t *)buf, (const uint64_t *)c->emu->ptrs[r], count);
+      else if (is_min)
         k_emu_min_i64<<<emu_grid(count), 256, 0, st>>>((int64_t *)buf, (const int64_t *)c->emu->ptrs[r], count);
       else
         k_emu_max_i32<<<emu_grid(count), 256, 0, st>>>((int32_t *)buf, (const int32_t *)c->emu->ptrs[r], count);
@@ -203,9 +212,13 @@ int run_loop(ghs_solver_t *s, ghs_comm *c) {
     }
     LOOP_CHECK(rc);
     if (multi && count) {
-      LOOP_CHECK(ghs_solver_pack_best(s, c->dense));
-      LOOP_CHECK(coll_allreduce<int64_t>(c, c->dense, count, st));
-      LOOP_CHECK(ghs_solver_unpack_best(s, c->dense));
+      if (uint64_t *slots = ghs_solver_best_slots_of(s)) {  // a dense level's first round: best in place
+        LOOP_CHECK(coll_allreduce<uint64_t>(c, slots, count, st));
+      } else {
+        LOOP_CHECK(ghs_solver_pack_best(s, c->dense));
+        LOOP_CHECK(coll_allreduce<int64_t>(c, c->dense, count, st));
+        LOOP_CHECK(ghs_solver_unpack_best(s, c->dense));
+      }
       uint64_t hooks = 0;
       LOOP_CHECK(ghs_solver_hook_local(s, c->hook, &hooks));
       if (hooks) {
