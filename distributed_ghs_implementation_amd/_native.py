@@ -37,7 +37,7 @@ EXPORTED_SYMBOLS = (
     "ghs_check_canonical",
     "ghs_solver_create", "ghs_solver_minedge", "ghs_solver_exchange_buffer", "ghs_solver_pack_best",
     "ghs_solver_flag_bits", "ghs_solver_merge_flag_bits",
-    "ghs_solver_unpack_best",
+    "ghs_solver_unpack_best", "ghs_solver_best_slots",
     "ghs_solver_contract", "ghs_solver_finish", "ghs_solver_reset", "ghs_solver_destroy",
     "ghs_solver_hook_local", "ghs_solver_unpack_hook",
     "ghs_rmat_temp_bytes", "ghs_rmat_generate", "ghs_rmat_tuples", "ghs_grid_generate",
@@ -213,6 +213,7 @@ def load():
             "ghs_solver_merge_flag_bits": (i32, [vp, vp, u32]),
             "ghs_solver_pack_best": (i32, [vp, vp]),
             "ghs_solver_unpack_best": (i32, [vp, vp]),
+            "ghs_solver_best_slots": (i32, [vp, P(vp), P(u64)]),
             "ghs_solver_contract": (i32, [vp, P(i32)]),
             "ghs_solver_finish": (i32, [vp, P(Result), P(RoundStats)]),
             "ghs_solver_hook_local": (i32, [vp, vp, P(ctypes.c_uint64)]),

@@ -4101,6 +4101,14 @@ int ghs_solver_pack_best(ghs_solver_t *s, int64_t *d_dense) {
   return GHS_OK;
 }
 
+int ghs_solver_best_slots(ghs_solver_t *s, uint64_t **d_slots, uint64_t *count) {
+  if (!s || !d_slots || !count) GHS_FAIL(GHS_E_ARG, "solver/slots/count is NULL");
+  if (s->phase != 1) GHS_FAIL(GHS_E_STATE, "best_slots must follow minedge");
+  *d_slots = ghs_solver_best_slots_of(s);
+  *count = *d_slots ? s->nact : 0;
+  return GHS_OK;
+}
+
 int ghs_solver_unpack_best(ghs_solver_t *s, const int64_t *d_dense) {
   if (!s || (s->nact && !d_dense)) GHS_FAIL(GHS_E_ARG, "solver/dense is NULL");
   if (s->phase != 1) GHS_FAIL(GHS_E_STATE, "unpack_best must follow minedge");

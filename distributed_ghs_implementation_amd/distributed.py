@@ -87,6 +87,16 @@ class HipStepper:
     def unpack(self, dense):
         _native.check(self.L.ghs_solver_unpack_best(self.h, _ptr(dense)))
 
+    def best_slots(self):
+        """A dense level's first round: the solver's own minima as an int64 view of `count` slots
+        holding uint64 keys (MIN-reduce them unsigned, in place), or None (use pack / unpack)."""
+        p = ctypes.c_void_p(0)
+        c = ctypes.c_uint64(0)
+        _native.check(self.L.ghs_solver_best_slots(self.h, ctypes.byref(p), ctypes.byref(c)))
+        if not p.value:
+            return None
+        return _device_u8_view(p.value, 8 * int(c.value), self.e.edges.device, self.e.ws).view(torch.int64)
+
     def hook_local(self):
         """Owner-computes CONNECT of a level's first round: the int32 slots to all-reduce with
         MAX (then unpack_hook), or None when the round hooks inside contract."""

@@ -186,6 +186,11 @@ int ghs_solver_flag_bits(ghs_solver_t *h, uint64_t **d_bits, uint64_t *words);
 int ghs_solver_merge_flag_bits(ghs_solver_t *h, const uint64_t *d_all, uint32_t nranks);
 int ghs_solver_pack_best(ghs_solver_t *h, int64_t *d_dense);
 int ghs_solver_unpack_best(ghs_solver_t *h, const int64_t *d_dense);
+/* optional, instead of pack_best / int64 MIN / unpack_best: a dense level's first round keeps its
+ * *count slots contiguous in the solver's own minima (identity order), so the caller may MIN
+ * all-reduce *d_slots in place as UNSIGNED 64-bit (ncclUint64 + ncclMin). *d_slots = NULL: this
+ * round needs pack / unpack. (ghs_solver_run uses it; ABI 4 addition) */
+int ghs_solver_best_slots(ghs_solver_t *h, uint64_t **d_slots, uint64_t *count);
 /* optional, after unpack_best (a level's first round, several ranks): owner-computes CONNECT.
  * Each rank hooks the fragments whose winning edge it holds and fills *count int32 slots
  * (par ^ fragment, 0 where another rank owns the winner); the caller all-reduces them with MAX

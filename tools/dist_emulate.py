@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--no-ref", action="store_true", help="skip the single-GPU reference (profiling)")
+    ap.add_argument("--no-inplace", action="store_true",
+                    help="pack / int64 MIN / unpack in every round (the gloo loop) instead of the library "
+                         "loop's in-place uint64 MIN of a dense level's first round")
     ap.add_argument("--profile", action="store_true",
                     help="per-launch HIP-event profile of the last rep: kernel ms per round of the max rank")
     ap.add_argument("--max-levels", type=int, default=None)
@@ -101,18 +104,29 @@ def main():
                     ms[r] += t
             assert len(set(counts)) == 1
             if counts[0]:
-                dense = []
-                for r, s in enumerate(steppers):
-                    d, t = timed(r, lambda: s.pack(counts[0]).clone())
-                    dense.append(d)
-                    ms[r] += t
-                red = dense[0]
-                for d in dense[1:]:
-                    red = torch.minimum(red, d)
-                coll.append(("allreduce_min_i64", int(red.numel()) * 8))
-                for r, s in enumerate(steppers):
-                    _, t = timed(r, lambda: s.unpack(red))
-                    ms[r] += t
+                slots = [None] if args.no_inplace else [s.best_slots() for s in steppers]
+                if slots[0] is not None:  # the library loop's in-place uint64 MIN (not timed)
+                    sign = torch.tensor(-(1 << 63), dtype=torch.int64, device=slots[0].device)
+                    red = slots[0] ^ sign
+                    for v in slots[1:]:
+                        red = torch.minimum(red, v ^ sign)
+                    red ^= sign
+                    for v in slots:
+                        v.copy_(red)
+                    coll.append(("allreduce_min_u64", int(red.numel()) * 8))
+                else:
+                    dense = []
+                    for r, s in enumerate(steppers):
+                        d, t = timed(r, lambda: s.pack(counts[0]).clone())
+                        dense.append(d)
+                        ms[r] += t
+                    red = dense[0]
+                    for d in dense[1:]:
+                        red = torch.minimum(red, d)
+                    coll.append(("allreduce_min_i64", int(red.numel()) * 8))
+                    for r, s in enumerate(steppers):
+                        _, t = timed(r, lambda: s.unpack(red))
+                        ms[r] += t
                 hooks = []
                 for r, s in enumerate(steppers):
                     h, t = timed(r, lambda: (lambda x: None if x is None else x.clone())(s.hook_local()))
