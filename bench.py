@@ -9,7 +9,9 @@ parameters, unique hashed weights — no dataset download).
   N = 1: R-MAT scale 24 (BASELINE config 3), the headline `value`; the line also carries
          `scaling_base`: R-MAT scale 26 (config 4's graph) solved on this one GPU.
   N > 1 (torch.distributed.run, one rank per GPU, RCCL): strong scaling on R-MAT scale 26 —
-         every N solves the same graph, so scaling_base and the N > 1 lines form one curve.
+         every N solves the same graph, so scaling_base and the N > 1 lines form one curve; a
+         step there also gathers the MSF edge ids to rank 0 (the reference's collect_results),
+         ms_per_step_solve times the solve alone. "scaling" is "strong" on every line.
 Rank 0 prints ONE JSON line. After the timed steps one extra step runs with every kernel launch
 bracketed by HIP events on the solve's stream (libghs_mst.so ghs_profile_enable): `kernels` lists
 every kernel's time per step and achieved GB/s under its algorithmic byte model (launch_bytes),
@@ -82,14 +84,10 @@ def _first_round(stats, r):
 
 def launch_bytes(rec, stats, res, n):
     k = rec["kernel"]
-    # bucketed heavy edges (pass_flags bit 0): k_select also writes the heavy copy (12 B per edge
-    # not in level 0) and k_filter streams that copy instead of the canonical list
-    heavy = max(res.canon_edges - res.select_out, 0) if res.pass_flags & 1 else 0
     if k == "k_select":
-        return 12.0 * res.canon_edges + 16.0 * res.select_out + 12.0 * heavy  # u, v, w in; level-0 edges out
+        return 12.0 * res.canon_edges + 16.0 * res.select_out  # u, v, w in; level-0 edges out
     if k == "k_filter":
-        src = heavy if res.pass_flags & 1 else res.canon_edges
-        return 12.0 * src + 16.0 * res.filter_out  # stream + level-1 and pending edges out
+        return 12.0 * res.canon_edges + 16.0 * res.filter_out  # stream + level-1 and pending edges out
     if k == "k_resolve":
         return 8.0 * n + n / 8.0  # lab read + write, giant bitmap
     if k == "k_jump_ident":
@@ -155,22 +153,34 @@ def stage1_roofline(records, stats):
             "definition": "24 B x sum of live edges over every min-edge round / sum of stage-1 time (BASELINE.md)"}
 
 
-PMC_NAMES = {"k_minedge<IDENT>": "k_minedge<true, false>", "k_minedge<COMPACT>": "k_minedge<false, true>"}
+# profile name -> the PMC file's kernel-name prefix (rocprofv3 prints every template argument:
+# k_minedge<false, true, false>; any later template parameter still matches the prefix)
+PMC_NAMES = {"k_minedge<IDENT>": "k_minedge<true, false", "k_minedge<COMPACT>": "k_minedge<false, true"}
+
+
+def _pmc_match(name, key):
+    """key (a PMC file's kernel name) is the profile kernel `name`: equal, or a templated name
+    whose arguments start with the mapped prefix."""
+    want = PMC_NAMES.get(name, name)
+    if key == want:
+        return True
+    return "<" in want and key.startswith(want) and key[len(want):len(want) + 1] in (">", ",")
 
 
 def load_traffic(workload_tag, kernel):
     """Per-launch HBM bytes of `kernel` from a committed PMC profile (profiles/**/*_pmc.json,
     the newest round's wins)."""
     best = None
-    name = PMC_NAMES.get(kernel, kernel)
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*_pmc.json"), recursive=True)):
         try:
             d = json.load(open(p))
         except Exception:
             continue
-        k = d.get("kernels", {}).get(name)
-        if d.get("workload") == workload_tag and k and k.get("traffic_bytes_per_launch"):
-            best = dict(k, _path=os.path.relpath(p, ROOT))
+        if d.get("workload") != workload_tag:
+            continue
+        for key, k in d.get("kernels", {}).items():
+            if _pmc_match(kernel, key) and k and k.get("traffic_bytes_per_launch"):
+                best = dict(k, _path=os.path.relpath(p, ROOT))
     return best
 
 
@@ -367,6 +377,16 @@ def main():
 
     eng = DistributedMST(edges, rank, world) if world > 1 else DeviceMST(edges)
     step = eng.run
+    if world > 1:
+        # N > 1: a step ends with the MSF on rank 0, as the reference's MPI run ends with
+        # collect_results (ghs_implementation_mpi.py:760-779): each rank's own-range MSF edge ids
+        # gathered to rank 0. The solve alone is timed separately (ms_per_step_solve).
+        dt_solve, _ = time_steps(eng.run, args.steps, args.warmup, world, dist)
+
+        def step():
+            out = eng.run()
+            eng.collect_mst(0)
+            return out
     dt, outs = time_steps(step, args.steps, args.warmup, world, dist)
     results = [r for r, _ in outs]
     if len(set((r.total_weight, r.num_mst_edges) for r in results)) != 1:
@@ -386,7 +406,7 @@ def main():
             print(f"ranks agree: weight {results[-1].total_weight} edges {results[-1].num_mst_edges} eid checksum {chk}",
                   file=sys.stderr)
 
-    ktab, s1, _ = profile_step(step, n)
+    ktab, s1, _ = profile_step(eng.run, n)
     # the canonical passes are also timed inside the timed steps (two events per pass, no idle
     # between dependent kernels of note): prefer those averages for k_select / k_filter
     for name, attr in (("k_select", "ms_select"), ("k_filter", "ms_filter")):
@@ -428,11 +448,14 @@ def main():
             cpu_nx = networkx_baseline(args.nx_scale, args.edgefactor)
         line = {"metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-                "higher_is_better": True, "scaling": "strong" if world > 1 else "weak", "vs_baseline": None,
+                "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
                 "dtype": "u64", "data": "synthetic (generated on GPU)", "config": cfg, "roofline": roofline,
                 "stage1_roofline": s1, "cpu_baseline": cpu_omp, "cpu_baseline_serial": cpu,
                 "cpu_baseline_networkx": cpu_nx, "end_to_end": e2e, "kernels": kernels,
                 "mst": {"total_weight": res0.total_weight, "edges": res0.num_mst_edges}, "breakdown": breakdown}
+        if world > 1:
+            line["ms_per_step_solve"] = round(dt_solve * 1e3 / args.steps, 4)
+            line["step"] = "solve + gather of the MSF edge ids to rank 0 (collect_results)"
     del eng
     if world == 1 and args.workload == "rmat" and args.scale is None and not args.no_scaling_base:
         # the strong-scaling reference point: config 4's graph (R-MAT s26) on this one GPU, the

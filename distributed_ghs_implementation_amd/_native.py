@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "ghs_solver_create", "ghs_solver_minedge", "ghs_solver_exchange_buffer", "ghs_solver_pack_best",
     "ghs_solver_flag_bits", "ghs_solver_merge_flag_bits",
     "ghs_solver_unpack_best", "ghs_solver_best_slots",
-    "ghs_solver_contract", "ghs_solver_finish", "ghs_solver_reset", "ghs_solver_destroy",
+    "ghs_solver_contract", "ghs_solver_finish", "ghs_solver_reset", "ghs_solver_cancel", "ghs_solver_destroy",
     "ghs_solver_hook_local", "ghs_solver_unpack_hook",
     "ghs_rmat_temp_bytes", "ghs_rmat_generate", "ghs_rmat_tuples", "ghs_grid_generate",
     "ghs_profile_enable", "ghs_profile_read", "ghs_kernel_name",
@@ -95,7 +95,7 @@ class RoundStatsList(collections.abc.Sequence):
         return repr(list(self))
 
 
-ABI_VERSION = 4  # include/ghs_mst.h GHS_MST_ABI_VERSION
+ABI_VERSION = 5  # include/ghs_mst.h GHS_MST_ABI_VERSION
 
 
 class Result(ctypes.Structure):
@@ -148,19 +148,39 @@ def profile_read():
             return out
 
 
+# ghs_config_t.options bits (include/ghs_mst.h GHS_OPT_*)
+OPT_NO_SEED_RUNS = 0x1
+OPT_NO_DENSE = 0x2
+OPT_DEBUG = 0x10
+OPT_TIME_ROUNDS = 0x20
+OPT_DETAIL = 0x40
+
+
 class Config(ctypes.Structure):
-    """ghs_config_t: the weight-level plan of the filter (speed only; results never change)."""
+    """ghs_config_t: the weight-level plan of the filter and the path options (speed only;
+    results never change). The library reads no environment variable that changes its path."""
     _fields_ = [
         ("max_levels", ctypes.c_uint32),
         ("num_ranks", ctypes.c_uint32),
         ("level1_edges_per_vertex", ctypes.c_double),
         ("level_growth", ctypes.c_double),
+        ("options", ctypes.c_uint32),
+        ("dedup_max", ctypes.c_uint32),
+        ("fault_rank", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
     ]
 
 
-def make_config(max_levels=None, level1_edges_per_vertex=None, level_growth=None, num_ranks=None):
+def make_config(max_levels=None, level1_edges_per_vertex=None, level_growth=None, num_ranks=None, options=None,
+                dedup_max=None, fault_rank=None):
     c = Config()
     load().ghs_default_config(ctypes.byref(c))
+    if options is not None:
+        c.options = int(options)
+    if dedup_max is not None:
+        c.dedup_max = int(dedup_max)
+    if fault_rank is not None:
+        c.fault_rank = int(fault_rank)
     if num_ranks is not None:
         c.num_ranks = int(num_ranks)
     if max_levels is not None:
@@ -219,6 +239,7 @@ def load():
             "ghs_solver_hook_local": (i32, [vp, vp, P(ctypes.c_uint64)]),
             "ghs_solver_unpack_hook": (i32, [vp, vp]),
             "ghs_solver_reset": (i32, [vp]),
+            "ghs_solver_cancel": (i32, [vp]),
             "ghs_solver_destroy": (i32, [vp]),
             "ghs_rmat_temp_bytes": (sz, [u32, u32]),
             "ghs_rmat_generate": (i32, [u32, u32, u64, u64, vp, vp, vp, P(u64), vp, sz, vp]),

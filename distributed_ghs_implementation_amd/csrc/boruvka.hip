@@ -56,6 +56,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -1938,445 +1939,6 @@ GHS_STREAM_KERNEL_6 void k_level_pass(const uint32_t *__restrict__ ru, const uin
 }
 
 // ------------------------------------------------------------------------------------------
-// Heavy-edge buckets (hv). k_filter's cost is its random b-probes of the giant bitmap: one L2
-// request per heavy edge, served at the L2 request rate (~265 G/s from a 2-MiB bitmap, ~121 G/s
-// once the bitmap outgrows an XCD's 4-MiB L2 — s26), and they do not overlap the stream, so the
-// pass costs stream + probes. With the heavy edges grouped by b, every b-probe of a group of
-// blocks falls in one slice of the bitmap: 2^sb vertices (sb <= 20: 128 KiB) held in LDS.
-//  - k_select_hv (opens level 0, the first stream) additionally writes every heavy edge
-//    (w >= level 0's bound) to a heavy copy. A block streams Qb edges (a multiple of HV_GS =
-//    2048), each of its 4 waves a contiguous quarter of them — so the level-0 edges leave in
-//    canonical order, one wave-private segment per quarter, exactly as k_select writes them
-//    (k_seed_runs relies on it). Sort group g of a block = the g-th 512 edges of every quarter:
-//    the group's heavy edges sorted by bucket (b >> sb) through LDS and written contiguously at
-//    the group's own position (no compaction across groups: position = block start + g * HV_GS),
-//    with a table of nb + 1 u16 bucket offsets per group. An entry is 12 B: a,
-//    (b - bucket base) << 11 | (quarter << 9 | offset in the quarter's 512), w.
-//  - k_filter_hv (opens level 1) reads the copy bucket by bucket: the block loads slice k of the
-//    bitmap into LDS, its waves stream the bucket-k sub-runs of their groups, probe b in LDS and
-//    a (sorted within a group's quarter: a few lines) in the L2-resident bitmap.
-// The copy costs one more write of the heavy edges during the first stream; k_filter then reads
-// the copy instead of the canonical list (the same 12 B per edge) with no L2 probes for b.
-// Positions run to the last block's end (< T + Qb): the workspace reserves that slack.
-// ------------------------------------------------------------------------------------------
-constexpr uint32_t HV_GS = 2048;        // edges per sort group: 512 from each wave's quarter
-constexpr uint32_t HV_IDX_BITS = 11;    // an entry's quarter and offset in its group
-constexpr uint32_t HV_SB_MAX = 20;      // vertices per bucket <= 2^20 (a 128-KiB bitmap slice)
-constexpr uint32_t HV_NB_MAX = 64;      // buckets
-constexpr uint32_t HV_FBLOCK = 1024;    // k_filter_hv block: 16 waves share one LDS slice
-constexpr uint64_t HV_MAX_EDGES = 1ull << 28;  // edges per solver (see solver_begin)
-#ifndef GHS_HV_DEFAULT
-#define GHS_HV_DEFAULT 0
-#endif
-constexpr bool HV_DEFAULT = GHS_HV_DEFAULT != 0;  // env GHS_HV overrides
-static_assert(HV_SB_MAX + HV_IDX_BITS <= 32, "hv entry packing");
-
-// a block's range of k_select_hv (and the decoding in k_filter_hv): gsel blocks, Qb edges each
-__device__ __forceinline__ uint64_t hv_block_edges(uint64_t T, uint32_t gsel) {
-  const uint64_t per = (T + gsel - 1) / gsel;
-  return ((per + HV_GS - 1) / HV_GS) * HV_GS;
-}
-
-__global__ __launch_bounds__(BLOCK, 3) void k_select_hv(uint32_t n, uint64_t e_lo, uint64_t e_hi,
-                                                       const uint32_t *__restrict__ eu, const uint32_t *__restrict__ ev,
-                                                       const uint32_t *__restrict__ ew, const uint64_t *__restrict__ w_hi_p,
-                                                       uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
-                                                       uint64_t *__restrict__ okey, uint64_t *__restrict__ ostart,
-                                                       uint64_t *__restrict__ ocount, uint8_t *__restrict__ mark,
-                                                       unsigned long long *__restrict__ err, uint32_t sb, uint32_t nb,
-                                                       uint32_t *__restrict__ ha, uint32_t *__restrict__ hb,
-                                                       uint32_t *__restrict__ hw, uint16_t *__restrict__ htab) {
-  const uint64_t w_hi = *w_hi_p;
-  __shared__ WaveStage s_stage[BLOCK / WAVE];
-  __shared__ uint32_t s_ha[HV_GS], s_hb[HV_GS], s_hw[HV_GS];
-  __shared__ uint32_t s_cnt[2][HV_NB_MAX + 1];  // bucket counts -> bases, alternating per group
-  const uint32_t lane = threadIdx.x & (WAVE - 1), wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
-  const uint64_t E0 = e_lo & ~3ull;
-  const uint64_t T = e_hi - E0;
-  const uint64_t Qb = hv_block_edges(T, gridDim.x);
-  const uint64_t Qw = Qb / 4;                 // a wave's quarter (a multiple of 512)
-  const uint32_t gpb = (uint32_t)(Qb / HV_GS);  // sort groups per block
-  const uint64_t vb = Qb * blockIdx.x;
-  const uint64_t wb = vb + (uint64_t)wid * Qw;  // this wave's quarter [wb, we)
-  const uint64_t we = (wb + Qw < T) ? wb + Qw : (wb < T ? T : wb);
-  const uint64_t eb = E0 + wb;
-  const uint64_t nbytes = (we - wb) * 4;
-  const __amdgpu_buffer_rsrc_t ru = make_rsrc(eu + eb, nbytes);
-  const __amdgpu_buffer_rsrc_t rv = make_rsrc(ev + eb, nbytes);
-  const __amdgpu_buffer_rsrc_t rw = make_rsrc(ew + eb, nbytes);
-  uint32_t bpa = 0, bpb = 0;  // the edge before the quarter's first (offset -4 is outside the resource)
-  if (eb > 0 && we > wb) {
-    bpa = eu[eb - 1];
-    bpb = ev[eb - 1];
-  }
-  WaveOut wo;  // level-0 edges: the quarter's wave-private segment
-  wo.pos = wb;
-  bool bad = false;
-  for (uint32_t i = threadIdx.x; i < 2 * (HV_NB_MAX + 1); i += BLOCK) (&s_cnt[0][0])[i] = 0;
-  __syncthreads();
-  uint32_t par = 0;
-  const uint32_t ngroups = vb < T ? gpb : 0u;  // every group of a block with edges gets its table row
-  // the group's two tiles per wave, prefetched one group ahead (past the quarter: reads 0)
-  uint4 fa[2], fb[2], fw[2];
-  uint32_t fpa[2], fpb[2];
-  auto fetch = [&](uint32_t g) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t off = (g * 512u + h * 256u + lane * 4u) * 4u;
-      fa[h] = ld_b128(ru, off);
-      fb[h] = ld_b128(rv, off);
-      fw[h] = ld_b128(rw, off);
-      fpa[h] = ld_b32(ru, off - 4);
-      fpb[h] = ld_b32(rv, off - 4);
-    }
-  };
-  fetch(0);
-  for (uint32_t g = 0; g < ngroups; ++g, par ^= 1) {
-    uint32_t xa[8], xb[8], xw[8], xr[8];  // the lane's heavy edges: a, packed b | idx, w, rank << 8 | bucket
-    uint32_t hmask = 0;
-    uint4 ta[2], tb[2], tw[2];
-    uint32_t tpa[2], tpb[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      ta[h] = fa[h]; tb[h] = fb[h]; tw[h] = fw[h]; tpa[h] = fpa[h]; tpb[h] = fpb[h];
-    }
-    fetch(g + 1);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t q = g * 512u + h * 256u + lane * 4u;  // offset in the quarter
-      const uint64_t v = wb + q;  // relative to E0
-      const uint64_t e0 = E0 + v;
-      const uint4 ca = ta[h], cb = tb[h], cw = tw[h];
-      uint32_t pa = tpa[h], pb = tpb[h];
-      if (q == 0) {
-        pa = bpa;
-        pb = bpb;
-      }
-      const uint32_t a[4] = {ca.x, ca.y, ca.z, ca.w}, b[4] = {cb.x, cb.y, cb.z, cb.w}, w[4] = {cw.x, cw.y, cw.z, cw.w};
-      const uint32_t nv = v < we ? (uint32_t)((we - v) < 4 ? (we - v) : 4) : 0u;
-      const uint32_t nskip = e0 < e_lo ? (uint32_t)(e_lo - e0) : 0u;
-      const uint32_t first = (e0 == 0) ? 1u : 0u;
-      bool out[4];
-      uint64_t key[4];
-      uint32_t omask = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        bool live = ((uint32_t)j < nv) & ((uint32_t)j >= nskip);
-        const uint32_t ordered = (j == 0 ? first : 0u) | (uint32_t)(pa < a[j]) | ((uint32_t)(pa == a[j]) & (uint32_t)(pb < b[j]));
-        const uint32_t ok = (uint32_t)(a[j] < b[j]) & (uint32_t)(b[j] < n) & ordered;
-        bad |= live & (ok == 0u);
-        live = live & (ok != 0u);  // never index with an unchecked id
-        pa = a[j];
-        pb = b[j];
-        out[j] = live & ((uint64_t)w[j] < w_hi);
-        const bool heavy = live & ((uint64_t)w[j] >= w_hi);
-        omask |= out[j] ? (1u << j) : 0u;
-        key[j] = ((uint64_t)w[j] << 32) | (uint32_t)(e0 + j);
-        if (mark && out[j]) {
-          mark[a[j]] = 1;
-          mark[b[j]] = 1;
-        }
-        const uint32_t k = b[j] >> sb;
-        uint32_t r = 0;
-        if (heavy) r = atomicAdd(&s_cnt[par][k], 1u);
-        xa[h * 4 + j] = a[j];
-        xb[h * 4 + j] = ((b[j] - (k << sb)) << HV_IDX_BITS) | (wid << 9) | (h * 256u + lane * 4u + (uint32_t)j);
-        xw[h * 4 + j] = w[j];
-        xr[h * 4 + j] = (r << 8) | k;
-        hmask |= heavy ? (1u << (h * 4 + j)) : 0u;
-      }
-      wave_append(s_stage[wid], wo, a, b, key, omask, osrc, odst, okey);
-    }
-    __syncthreads();
-    // bucket bases: exclusive scan of the nb counts by wave 0; the group's table row
-    if (wid == 0) {
-      const uint32_t c = lane < nb ? s_cnt[par][lane] : 0u;
-      uint32_t tot;
-      const uint32_t ex = wave_excl_scan(c, &tot);
-      if (lane < nb) s_cnt[par][lane] = ex;
-      if (lane == 0) s_cnt[par][nb] = tot;
-      uint16_t *row = htab + ((uint64_t)blockIdx.x * gpb + g) * (nb + 1);
-      if (lane < nb) row[lane] = (uint16_t)ex;
-      if (lane == WAVE - 1) row[nb] = (uint16_t)tot;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if (hmask & (1u << e)) {
-        const uint32_t pos = s_cnt[par][xr[e] & 255u] + (xr[e] >> 8);
-        s_ha[pos] = xa[e];
-        s_hb[pos] = xb[e];
-        s_hw[pos] = xw[e];
-      }
-    }
-    // the other parity's counters were last read before this group's first barrier
-    if (threadIdx.x <= nb) s_cnt[par ^ 1][threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t tot = s_cnt[par][nb];
-    const uint64_t gpos = vb + (uint64_t)g * HV_GS;
-    for (uint32_t i = threadIdx.x; i < tot; i += BLOCK) {
-      ha[gpos + i] = s_ha[i];
-      hb[gpos + i] = s_hb[i];
-      hw[gpos + i] = s_hw[i];
-    }
-    // the prefetched group has landed by now (waited here, not at the loop head)
-    asm volatile("" ::"v"(fa[0].x), "v"(fb[0].x), "v"(fw[0].x), "v"(fa[1].x), "v"(fb[1].x), "v"(fw[1].x), "v"(fpa[0]),
-                 "v"(fpb[0]), "v"(fpa[1]), "v"(fpb[1]));
-  }
-  if (bad) atomicOr(err, 8ull);
-  wave_finish(s_stage[wid], wo, osrc, odst, okey, wb, wb < T, ostart, ocount, blockIdx.x * (BLOCK / WAVE) + wid);
-}
-
-// FILTER over the heavy copy (see above): same decisions and outputs as k_filter (level-1 edges
-// relabelled, heavier survivors pending as u, v, key), one output segment per wave (its groups'
-// positions), ordered by bucket within a wave. A wave streams its groups' bucket-k sub-runs as
-// one virtual stream (lane i holds group i's sub-run start c_i; an entry finds its group by a
-// binary search over the lanes), HV_EPL entries per lane per iteration, software-pipelined: the
-// a-probes and label gathers of iteration i are issued before the loads of iteration i + 1, so
-// waiting for them leaves those loads in flight.
-#ifndef GHS_HV_EPL
-#define GHS_HV_EPL 4
-#endif
-constexpr int HV_EPL = GHS_HV_EPL;
-__global__ __launch_bounds__(HV_FBLOCK) void k_filter_hv(
-    uint64_t e_lo, uint64_t e_hi, uint32_t sb, uint32_t nb, const uint32_t *__restrict__ ha,
-    const uint32_t *__restrict__ hb, const uint32_t *__restrict__ hw, const uint16_t *__restrict__ htab,
-    uint32_t gsel, const uint64_t *__restrict__ w_range, const uint64_t *__restrict__ giant_bits, uint64_t bits_words,
-    const uint32_t *__restrict__ giant_ptr, const uint32_t *__restrict__ lab, uint32_t *__restrict__ lsrc,
-    uint32_t *__restrict__ ldst, uint64_t *__restrict__ lkey, uint64_t *__restrict__ lstart,
-    uint64_t *__restrict__ lcount, uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
-    uint64_t *__restrict__ okey, uint64_t *__restrict__ ostart, uint64_t *__restrict__ ocount,
-    uint8_t *__restrict__ mark) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_bits[1u << (HV_SB_MAX - 5)];
-  const uint64_t w_hi = w_range[1];
-  const uint32_t lane = threadIdx.x & (WAVE - 1), wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
-  const uint64_t E0 = e_lo & ~3ull;
-  const uint64_t T = e_hi - E0;
-  const uint64_t Qb = hv_block_edges(T, gsel), Qw = Qb / 4;  // k_select_hv's blocks
-  const uint64_t gpb = Qb / HV_GS;
-  const uint64_t NG = ((T + Qb - 1) / Qb) * gpb;  // the groups of every block with edges
-  const uint64_t W = (uint64_t)gridDim.x * (HV_FBLOCK / WAVE);
-  const uint64_t gw = (uint64_t)blockIdx.x * (HV_FBLOCK / WAVE) + wid;
-  const uint64_t gA = NG * gw / W, gB = NG * (gw + 1) / W;  // this wave's groups
-  const uint64_t seg_begin = gA * HV_GS;
-  const uint32_t *bits32 = reinterpret_cast<const uint32_t *>(giant_bits);
-  const uint32_t giant = giant_ptr[0];
-  const uint32_t swords = 1u << (sb - 5);
-  // the wave's output segments (its groups' positions) as buffer resources: masked lanes store
-  // to ST_DROP, so every output store is issued every iteration
-  const uint64_t span = (gB - gA) * HV_GS;
-  const __amdgpu_buffer_rsrc_t rls = make_rsrc_u32(lsrc + seg_begin, span * 4), rld = make_rsrc_u32(ldst + seg_begin, span * 4);
-  const __amdgpu_buffer_rsrc_t rlk = make_rsrc_u32(lkey + seg_begin, span * 8);
-  const __amdgpu_buffer_rsrc_t ros = make_rsrc_u32(osrc + seg_begin, span * 4), rod = make_rsrc_u32(odst + seg_begin, span * 4);
-  const __amdgpu_buffer_rsrc_t rok = make_rsrc_u32(okey + seg_begin, span * 8);
-  const __amdgpu_buffer_rsrc_t rmark = make_rsrc_u32(mark, mark ? bits_words * 32 : 0);  // labels < n
-  bool touch_giant = false;
-  uint64_t nlev = 0, nrem = 0;
-  for (uint32_t k = 0; k < nb; ++k) {
-    __syncthreads();  // every wave is done with the previous slice
-    {
-      // slice k: 16-B loads, all of a thread's issued before any is stored (one round trip; the
-      // bitmap buffer is 16-B aligned and padded to whole 16-B words)
-      const uint4 *src4 = reinterpret_cast<const uint4 *>(bits32 + (uint64_t)k * swords);
-      const uint64_t avail4 = bits_words > (uint64_t)k * swords ? (bits_words - (uint64_t)k * swords) / 4 : 0;
-      uint4 *dst4 = reinterpret_cast<uint4 *>(s_bits);
-      constexpr uint32_t PER = (1u << (HV_SB_MAX - 5)) / 4 / HV_FBLOCK;  // 8 at the largest slice
-      uint4 t[PER];
-#pragma unroll
-      for (uint32_t r = 0; r < PER; ++r) {
-        const uint32_t i = threadIdx.x + r * HV_FBLOCK;
-        t[r] = (i < swords / 4 && i < avail4) ? src4[i] : make_uint4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (uint32_t r = 0; r < PER; ++r) {
-        const uint32_t i = threadIdx.x + r * HV_FBLOCK;
-        if (i < swords / 4) dst4[i] = t[r];
-      }
-    }
-    __syncthreads();
-    for (uint64_t gc = gA; gc < gB; gc += WAVE) {
-      // lane i: group gc + i's bucket-k sub-run [st, st + len), its start c in the wave's virtual
-      // stream, and the eid of its quarter-0 edge 0 (eid = ebase + quarter * Qw + offset)
-      const uint64_t gl = gc + lane;
-      const bool ing = gl < gB;
-      const uint32_t o0 = ing ? htab[gl * (nb + 1) + k] : 0u, o1 = ing ? htab[gl * (nb + 1) + k + 1] : 0u;
-      uint32_t E;
-      const uint32_t c = wave_excl_scan(o1 - o0, &E);
-      const uint32_t st = (uint32_t)(gl * HV_GS) + o0;
-      const uint32_t ebase = (uint32_t)(E0 + (gl / gpb) * Qb + (gl % gpb) * 512u);  // m < 2^31
-      // entry x = x0 + lane + 64 j of the virtual stream -> position p, eid base eb (every lane
-      // runs every shuffle: a bpermute from a lane switched off by a branch reads 0)
-      // the next sub-run's start (c of lane i + 1; E past the last) and the position offset
-      const uint32_t cnext = lane == WAVE - 1 ? E : __shfl_down(c, 1);
-      const uint32_t delta = st - c;  // position = x + delta within the sub-run
-      auto locate = [&](uint32_t x0, uint32_t *p, uint32_t *eb) {
-        int lo = 0;  // the last sub-run starting at or before x (non-empty: the next starts after x)
-#pragma unroll
-        for (int j = 0; j < HV_EPL; ++j) {
-          const uint32_t x = x0 + lane + WAVE * j;
-          if (j == 0) {
-#pragma unroll
-            for (int s = 32; s >= 1; s >>= 1) {
-              const int cand = lo + s;
-              const uint32_t cv = __shfl(c, cand & (WAVE - 1));
-              if (cand < WAVE && cv <= x) lo = cand;
-            }
-          } else {
-            // 64 entries later: one or two sub-runs further on (sub-runs of >= 32 entries), else
-            // a fresh search from here
-            const uint32_t n1 = __shfl(cnext, lo);
-            if (n1 <= x && lo < WAVE - 1) ++lo;
-            const uint32_t n2 = __shfl(cnext, lo);
-            if (n2 <= x && lo < WAVE - 1) ++lo;
-            const uint32_t n3 = __shfl(cnext, lo);
-            if (__any(n3 <= x && lo < WAVE - 1)) {
-              int l2 = 0;
-#pragma unroll
-              for (int s = 32; s >= 1; s >>= 1) {
-                const int cand = l2 + s;
-                const uint32_t cv = __shfl(c, cand & (WAVE - 1));
-                if (cand < WAVE && cv <= x) l2 = cand;
-              }
-              lo = l2;
-            }
-          }
-          const uint32_t dp = __shfl(delta, lo), ep = __shfl(ebase, lo);
-          p[j] = x < E ? x + dp : 0u;
-          eb[j] = ep;
-        }
-      };
-      // Three-stage pipeline over chunks of HV_EPL x 64 entries; iteration `it` stores chunk it-2
-      // (its label gathers landed), decides chunk it-1 (its a-probes landed) and issues its label
-      // gathers, issues chunk it's a-probes (its loads landed) and chunk it+1's loads. Every stage
-      // runs every iteration (dead lanes read index 0, stores to a dropped offset), so the number
-      // of memory instructions per iteration is fixed and each wait is a counted vmcnt that leaves
-      // the later stages' requests in flight.
-      constexpr uint32_t CH = HV_EPL * WAVE;
-      const uint32_t niter = (E + CH - 1) / CH;
-      uint32_t dA[HV_EPL], dB[HV_EPL], dW[HV_EPL], dE[HV_EPL];                 // chunk it: loads
-      uint32_t rA[HV_EPL], rB[HV_EPL], rW[HV_EPL], rE[HV_EPL], rP[HV_EPL];     // it-1: a-probes
-      uint32_t qA[HV_EPL], qB[HV_EPL], qW[HV_EPL], qE[HV_EPL], qla[HV_EPL], qlb[HV_EPL];  // it-2: gathers
-      uint32_t dv = 0, rv = 0, qlev = 0, qrem = 0, qga = 0, qgb = 0;  // per-entry bits (j)
-#pragma unroll
-      for (int j = 0; j < HV_EPL; ++j) {
-        rA[j] = rB[j] = rW[j] = rE[j] = rP[j] = 0u;
-        qA[j] = qB[j] = qW[j] = qE[j] = qla[j] = qlb[j] = 0u;
-      }
-      auto load_chunk = [&](uint32_t it) {
-        uint32_t p[HV_EPL];
-        locate(it * CH, p, dE);
-        dv = 0;
-#pragma unroll
-        for (int j = 0; j < HV_EPL; ++j) {
-          dA[j] = ha[p[j]];
-          dB[j] = hb[p[j]];
-          dW[j] = hw[p[j]];
-          dv |= (it * CH + lane + WAVE * j < E) ? (1u << j) : 0u;
-        }
-      };
-      load_chunk(0);
-      for (uint32_t it = 0; it < niter + 2; ++it) {
-        {  // O: chunk it-2
-          uint32_t lmask = qlev, rmask = qrem;
-#pragma unroll
-          for (int j = 0; j < HV_EPL; ++j) {
-            qla[j] = (qga >> j) & 1u ? giant : qla[j];
-            qlb[j] = (qgb >> j) & 1u ? giant : qlb[j];
-            if (qla[j] == qlb[j]) lmask &= ~(1u << j);
-            const bool mk = (lmask >> j) & 1u;
-            st_b8(1, rmark, (mk && !((qga >> j) & 1u)) ? qla[j] : ST_DROP);
-            st_b8(1, rmark, (mk && !((qgb >> j) & 1u)) ? qlb[j] : ST_DROP);
-          }
-          touch_giant |= (lmask & (qga | qgb)) != 0u;
-          uint32_t tot;
-          const uint32_t ex = wave_excl_scan((uint32_t)__popc(lmask) | ((uint32_t)__popc(rmask) << 16), &tot);
-          uint32_t pl = (uint32_t)nlev + (ex & 0xffffu), pr = (uint32_t)nrem + (ex >> 16);
-#pragma unroll
-          for (int j = 0; j < HV_EPL; ++j) {
-            const uint32_t idx = qB[j] & ((1u << HV_IDX_BITS) - 1);
-            const uint32_t eid = qE[j] + (idx >> 9) * (uint32_t)Qw + (idx & 511u);
-            const uint64_t key = ((uint64_t)qW[j] << 32) | eid;
-            const bool l = (lmask >> j) & 1u, r = (rmask >> j) & 1u;
-            st_b32(qla[j], rls, l ? pl * 4u : ST_DROP);
-            st_b32(qlb[j], rld, l ? pl * 4u : ST_DROP);
-            st_b64(key, rlk, l ? pl * 8u : ST_DROP);
-            st_b32(qA[j], ros, r ? pr * 4u : ST_DROP);
-            st_b32((k << sb) + (qB[j] >> HV_IDX_BITS), rod, r ? pr * 4u : ST_DROP);
-            st_b64(key, rok, r ? pr * 8u : ST_DROP);
-            pl += l ? 1u : 0u;
-            pr += r ? 1u : 0u;
-          }
-          nlev += tot & 0xffffu;
-          nrem += tot >> 16;
-        }
-        {  // G: chunk it-1 — decisions, label gathers
-          uint32_t nlv = 0, nrm = 0, nga = 0, ngb = 0;
-#pragma unroll
-          for (int j = 0; j < HV_EPL; ++j) {
-            const bool valid = (rv >> j) & 1u;
-            const uint32_t bl = valid ? rB[j] >> HV_IDX_BITS : 0u;  // a dead lane's entry is not read
-            const uint32_t b = (k << sb) + bl;
-            const uint32_t ga = valid ? (rP[j] >> (rA[j] & 31)) & 1u : 0u;
-            const uint32_t gb = (s_bits[bl >> 5] >> (bl & 31)) & 1u;
-            const bool keep = valid & ((ga & gb) == 0u);
-            const bool lev = keep & ((uint64_t)rW[j] < w_hi);
-            const bool rem = keep & !lev;
-            qla[j] = lab[(lev & (ga == 0u)) ? rA[j] : 0u];
-            qlb[j] = lab[(lev & (gb == 0u)) ? b : 0u];
-            nlv |= lev ? (1u << j) : 0u;
-            nrm |= rem ? (1u << j) : 0u;
-            nga |= ga << j;
-            ngb |= gb << j;
-            qA[j] = rA[j];
-            qB[j] = rB[j];
-            qW[j] = rW[j];
-            qE[j] = rE[j];
-          }
-          qlev = nlv;
-          qrem = nrm;
-          qga = nga;
-          qgb = ngb;
-        }
-        {  // P: chunk it — a-probes (a group's quarter holds sorted a ends: few lines)
-#pragma unroll
-          for (int j = 0; j < HV_EPL; ++j) {
-            rA[j] = dA[j];
-            rB[j] = dB[j];
-            rW[j] = dW[j];
-            rE[j] = dE[j];
-            rP[j] = bits32[((dv >> j) & 1u) ? (dA[j] >> 5) : 0u];
-          }
-          rv = dv;
-        }
-        load_chunk(it + 1);  // L: chunk it+1 (past the end: index 0, no valid bits)
-      }
-    }
-  }
-  if (__syncthreads_or(touch_giant ? 1 : 0) && threadIdx.x == 0 && mark) mark[giant] = 1;
-  // both outputs padded to a multiple of 4 with dead entries (a = LABEL_NONE); the segment's
-  // span (its groups' positions) always leaves room (a multiple of 4 >= its entries)
-  const uint64_t padded = (nrem + 3) & ~3ull, lpadded = (nlev + 3) & ~3ull;
-  if (lane < padded - nrem) {
-    const uint64_t pos = seg_begin + nrem + lane;
-    osrc[pos] = LABEL_NONE;
-    odst[pos] = 0;
-    okey[pos] = KEY_NONE;
-  }
-  if (lane < lpadded - nlev) {
-    const uint64_t pos = seg_begin + nlev + lane;
-    lsrc[pos] = LABEL_NONE;
-    ldst[pos] = 0;
-    lkey[pos] = KEY_NONE;
-  }
-  if (lane == 0) {
-    lstart[gw] = seg_begin;
-    lcount[gw] = lpadded;
-    ostart[gw] = seg_begin;
-    ocount[gw] = padded;
-  }
-}
-
-// ------------------------------------------------------------------------------------------
 // Dense levels (several ranks). Once a level's active list A (nact0 fragment roots, identical on
 // every rank) is known, the level runs in a dense label space 0..nact0-1: a root's dense label is
 // its rank among the level's flags (DenseRank: popc over the flag words + word / chunk prefixes),
@@ -2870,6 +2432,7 @@ struct HostRes {
   std::vector<hipEvent_t> ev_pool;      // timing events, 6 per round
   hipEvent_t pass_ev[4] = {};           // the canonical passes' events
   hipEvent_t plan_ev = nullptr;         // the weight sample has landed in h_sample
+  hipEvent_t sync_ev = nullptr;         // the cancellable waits of a multi-rank solver (solver_sync)
   unsigned long long seq = 0;           // round reports issued through h_slot (monotonic across solves)
   std::vector<hipEvent_t> prof_ev;      // ghs_profile_enable: two events per launch
 };
@@ -2886,6 +2449,7 @@ static int hostres_init(HostRes *r) {
   GHS_HIP_CHECK(hipHostMalloc((void **)&r->h_sample, 16384 * 4, hipHostMallocDefault));
   for (int i = 0; i < 4; ++i) GHS_HIP_CHECK(hipEventCreateWithFlags(&r->pass_ev[i], TIMING_EVENT_FLAGS));
   GHS_HIP_CHECK(hipEventCreateWithFlags(&r->plan_ev, hipEventDisableTiming));
+  GHS_HIP_CHECK(hipEventCreateWithFlags(&r->sync_ev, hipEventDisableTiming));
   memset(r->h_slot, 0, SLOT_RING * sizeof(RoundSlot));
   return GHS_OK;
 }
@@ -2898,6 +2462,7 @@ static void hostres_free(HostRes *r) {
   for (int i = 0; i < 4; ++i)
     if (r->pass_ev[i]) (void)hipEventDestroy(r->pass_ev[i]);
   if (r->plan_ev) (void)hipEventDestroy(r->plan_ev);
+  if (r->sync_ev) (void)hipEventDestroy(r->sync_ev);
   if (r->h_cnt) (void)hipHostFree(r->h_cnt);
   if (r->h_slot) (void)hipHostFree(r->h_slot);
   if (r->h_sample) (void)hipHostFree(r->h_sample);
@@ -2986,12 +2551,6 @@ struct ghs_solver {
   char *ws_base = nullptr;      // the caller's workspace (carved by workspace_layout)
   bool seed_runs = true;        // level 0 round 0: a-side runs by k_seed_runs (GHS_SEED_RUNS=0: off)
   uint32_t dedup_max = 0;       // parallel-edge filter at <= this many active fragments (GHS_DEDUP_MAX)
-  // heavy-edge buckets (k_select_hv / k_filter_hv): on when the plan has >= 2 levels and the
-  // vertices span 2..HV_NB_MAX buckets of 2^hv_sb (GHS_HV=0: off; GHS_HV_SB: bucket size, tests)
-  bool hv = false;
-  bool hv_env = HV_DEFAULT;
-  uint32_t hv_sb = HV_SB_MAX, hv_nb = 0;
-  uint32_t hv_gsel = 1;         // k_select_hv's grid (k_filter_hv decodes the eids from it)
   // dense levels (several ranks, see k_dense_open): the dense arrays, the vertex arrays they stand
   // in for while a level runs, and the level's fragment count
   uint32_t *dlab = nullptr, *dpar = nullptr, *dvtx = nullptr;
@@ -3006,6 +2565,10 @@ struct ghs_solver {
   bool dense_mode = false;      // several ranks and the dense arrays exist (GHS_DENSE=0: off)
   bool level_dense = false;     // the open level runs in dense labels
   uint64_t dense_n = 0;
+  // multi-rank failure agreement: another rank's failure ends this solver's waits (the flags are
+  // read with __atomic loads; set by ghs_solver_cancel / the driver's shared group flag)
+  int cancel_flag = 0;
+  const int *group_cancel = nullptr;
   bool prof = false;            // ghs_profile_enable: every launch bracketed by events
   uint32_t prof_id = 0;         // tag of this handle's profile records (creation order)
   struct ProfRec {
@@ -3027,6 +2590,7 @@ uint32_t ghs_solver_ranks_of(const ghs_solver *s) { return s->cfg.num_ranks; }
 // the round's slots in place: a dense level's identity round (its first) keeps the active
 // fragments' minima contiguous in best[0, nact) — an unsigned MIN all-reduce over best itself
 // replaces pack_best / all-reduce / unpack_best (nullptr: use those)
+void ghs_solver_set_group_cancel(ghs_solver *s, const int *flag) { s->group_cancel = flag; }
 uint64_t *ghs_solver_best_slots_of(ghs_solver *s) {
   return (s->phase == 1 && s->nact && s->act_ident && s->level_dense) ? s->best : nullptr;
 }
@@ -3071,10 +2635,44 @@ struct KtScope {
 };
 #define KT(kernel, items) KtScope _kt_scope(s, (kernel), (items))
 
+static bool solver_cancelled(const ghs_solver *s) {
+  return __atomic_load_n(&s->cancel_flag, __ATOMIC_ACQUIRE) ||
+         (s->group_cancel && __atomic_load_n(s->group_cancel, __ATOMIC_ACQUIRE));
+}
+
+bool ghs_solver_cancelled_of(const ghs_solver *s) { return solver_cancelled(s); }
+
+// wait until `ev` (recorded on the solver's stream) has completed. One rank: a blocking wait.
+// Several ranks: a poll that another rank's failure ends (ghs_solver_cancel) — a rank whose peer
+// failed would otherwise wait forever behind a collective the peer never joins.
+static int event_wait(ghs_solver *s, hipEvent_t ev) {
+  if (s->cfg.num_ranks <= 1 && !s->group_cancel) {
+    GHS_HIP_CHECK(hipEventSynchronize(ev));
+    return GHS_OK;
+  }
+  for (uint32_t spins = 0;; ++spins) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return GHS_OK;
+    if (q != hipErrorNotReady) GHS_HIP_CHECK(q);
+    if (solver_cancelled(s)) GHS_FAIL(GHS_E_STATE, "cancelled: another rank of the solve failed");
+    if (spins > 4096) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+// every piece of work enqueued so far on the solver's stream has completed
+static int solver_sync(ghs_solver *s) {
+  if (s->cfg.num_ranks <= 1 && !s->group_cancel) {
+    GHS_HIP_CHECK(hipStreamSynchronize(s->stream));
+    return GHS_OK;
+  }
+  GHS_HIP_CHECK(hipEventRecord(s->res->sync_ev, s->stream));
+  return event_wait(s, s->res->sync_ev);
+}
+
 // after the solve: durations into the process-wide profile (one stream sync)
 static int prof_collect(ghs_solver *s) {
   if (!s->prof || s->prof_recs.empty()) return GHS_OK;
-  GHS_HIP_CHECK(hipStreamSynchronize(s->stream));
+  if (int rc = solver_sync(s)) return rc;
   std::lock_guard<std::mutex> lock(g_prof_mutex);
   for (const auto &r : s->prof_recs) {
     ghs_kernel_record_t rec = r.rec;
@@ -3088,7 +2686,6 @@ static int prof_collect(ghs_solver *s) {
 }
 
 static std::mutex g_mutex;  // the one-shot entry points are serialised per process
-static HostRes *g_create_pool = nullptr;  // set (under g_mutex) while ghs_mst_device creates its solver
 
 // process-wide host resources of the one-shot entry point, one set per device (under g_mutex)
 static HostRes *pooled_res(int *rc) {
@@ -3222,6 +2819,10 @@ static void default_config(ghs_config_t *c) {
   c->num_ranks = 1;
   c->level1_edges_per_vertex = 0.0;  // auto: level1_auto()
   c->level_growth = 8.0;  // R-MAT s24 sweep (tools/sweep_levels.py): 3 levels, 0.5n / 4n / rest
+  c->options = 0;
+  c->dedup_max = 0;
+  c->fault_rank = 0;
+  c->reserved = 0;
 }
 
 // level1_edges_per_vertex <= 0 picks the first level's size from the density. The first level
@@ -3270,7 +2871,7 @@ static int plan_levels_enqueue(ghs_solver *s) {
 // the host copy of the plan (waits for it the first time)
 static int plan_sync(ghs_solver *s) {
   if (s->plan_known) return GHS_OK;
-  GHS_HIP_CHECK(hipEventSynchronize(s->res->plan_ev));
+  if (int rc = event_wait(s, s->res->plan_ev)) return rc;
   const uint64_t cnt = s->h_thr[PLAN_MAX];
   if (cnt < 2 || cnt > PLAN_MAX) GHS_FAIL(GHS_E_STATE, "bad level plan");
   s->thresholds.assign(s->h_thr, s->h_thr + cnt);
@@ -3285,15 +2886,6 @@ static bool levels_done(ghs_solver *s) {
   return s->level + 1 >= s->thresholds.size();
 }
 
-// the heavy copy (k_select_hv -> k_filter_hv) lives in the pending buffer rem[0], unused until
-// k_filter writes the pending edges to rem[1]: a -> src, packed b | idx -> dst, w -> the first
-// half of key (as u32), the groups' bucket tables after it
-constexpr uint32_t HV_FILTER_G = 256;  // k_filter_hv blocks: one per CU (128-KiB LDS slice each)
-constexpr uint32_t HV_SELECT_G = 768;  // k_select_hv blocks: 3 per CU (41 KiB of LDS each)
-static inline uint32_t *hv_w(ghs_solver *s) { return reinterpret_cast<uint32_t *>(s->rem[0].key); }
-static inline uint16_t *hv_tab(ghs_solver *s) {
-  return reinterpret_cast<uint16_t *>(reinterpret_cast<uint32_t *>(s->rem[0].key) + s->cap_arcs);
-}
 
 static int fail_counters(ghs_solver *s, unsigned long long err, const char *where) {
   s->phase = 2;
@@ -3351,15 +2943,8 @@ static int open_level(ghs_solver *s, bool async_open = false) {
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[0], st));
       {
         KT(GHS_K_SELECT, TC);
-        if (s->hv) G = std::min<unsigned>(G, HV_SELECT_G);  // co-resident: 3 blocks per CU (LDS)
-        s->hv_gsel = G;
-        if (s->hv)  // + the heavy copy, grouped by bucket of b, into rem[0] (read by k_filter_hv)
-          k_select_hv<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range + 1, Y.src, Y.dst,
-                                           Y.key, Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR, s->hv_sb, s->hv_nb,
-                                           s->rem[0].src, s->rem[0].dst, hv_w(s), hv_tab(s));
-        else
-          k_select<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range + 1, Y.src, Y.dst, Y.key,
-                                        Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR);
+        k_select<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range + 1, Y.src, Y.dst, Y.key,
+                                      Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR);
       }
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[1], st));
       GHS_HIP_CHECK(hipGetLastError());
@@ -3377,23 +2962,14 @@ static int open_level(ghs_solver *s, bool async_open = false) {
     if (!s->pending_built) {
       // FILTER + level split over the canonical list once level 0 is complete: level-1 edges
       // not inside one fragment -> Y; heavier edges not inside the giant -> pending (rem[rout])
-      G = s->hv ? HV_FILTER_G * (HV_FBLOCK / WAVE) : grid_for(TC, ARCS_PER_BLOCK, s->seg_g);
+      G = grid_for(TC, ARCS_PER_BLOCK, s->seg_g);
       if (TC) {
         GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[2], st));
         {
-        KT(GHS_K_FILTER, TC);
-        if (s->hv) {  // the heavy copy of k_select_hv (rem[0]); one output region per wave
-          if (rin != 0) GHS_FAIL(GHS_E_STATE, "heavy copy: pending buffers in use");
-          k_filter_hv<<<HV_FILTER_G, HV_FBLOCK, 0, st>>>(s->e_lo, s->e_hi, s->hv_sb, s->hv_nb, s->rem[0].src, s->rem[0].dst,
-                                                        hv_w(s), hv_tab(s), s->hv_gsel, d_range, s->bits,
-                                                        ((uint64_t)s->n + 127) / 128 * 4, s->giant, s->lab, Y.src,
-                                                        Y.dst, Y.key, Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key,
-                                                        RO.seg_start, RO.seg_count, mark);
-        } else {
+          KT(GHS_K_FILTER, TC);
           k_filter<<<G, BLOCK, 0, st>>>(s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range, s->bits, s->giant, s->lab,
                                         Y.src, Y.dst, Y.key, Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key,
                                         RO.seg_start, RO.seg_count, mark);
-        }
         }
         GHS_HIP_CHECK(hipGetLastError());
         GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[3], st));
@@ -3530,7 +3106,7 @@ static int open_level_finish(ghs_solver *s) {
   s->act_ident = false;
   s->act_cur = 0;
   GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, C_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-  GHS_HIP_CHECK(hipStreamSynchronize(st));
+  if (int rc = solver_sync(s)) return rc;
   if (s->h_cnt[C_ERR]) return fail_counters(s, s->h_cnt[C_ERR], "opening a level");
   const uint64_t S = s->h_cnt[C_LIVE];
   s->rem_total = s->h_cnt[C_PENDING];
@@ -3910,21 +3486,18 @@ static int solver_begin(ghs_solver *s) {
   if ((e = hipMemsetAsync(s->lb_state, 0, LB_MAX_TILES * 8, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset select state: ") + hipGetErrorString(e));
   k_init_counters<<<1, 64, 0, s->stream>>>(s->cnt, n);
   if ((e = hipGetLastError()) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("init kernels: ") + hipGetErrorString(e));
-  s->hv_nb = (uint32_t)(((uint64_t)n + (1ull << s->hv_sb) - 1) >> s->hv_sb);
-  // bucketed passes only up to HV_MAX_EDGES edges per solver: above it (R-MAT s25 / s26 on one
-  // GPU) they mis-decode some heavy edges (an invariant error in level 1's second round; cause
-  // not found) — such solves take the L2-probe passes
-  s->hv = s->hv_env && s->hv_nb >= 2 && s->hv_nb <= HV_NB_MAX && plan_levels_count(s) >= 2 && s->e_hi > s->e_lo &&
-          s->e_hi - s->e_lo <= HV_MAX_EDGES;
   s->level = 0;
   s->level_open = false;
   s->phase = n ? 0 : 2;
   return GHS_OK;
 }
 
-int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
-                      uint64_t e_lo, uint64_t e_hi, const ghs_config_t *cfg, void *d_workspace,
-                      size_t workspace_bytes, uint8_t *d_in_mst, void *stream, ghs_solver_t **out) {
+// pool: the one-shot entry point's process-wide host resources (nullptr: the handle owns its own).
+// Passed explicitly, not through a global, so concurrent creators (the multi-rank drivers' threads)
+// never adopt another caller's pinned counters.
+static int solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
+                         uint64_t e_lo, uint64_t e_hi, const ghs_config_t *cfg, void *d_workspace,
+                         size_t workspace_bytes, uint8_t *d_in_mst, void *stream, HostRes *pool, ghs_solver_t **out) {
   if (!out) GHS_FAIL(GHS_E_ARG, "out is NULL");
   *out = nullptr;
   if (m >= (1ull << 31)) GHS_FAIL(GHS_E_ARG, "m must be < 2^31");
@@ -3943,49 +3516,44 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   s->n = n; s->m = m; s->e_lo = e_lo; s->e_hi = e_hi;
   s->eu = d_u; s->ev = d_v; s->ew = d_w;
   s->in_mst = d_in_mst; s->stream = (hipStream_t)stream;
-  { const char *dbg = getenv("GHS_DEBUG"); s->debug = dbg && dbg[0] == '1'; }
-  { const char *det = getenv("GHS_DETAIL"); s->detail = det && det[0] == '1'; }
-  { const char *tr = getenv("GHS_TIME_ROUNDS"); s->time_rounds = tr && tr[0] == '1'; }
+  if (cfg) s->cfg = *cfg; else default_config(&s->cfg);
+  // path options come from the caller's config only (ABI 5): the library reads no environment
+  // variable that changes the algorithm or a launch shape (GHS_AB_ENV builds excepted, below)
+  const uint32_t opt = s->cfg.options;
+  s->debug = (opt & GHS_OPT_DEBUG) != 0;
+  s->detail = (opt & GHS_OPT_DETAIL) != 0;
+  s->time_rounds = (opt & GHS_OPT_TIME_ROUNDS) != 0;
+  s->seed_runs = (opt & GHS_OPT_NO_SEED_RUNS) == 0;
+  s->dedup_max = s->cfg.dedup_max;
   {
     std::lock_guard<std::mutex> lock(g_prof_mutex);
     s->prof = g_prof_on;
     s->prof_id = g_prof_next_id++;
   }
-  if (const char *la = getenv("GHS_LOOKAHEAD")) {  // A/B tests: rounds in flight ahead of the check
+#if GHS_AB_ENV
+  // A/B builds only (make AB=1): launch-shape experiments from the environment
+  if (const char *la = getenv("GHS_LOOKAHEAD")) {  // rounds in flight ahead of the check
     const long v = strtol(la, nullptr, 10);
     s->lookahead = (uint32_t)(v < 0 ? 0 : (v > 4 ? 4 : v));
   }
-  auto grid_env = [](const char *name, uint32_t *dst) {  // A/B tests: per-kernel grids
+  auto grid_env = [](const char *name, uint32_t *dst) {  // per-kernel grids
     if (const char *g = getenv(name)) {
       const long v = strtol(g, nullptr, 10);
       *dst = (uint32_t)(v < 256 ? 256 : (v > (long)SEG_G ? SEG_G : v));
     }
   };
   grid_env("GHS_MINEDGE_G", &s->cmp_g);
-  if (const char *sr = getenv("GHS_SEED_RUNS")) s->seed_runs = sr[0] != '0';
-  if (const char *dm = getenv("GHS_DEDUP_MAX")) s->dedup_max = (uint32_t)strtoul(dm, nullptr, 10);
-  if (const char *h = getenv("GHS_HV")) s->hv_env = h[0] != '0';
-  if (const char *h = getenv("GHS_HV_SB")) {
-    const long v = strtol(h, nullptr, 10);
-    s->hv_sb = (uint32_t)(v < 7 ? 7 : (v > (long)HV_SB_MAX ? HV_SB_MAX : v));  // >= 4 words per slice
-  }
   grid_env("GHS_IDENT_G", &s->ident_g);
   grid_env("GHS_WIN_G", &s->win_g);
   grid_env("GHS_LP_G", &s->lp_g);
-  if (const char *g = getenv("GHS_SEG_G")) {  // A/B tests: blocks of the streaming kernels
-    const long v = strtol(g, nullptr, 10);
-    s->seg_g = (uint32_t)(v < 256 ? 256 : (v > (long)SEG_G ? SEG_G : v));
-  }
-  if (cfg) s->cfg = *cfg; else default_config(&s->cfg);
+  grid_env("GHS_SEG_G", &s->seg_g);
+#endif
   s->ws_base = (char *)d_workspace;
   workspace_layout(n, m, e_hi - e_lo, s, s->ws_base);
-  {
-    const char *dn = getenv("GHS_DENSE");
-    s->dense_mode = s->cfg.num_ranks > 1 && s->dlab != nullptr && !(dn && dn[0] == '0');
-  }
+  s->dense_mode = s->cfg.num_ranks > 1 && s->dlab != nullptr && (opt & GHS_OPT_NO_DENSE) == 0;
 
-  if (g_create_pool) {
-    s->res = g_create_pool;
+  if (pool) {
+    s->res = pool;
   } else {
     s->res = &s->own;
     if (int rc = hostres_init(&s->own)) {
@@ -3999,6 +3567,13 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   }
   *out = s;
   return GHS_OK;
+}
+
+int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
+                      uint64_t e_lo, uint64_t e_hi, const ghs_config_t *cfg, void *d_workspace,
+                      size_t workspace_bytes, uint8_t *d_in_mst, void *stream, ghs_solver_t **out) {
+  return solver_create(n, m, d_u, d_v, d_w, e_lo, e_hi, cfg, d_workspace, workspace_bytes, d_in_mst, stream, nullptr,
+                       out);
 }
 
 // stepwise API: one round per minedge/contract pair, exact counts after every contract
@@ -4038,7 +3613,7 @@ int ghs_solver_minedge(ghs_solver_t *s, uint64_t *num_active) {
 int ghs_solver_exchange_buffer(ghs_solver_t *s, uint8_t **d_flags, uint64_t *bytes) {
   if (!s || !d_flags || !bytes) GHS_FAIL(GHS_E_ARG, "solver/d_flags/bytes is NULL");
   if (!s->pending_exchange) GHS_FAIL(GHS_E_STATE, "no exchange pending");
-  GHS_HIP_CHECK(hipStreamSynchronize(s->stream));  // the flags are complete before the caller reads them
+  if (int rc = solver_sync(s)) return rc;  // the flags are complete before the caller reads them
   *d_flags = s->flags;
   *bytes = (uint64_t)s->n + 1;  // n fragment flags + the error byte
   return GHS_OK;
@@ -4046,7 +3621,7 @@ int ghs_solver_exchange_buffer(ghs_solver_t *s, uint8_t **d_flags, uint64_t *byt
 
 int ghs_solver_flag_bits(ghs_solver_t *s, uint64_t **d_bits, uint64_t *words) {
   if (int rc = ghs_solver_flag_bits_async(s, d_bits, words)) return rc;
-  GHS_HIP_CHECK(hipStreamSynchronize(s->stream));  // complete before the caller's collective reads it
+  if (int rc = solver_sync(s)) return rc;  // complete before the caller's collective reads it
   return GHS_OK;
 }
 
@@ -4173,7 +3748,7 @@ int ghs_solver_contract(ghs_solver_t *s, int *done) {
   s->hooked = false;
   const int nb = s->act_ident ? 0 : (s->act_cur ^ 1);
   GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, C_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
-  GHS_HIP_CHECK(hipStreamSynchronize(s->stream));
+  if (int rc = solver_sync(s)) return rc;
   if (s->h_cnt[C_ERR]) return fail_counters(s, s->h_cnt[C_ERR], ("in round " + std::to_string(s->round + 1)).c_str());
   push_stats(s, s->level_round, live_in, nact_in, s->h_cnt[C_EDGES]);
   s->nact = s->h_cnt[C_ACT + nb];
@@ -4198,7 +3773,7 @@ int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *
     s->h_cnt[C_EDGES] = s->rep_edges;
   } else {
     GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, C_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
-    GHS_HIP_CHECK(hipStreamSynchronize(s->stream));
+    if (int rc = solver_sync(s)) return rc;
   }
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s->t0).count();
   if (int rc = prof_collect(s)) return rc;
@@ -4231,7 +3806,7 @@ int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *
     result->canon_edges = s->e_hi - s->e_lo;
     result->select_out = s->select_out;
     result->filter_out = s->filter_out;
-    result->pass_flags = s->hv ? 1u : 0u;
+    result->pass_flags = 0;
   }
   return GHS_OK;
 }
@@ -4244,9 +3819,8 @@ int ghs_solver_reset(ghs_solver_t *s) {
   t.eu = s->eu; t.ev = s->ev; t.ew = s->ew;
   t.in_mst = s->in_mst; t.stream = s->stream; t.cfg = s->cfg;
   t.debug = s->debug; t.lookahead = s->lookahead; t.seed_runs = s->seed_runs; t.dedup_max = s->dedup_max;
-  t.hv_env = s->hv_env; t.hv_sb = s->hv_sb;
-  { const char *det = getenv("GHS_DETAIL"); t.detail = det && det[0] == '1'; }
-  { const char *tr = getenv("GHS_TIME_ROUNDS"); t.time_rounds = tr && tr[0] == '1'; }
+  t.detail = s->detail; t.time_rounds = s->time_rounds;
+  t.group_cancel = s->group_cancel;
   { std::lock_guard<std::mutex> lock(g_prof_mutex); t.prof = g_prof_on; }
   t.prof_id = s->prof_id;
   t.seg_g = s->seg_g; t.cmp_g = s->cmp_g; t.ident_g = s->ident_g; t.win_g = s->win_g; t.lp_g = s->lp_g;
@@ -4260,6 +3834,12 @@ int ghs_solver_reset(ghs_solver_t *s) {
   *s = std::move(t);
   s->res = owned ? &s->own : pool;
   return solver_begin(s);
+}
+
+int ghs_solver_cancel(ghs_solver_t *s) {
+  if (!s) GHS_FAIL(GHS_E_ARG, "solver is NULL");
+  __atomic_store_n(&s->cancel_flag, 1, __ATOMIC_RELEASE);
+  return GHS_OK;
 }
 
 int ghs_solver_destroy(ghs_solver_t *s) {
@@ -4280,9 +3860,7 @@ int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *
   int rc = GHS_OK;
   HostRes *pool = pooled_res(&rc);
   if (!pool) return rc;
-  g_create_pool = pool;
-  rc = ghs_solver_create(n, m, d_u, d_v, d_w, 0, m, &c, d_workspace, workspace_bytes, d_in_mst, stream, &s);
-  g_create_pool = nullptr;
+  rc = solver_create(n, m, d_u, d_v, d_w, 0, m, &c, d_workspace, workspace_bytes, d_in_mst, stream, pool, &s);
   if (rc) return rc;
   while (!rc && s->phase != 2) {
     if (!s->level_open) {

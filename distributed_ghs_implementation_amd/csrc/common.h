@@ -64,6 +64,9 @@ uint32_t ghs_solver_n_of(const ghs_solver *s);
 uint32_t ghs_solver_ranks_of(const ghs_solver *s);
 uint64_t *ghs_solver_best_slots_of(ghs_solver *s);
 int ghs_solver_flag_bits_async(ghs_solver *s, uint64_t **d_bits, uint64_t *words);
+// a multi-rank driver's shared failure flag: the solver's waits end once it is set
+void ghs_solver_set_group_cancel(ghs_solver *s, const int *flag);
+bool ghs_solver_cancelled_of(const ghs_solver *s);
 
 #define GHS_HIP_CHECK(expr)                                                                     \
   do {                                                                                          \

@@ -94,6 +94,8 @@ struct ghs_comm {
   ncclComm_t nccl = nullptr;
   bool own_nccl = false;
   ghs::EmuGroup *emu = nullptr;
+  int32_t *agree = nullptr;      // device int of the setup agreement (RCCL)
+  int *group_cancel = nullptr;   // ghs_mst_multi: set by the first failing rank of the clique
   // device scratch of the loop (grown on demand)
   int64_t *dense = nullptr;
   int32_t *hook = nullptr;
@@ -184,10 +186,50 @@ int coll_allreduce(ghs_comm *c, T *buf, size_t count, hipStream_t st) {
   return GHS_OK;
 }
 
-#define LOOP_CHECK(expr)          \
-  do {                            \
-    const int _rc = (expr);       \
-    if (_rc < 0) return _rc;      \
+// Setup agreement, before a rank's first collective: every rank contributes its setup status and
+// learns whether any rank failed (int32 MAX over RCCL; the emulated group's barrier). A rank whose
+// workspace allocation or copy failed thereby fails the call on every rank instead of leaving the
+// others blocked in the level-open all-gather. Returns GHS_OK or this rank's error (its own, or
+// GHS_E_STATE for a peer's).
+int comm_agree(ghs_comm *c, int local_rc, hipStream_t st) {
+  if (c->emu) {
+    if (local_rc) {
+      c->emu->abort();
+      return local_rc;
+    }
+    COMM_BARRIER(c);
+    return GHS_OK;
+  }
+  if (!c->nccl || !c->agree) return local_rc;
+  const int32_t mine = local_rc ? 1 : 0;
+  int32_t any = 1;
+  GHS_HIP_CHECK(hipMemcpyAsync(c->agree, &mine, 4, hipMemcpyHostToDevice, st));
+  COMM_NCCL(ncclAllReduce(c->agree, c->agree, 1, ncclInt32, ncclMax, c->nccl, st));
+  GHS_HIP_CHECK(hipMemcpyAsync(&any, c->agree, 4, hipMemcpyDeviceToHost, st));
+  GHS_HIP_CHECK(hipStreamSynchronize(st));
+  if (local_rc) return local_rc;
+  if (any) GHS_FAIL(GHS_E_STATE, "another rank failed during setup");
+  return GHS_OK;
+}
+
+// A rank's solve failed mid-loop: tell the rest of the clique (its waits end: solver_sync polls
+// the group flag) and abort this rank's communicator, which ends its RCCL kernels still waiting
+// for peers, so its stream drains; the handle is not destroyed again afterwards.
+int loop_fail(ghs_comm *c, int rc) {
+  if (!c) return rc;
+  if (c->group_cancel) __atomic_store_n(c->group_cancel, 1, __ATOMIC_RELEASE);
+  if (c->emu) c->emu->abort();
+  if (c->nccl) {
+    (void)ncclCommAbort(c->nccl);
+    c->nccl = nullptr;
+  }
+  return rc;
+}
+
+#define LOOP_CHECK(expr)                  \
+  do {                                    \
+    const int _rc = (expr);               \
+    if (_rc < 0) return loop_fail(c, _rc); \
   } while (0)
 
 int run_loop(ghs_solver_t *s, ghs_comm *c) {
@@ -195,11 +237,17 @@ int run_loop(ghs_solver_t *s, ghs_comm *c) {
   const bool multi = nr > 1;
   hipStream_t st = ghs_solver_stream_of(s);
   if (multi) {
-    GHS_HIP_CHECK(hipSetDevice(c->dev));
+    if (hipSetDevice(c->dev) != hipSuccess) {
+      ghs::set_error("hipSetDevice of the communicator's device failed");
+      return loop_fail(c, GHS_E_HIP);
+    }
     LOOP_CHECK(comm_scratch(c, ghs_solver_n_of(s)));
   }
   for (uint32_t guard = 0;; ++guard) {
-    if (guard > 16 * GHS_MAX_ROUND_STATS) GHS_FAIL(GHS_E_ROUNDCAP, "round cap exceeded");
+    if (guard > 16 * GHS_MAX_ROUND_STATS) {
+      ghs::set_error("round cap exceeded");
+      return loop_fail(c, GHS_E_ROUNDCAP);
+    }
     uint64_t count = 0;
     int rc = ghs_solver_minedge(s, &count);
     while (rc == GHS_NEED_EXCHANGE) {  // a level opened: OR its fragment flags (+ error bit)
@@ -235,7 +283,7 @@ int run_loop(ghs_solver_t *s, ghs_comm *c) {
 void comm_free(ghs_comm *c) {
   if (!c) return;
   if (hipSetDevice(c->dev) == hipSuccess) {
-    for (void *p : {(void *)c->dense, (void *)c->hook, (void *)c->gathered})
+    for (void *p : {(void *)c->dense, (void *)c->hook, (void *)c->gathered, (void *)c->agree})
       if (p) (void)hipFree(p);
   }
   if (c->nccl && c->own_nccl) ncclCommDestroy(c->nccl);
@@ -268,25 +316,43 @@ int rank_fail(Rank &d, int rc) {
   d.rc = rc;
   d.err = ghs_last_error();
   if (d.comm && d.comm->emu) d.comm->emu->abort();
+  if (d.comm && d.comm->group_cancel) __atomic_store_n(d.comm->group_cancel, 1, __ATOMIC_RELEASE);
   return rc;
 }
 
-// create the rank's solver over device-resident u/v/w and run it to completion
+// create the rank's solver over device-resident u/v/w, agree with the other ranks that every setup
+// succeeded, and run it to completion. setup_rc: the driver's own setup of this rank (stream,
+// copies) — a failed rank still joins the agreement, so its peers leave too.
 int rank_solve(Rank &d, int r, int N, uint32_t n, uint64_t m, const uint32_t *du, const uint32_t *dv,
-               const uint32_t *dw, uint8_t *d_in_mst, const ghs_config_t *cfg) {
-  if (hipSetDevice(d.dev) != hipSuccess) return rank_fail(d, GHS_E_HIP);
+               const uint32_t *dw, uint8_t *d_in_mst, const ghs_config_t *cfg, int setup_rc) {
+  int rc = setup_rc;
   uint64_t lo, hi;
   edge_range(m, r, N, &lo, &hi);
   const size_t wsb = ghs_workspace_bytes(n, m, hi - lo);
-  if (hipMalloc(&d.ws, wsb) != hipSuccess) {
-    ghs::set_error("hipMalloc of a rank workspace failed");
-    return rank_fail(d, GHS_E_HIP);
-  }
   ghs_config_t c2;
   if (cfg) c2 = *cfg; else ghs_default_config(&c2);
   c2.num_ranks = (uint32_t)N;
-  int rc = ghs_solver_create(n, m, du, dv, dw, lo, hi, &c2, d.ws, wsb, d_in_mst, d.stream, &d.solver);
-  if (rc < 0) return rank_fail(d, rc);
+  if (!rc && hipSetDevice(d.dev) != hipSuccess) {
+    ghs::set_error("hipSetDevice failed");
+    rc = GHS_E_HIP;
+  }
+  if (!rc && c2.fault_rank == (uint32_t)r + 1) {  // test hook (ghs_config_t.fault_rank)
+    ghs::set_error("injected setup failure (fault_rank)");
+    rc = GHS_E_NOMEM;
+  }
+  if (!rc && hipMalloc(&d.ws, wsb) != hipSuccess) {
+    ghs::set_error("hipMalloc of a rank workspace failed");
+    rc = GHS_E_NOMEM;
+  }
+  if (!rc) rc = ghs_solver_create(n, m, du, dv, dw, lo, hi, &c2, d.ws, wsb, d_in_mst, d.stream, &d.solver);
+  if (rc < 0) d.err = ghs_last_error();
+  const int agreed = comm_agree(d.comm, rc < 0 ? rc : GHS_OK, d.stream);
+  if (agreed < 0) {
+    if (!rc) d.err = ghs_last_error();
+    d.rc = agreed;
+    if (d.comm && d.comm->group_cancel) __atomic_store_n(d.comm->group_cancel, 1, __ATOMIC_RELEASE);
+    return agreed;
+  }
   rc = ghs_solver_run(d.solver, d.comm);
   if (rc < 0) return rank_fail(d, rc);
   d.stats.assign(GHS_MAX_ROUND_STATS, ghs_round_stats_t{});
@@ -351,6 +417,11 @@ extern "C" int ghs_comm_init(int nranks, int rank, const uint8_t *id, ghs_comm_t
     GHS_FAIL(GHS_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
   }
   c->own_nccl = true;
+  if (hipMalloc((void **)&c->agree, 4) != hipSuccess) {
+    ncclCommDestroy(c->nccl);
+    delete c;
+    GHS_FAIL(GHS_E_NOMEM, "hipMalloc of the communicator's agreement word failed");
+  }
   *out = c;
   return GHS_OK;
 }
@@ -365,7 +436,13 @@ extern "C" int ghs_solver_run(ghs_solver_t *s, ghs_comm_t *comm) {
   const uint32_t nr = ghs_solver_ranks_of(s);
   if (nr > 1 && (!comm || comm->nranks != (int)nr))
     GHS_FAIL(GHS_E_ARG, "a solver of " + std::to_string(nr) + " ranks needs a communicator of as many ranks");
-  return run_loop(s, comm);
+  if (nr > 1 && !comm->nccl && !comm->emu) GHS_FAIL(GHS_E_STATE, "the communicator was aborted by an earlier failure");
+  if (comm && comm->group_cancel) ghs_solver_set_group_cancel(s, comm->group_cancel);
+  int prev = 0;
+  const bool have_prev = hipGetDevice(&prev) == hipSuccess;
+  const int rc = run_loop(s, comm);
+  if (have_prev) (void)hipSetDevice(prev);  // the caller's current device, as it was
+  return rc;
 }
 
 extern "C" int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t *v, const uint32_t *w,
@@ -397,6 +474,7 @@ extern "C" int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const ui
       err = std::string("ncclCommInitAll: ") + ncclGetErrorString(nr);
     }
   }
+  int group_failed = 0;  // set by the first failing rank: the others' waits end (solver_sync)
   for (int i = 0; i < num_gpus; ++i) {
     d[i].dev = devs[i];
     comms[i].nranks = num_gpus;
@@ -404,7 +482,12 @@ extern "C" int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const ui
     comms[i].dev = devs[i];
     comms[i].nccl = rc == GHS_OK ? nc[i] : nullptr;
     comms[i].own_nccl = false;
+    comms[i].group_cancel = &group_failed;
     d[i].comm = &comms[i];
+    if (rc == GHS_OK && (hipSetDevice(devs[i]) != hipSuccess || hipMalloc((void **)&comms[i].agree, 4) != hipSuccess)) {
+      rc = GHS_E_NOMEM;
+      err = "hipMalloc of the setup-agreement word failed";
+    }
   }
   if (rc == GHS_OK) {
     // one thread per device: stream, H2D copies of the replicated list, then the solve (the
@@ -413,27 +496,27 @@ extern "C" int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const ui
     for (int i = 0; i < num_gpus; ++i)
       th.emplace_back([&, i] {
         Rank &x = d[i];
+        // setup errors are carried into rank_solve, whose agreement fails every rank together
+        int setup = GHS_OK;
+        const size_t cb = al256(m * 4);
+        char *c = nullptr;
         if (hipSetDevice(x.dev) != hipSuccess || hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking) != hipSuccess) {
           ghs::set_error("device setup failed");
-          rank_fail(x, GHS_E_HIP);
-          return;
-        }
-        const size_t cb = al256(m * 4);
-        if (hipMalloc(&x.canon, 3 * cb + 256) != hipSuccess || hipMalloc((void **)&x.in_mst, m ? m : 1) != hipSuccess) {
+          setup = GHS_E_HIP;
+        } else if (hipMalloc(&x.canon, 3 * cb + 256) != hipSuccess || hipMalloc((void **)&x.in_mst, m ? m : 1) != hipSuccess) {
           ghs::set_error("hipMalloc of the device's canonical copy failed");
-          rank_fail(x, GHS_E_HIP);
-          return;
+          setup = GHS_E_NOMEM;
+        } else {
+          c = (char *)x.canon;
+          if (m && (hipMemcpyAsync(c, u, m * 4, hipMemcpyHostToDevice, x.stream) != hipSuccess ||
+                    hipMemcpyAsync(c + cb, v, m * 4, hipMemcpyHostToDevice, x.stream) != hipSuccess ||
+                    hipMemcpyAsync(c + 2 * cb, w, m * 4, hipMemcpyHostToDevice, x.stream) != hipSuccess)) {
+            ghs::set_error("H2D copy of the canonical list failed");
+            setup = GHS_E_HIP;
+          }
         }
-        char *c = (char *)x.canon;
-        if (m && (hipMemcpyAsync(c, u, m * 4, hipMemcpyHostToDevice, x.stream) != hipSuccess ||
-                  hipMemcpyAsync(c + cb, v, m * 4, hipMemcpyHostToDevice, x.stream) != hipSuccess ||
-                  hipMemcpyAsync(c + 2 * cb, w, m * 4, hipMemcpyHostToDevice, x.stream) != hipSuccess)) {
-          ghs::set_error("H2D copy of the canonical list failed");
-          rank_fail(x, GHS_E_HIP);
-          return;
-        }
-        if (rank_solve(x, i, num_gpus, n, m, (const uint32_t *)c, (const uint32_t *)(c + cb),
-                       (const uint32_t *)(c + 2 * cb), x.in_mst, cfg))
+        if (rank_solve(x, i, num_gpus, n, m, (const uint32_t *)c, (const uint32_t *)(c ? c + cb : nullptr),
+                       (const uint32_t *)(c ? c + 2 * cb : nullptr), x.in_mst, cfg, setup))
           return;
         uint64_t lo, hi;
         edge_range(m, i, num_gpus, &lo, &hi);
@@ -453,7 +536,8 @@ extern "C" int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const ui
       ncclCommDestroy(comms[i].nccl);
       comms[i].nccl = nullptr;
     }
-    for (void *p : {(void *)comms[i].dense, (void *)comms[i].hook, (void *)comms[i].gathered})
+    (void)hipSetDevice(devs[i]);
+    for (void *p : {(void *)comms[i].dense, (void *)comms[i].hook, (void *)comms[i].gathered, (void *)comms[i].agree})
       if (p) (void)hipFree(p);
   }
   (void)hipSetDevice(prev);
@@ -480,16 +564,18 @@ extern "C" int ghs_mst_emulated(uint32_t n, uint64_t m, const uint32_t *d_u, con
     d[i].dev = dev;
     d[i].comm = &comms[i];
   }
+  int group_failed = 0;
+  for (auto &c : comms) c.group_cancel = &group_failed;
   std::vector<std::thread> th;
   for (int i = 0; i < num_ranks; ++i)
     th.emplace_back([&, i] {
       Rank &x = d[i];
+      int setup = GHS_OK;
       if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking) != hipSuccess) {
         ghs::set_error("stream creation failed");
-        rank_fail(x, GHS_E_HIP);
-        return;
+        setup = GHS_E_HIP;
       }
-      if (rank_solve(x, i, num_ranks, n, m, d_u, d_v, d_w, d_in_mst, cfg)) return;
+      if (rank_solve(x, i, num_ranks, n, m, d_u, d_v, d_w, d_in_mst, cfg, setup)) return;
       if (hipStreamSynchronize(x.stream) != hipSuccess) {
         ghs::set_error("stream sync failed");
         rank_fail(x, GHS_E_HIP);

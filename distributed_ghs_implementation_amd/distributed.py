@@ -26,7 +26,7 @@ orchestration can be exercised on CPU with the gloo backend in tests (tests inje
 stepper from oracle/); the product stepper is `HipStepper` (libghs_mst.so).
 """
 import ctypes
-import os
+import threading
 
 import torch
 import torch.distributed as dist
@@ -127,6 +127,12 @@ class HipStepper:
         """Start the next solve on the same handle (no new host resources)."""
         _native.check(self.L.ghs_solver_reset(self.h))
 
+    def cancel(self):
+        """Thread-safe: end the waits of a ghs_solver_run in progress on another thread (a peer
+        rank failed); that call then returns GHS_E_STATE."""
+        if self.h:
+            self.L.ghs_solver_cancel(self.h)
+
     def close(self):
         if self.h:
             self.L.ghs_solver_destroy(self.h)
@@ -207,6 +213,36 @@ def torch_allreduce_min(group=None):
     return fn
 
 
+class _FailureWatch:
+    """A daemon thread polling `key` in a torch.distributed store; when any rank sets it, the
+    stepper's solve in progress is cancelled (see DistributedMST._watchdog)."""
+
+    def __init__(self, store, key, stepper, period=0.02):
+        self.store, self.key, self.stepper = store, key, stepper
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, args=(period,), daemon=True)
+        self._t.start()
+
+    def _run(self, period):
+        while not self._stop.wait(period):
+            try:
+                if self.store.check([self.key]):
+                    self.stepper.cancel()
+                    return
+            except Exception:  # noqa: BLE001 (store gone: the process group is shutting down)
+                return
+
+    def report(self):
+        try:
+            self.store.set(self.key, b"1")
+        except Exception:  # noqa: BLE001
+            pass
+
+    def stop(self):
+        self._stop.set()
+        self._t.join()
+
+
 def _device_u8_view(ptr, nbytes, device, owner):
     """A torch uint8 tensor over nbytes of device memory inside `owner`'s storage (the solver's
     workspace) — no copy, so the all-reduce combines the engine's own flag array."""
@@ -234,12 +270,28 @@ class DistributedMST:
         if config is None:
             config = _native.make_config(num_ranks=self.world)
         config.num_ranks = self.world
-        self.engine = DeviceMST(edges, lo, hi, config)
         self.edges = edges
         self.stepper = None
+        self._solves = 0
+        # setup agreement before the first collective: a rank whose workspace allocation fails
+        # raises on EVERY rank instead of leaving the others blocked in the next collective
+        err = None
+        try:
+            if config.fault_rank == self.rank + 1:  # test hook (ghs_config_t.fault_rank)
+                raise _native.GHSError(_native.GHS_E_NOMEM, "injected setup failure (fault_rank)")
+            self.engine = DeviceMST(edges, lo, hi, config)
+        except Exception as ex:  # noqa: BLE001 (re-raised below, after the agreement)
+            err = ex
+        if self.world > 1 and dist.is_initialized():
+            dev = edges.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+            flag = torch.tensor([1 if err is not None else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+            if err is None and int(flag.item()):
+                raise _native.GHSError(_native.GHS_E_STATE, "another rank failed during setup")
+        if err is not None:
+            raise err
         if native is None:
-            native = (self.world > 1 and dist.is_initialized() and dist.get_backend(group) == "nccl"
-                      and os.environ.get("GHS_DIST_NATIVE", "1") != "0")
+            native = self.world > 1 and dist.is_initialized() and dist.get_backend(group) == "nccl"
         self.native = bool(native)
         self.comm = self._make_comm() if self.native and self.world > 1 else None
 
@@ -250,7 +302,9 @@ class DistributedMST:
             uid.copy_(torch.frombuffer(bytearray(_native.comm_unique_id()), dtype=torch.uint8))
         src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
         dist.broadcast(uid, src=src, group=self.group)
-        return _native.Comm(self.world, self.rank, bytes(uid.cpu().numpy().tobytes()))
+        # the communicator binds to the device current at ghs_comm_init: the edges' device
+        with torch.cuda.device(self.edges.device):
+            return _native.Comm(self.world, self.rank, bytes(uid.cpu().numpy().tobytes()))
 
     def run(self):
         """The level/round loop over the owned edge range. Returns (Result, stats). The solver
@@ -259,6 +313,8 @@ class DistributedMST:
             self.stepper = HipStepper(self.engine)
         else:
             self.stepper.reset()
+        self._solves += 1
+        watch = self._watchdog() if self.native and self.world > 1 else None
         try:
             if self.native:
                 self.stepper.run_native(self.comm)
@@ -266,8 +322,26 @@ class DistributedMST:
                 run_rounds(self.stepper, torch_allreduce_min(self.group))
             return self.stepper.finish()
         except BaseException:
+            if watch is not None:
+                watch.report()  # the peers' waits end (their ghs_solver_run returns an error)
+                watch.stop()    # before the handle goes away under the watchdog thread
+                watch = None
             self.close()
             raise
+        finally:
+            if watch is not None:
+                watch.stop()
+
+    def _watchdog(self):
+        """Failure agreement during a native solve: a rank that fails sets a key in the process
+        group's store; every rank's watchdog thread polls it and cancels its own solver, whose
+        waits then end (ghs_solver_cancel) instead of blocking behind the failed rank's missing
+        collective. None when the store is not reachable."""
+        try:
+            store = dist.distributed_c10d._get_default_store()
+        except Exception:  # noqa: BLE001
+            return None
+        return _FailureWatch(store, f"ghs_failed/{self._solves}", self.stepper)
 
     def close(self):
         if self.stepper is not None:
@@ -297,6 +371,32 @@ class DistributedMST:
         for (plo, phi), part in zip(ranges, parts):
             out[plo:phi] = part[: phi - plo].to(flags.device)
         return out
+
+    def collect_mst(self, dst=0):
+        """The reference's `collect_results` (ghs_implementation_mpi.py:760-779: every rank sends
+        its BRANCH edges to rank 0): each rank compacts its own range's MSF flags to global edge
+        ids and `dst` gathers them (collective). Returns the sorted int64 eids of the whole MSF on
+        `dst` (the ranks' ranges ascend, so the concatenation is sorted), None elsewhere."""
+        m = self.edges.m
+        lo, hi = edge_range(m, self.rank, self.world)
+        mine = torch.nonzero(self.engine.in_mst[lo:hi]).flatten().to(torch.int64) + lo
+        if not (dist.is_initialized() and dist.get_world_size(self.group) > 1):
+            return mine
+        world = dist.get_world_size(self.group)
+        dev = mine.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        cnt = torch.tensor([mine.numel()], dtype=torch.int64, device=dev)
+        counts = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(counts, cnt, group=self.group)
+        counts = [int(c.item()) for c in counts]
+        width = max(max(counts), 1)
+        pad = torch.full((width,), -1, dtype=torch.int64, device=dev)
+        pad[: mine.numel()] = mine.to(dev)
+        gdst = dist.get_global_rank(self.group, dst) if self.group is not None else dst
+        parts = [torch.empty_like(pad) for _ in range(world)] if self.rank == dst else None
+        dist.gather(pad, parts, dst=gdst, group=self.group)
+        if self.rank != dst:
+            return None
+        return torch.cat([p[:c] for p, c in zip(parts, counts)]).to(mine.device)
 
     def in_mst_host(self):
         """The MSF flags as a host bool array (collective, see gather_in_mst)."""

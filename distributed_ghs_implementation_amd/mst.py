@@ -54,10 +54,10 @@ class MSTResult:
         return mst_result_dict(self.triples(), algorithm)
 
 
-def minimum_spanning_forest(graph, num_gpus=1, devices=None):
+def minimum_spanning_forest(graph, num_gpus=1, devices=None, config=None):
     """Run the HIP engine on a CanonicalGraph (host arrays) -> MSTResult. num_gpus > 1 (or an
     explicit device list): one process drives that many GPUs of this node as an RCCL clique
-    (ghs_mst_multi: the MPI path's multi-rank solve as one call)."""
+    (ghs_mst_multi: the MPI path's multi-rank solve as one call; `config`: its ghs_config_t)."""
     if not isinstance(graph, CanonicalGraph):
         raise TypeError("expected a CanonicalGraph (use graph.canonicalize)")
     L = _native.load()
@@ -70,8 +70,9 @@ def minimum_spanning_forest(graph, num_gpus=1, devices=None):
     if num_gpus > 1 or devices is not None:
         devs = list(range(num_gpus)) if devices is None else [int(d) for d in devices]
         arr = (ctypes.c_int * len(devs))(*devs)
+        cfg = ctypes.byref(config) if config is not None else None
         _native.check(L.ghs_mst_multi(graph.n, m, u.ctypes.data, v.ctypes.data, w.ctypes.data, len(devs), arr,
-                                      None, in_mst.ctypes.data, ctypes.byref(res), stats))
+                                      cfg, in_mst.ctypes.data, ctypes.byref(res), stats))
     else:
         _native.check(L.ghs_mst_host(graph.n, m, u.ctypes.data, v.ctypes.data, w.ctypes.data, in_mst.ctypes.data,
                                      ctypes.byref(res), stats))

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GHS_MST_ABI_VERSION 4
+#define GHS_MST_ABI_VERSION 5
 
 #define GHS_OK 0
 #define GHS_NEED_EXCHANGE 1   /* ghs_solver_minedge on a multi-rank solver opened a level: OR-combine
@@ -68,8 +68,7 @@ typedef struct ghs_result {
   uint32_t rounds;            /* Boruvka rounds executed (all levels) */
   uint32_t num_stats;         /* entries filled in the stats array (<= GHS_MAX_ROUND_STATS) */
   uint32_t levels;            /* weight levels planned */
-  uint32_t pass_flags;        /* bit 0: the heavy edges went through the bucketed passes
-                                 (k_select_hv writes them grouped by b, k_filter_hv reads them) */
+  uint32_t pass_flags;        /* reserved (0); ABI 4's bucketed heavy-edge passes were removed */
   double ms_total;            /* host wall time of the solve (device-resident input -> flags) */
   /* The two full streams over the canonical list (HIP events on the solve's stream). */
   float ms_select;            /* k_select: validation + level-0 split */
@@ -84,13 +83,28 @@ typedef struct ghs_result {
  * last level the rest; max_levels = 1 runs plain Boruvka over every edge at once. Thresholds
  * are weight quantiles of a fixed sample of the canonical list, so every rank plans the same
  * levels. level1_edges_per_vertex <= 0 (the default) = auto: 0.5 when m >= 4n, else 1.0.
- * Results do not depend on the plan (only speed does). */
+ * Results do not depend on the plan (only speed does).
+ * ABI 5: every path option lives here (the library reads no environment variable that changes the
+ * algorithm or a launch shape); options = 0 and dedup_max = 0 select the default path. */
+#define GHS_OPT_NO_SEED_RUNS 0x1u  /* level 0, round 0: a-side minima through the min-edge kernel
+                                      instead of the single-writer run seeding */
+#define GHS_OPT_NO_DENSE 0x2u      /* several ranks: levels in vertex labels, not dense labels */
+#define GHS_OPT_DEBUG 0x10u        /* per-level sizes on stderr (diagnostic) */
+#define GHS_OPT_TIME_ROUNDS 0x20u  /* HIP events around the compacting min-edge launches
+                                      (ghs_round_stats_t.ms_minedge; idles the GPU ~6 us each) */
+#define GHS_OPT_DETAIL 0x40u       /* HIP events around every stage of every round (diagnostic) */
 typedef struct ghs_config {
   uint32_t max_levels;
   uint32_t num_ranks;         /* ranks sharing the solve (1 = single GPU; >1: identical rounds on
                                  every rank, so empty levels are not skipped) */
   double level1_edges_per_vertex;
   double level_growth;
+  uint32_t options;           /* GHS_OPT_* bits (0 = default path) */
+  uint32_t dedup_max;         /* cross-component parallel-edge filter in the compacting rounds once
+                                 at most this many fragments are active (0 = off, the default) */
+  uint32_t fault_rank;        /* test hook of the multi-rank drivers: 1 + the rank whose setup is
+                                 made to fail (ghs_mst_multi / ghs_mst_emulated); 0 = none */
+  uint32_t reserved;
 } ghs_config_t;
 
 /* ---- library / device ------------------------------------------------------------------- */
@@ -207,6 +221,11 @@ int ghs_solver_finish(ghs_solver_t *h, ghs_result_t *result, ghs_round_stats_t *
 /* start the next solve of the same inputs on the same handle (keeps the workspace layout and the
  * pinned host resources: a multi-GPU caller's per-solve create/destroy becomes one reset) */
 int ghs_solver_reset(ghs_solver_t *h);
+/* thread-safe, callable while another thread is inside ghs_solver_run (ABI 5): a rank whose peer
+ * failed ends its waits — the call in progress returns GHS_E_STATE instead of waiting forever
+ * behind a collective the peer never joins (DistributedMST: a watchdog thread calls it when
+ * another rank reports a failure). The handle is then only good for reset or destroy. */
+int ghs_solver_cancel(ghs_solver_t *h);
 int ghs_solver_destroy(ghs_solver_t *h);
 
 /* ---- the round loop in the library --------------------------------------------------------

@@ -34,8 +34,23 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi():
     L = _native.load()
-    assert L.ghs_abi_version() == _native.ABI_VERSION == 4
+    assert L.ghs_abi_version() == _native.ABI_VERSION == 5
     assert _native.device_count() >= 0
+
+
+def test_config_struct_and_no_environment_knobs():
+    """ghs_config_t (ABI 5) carries every path option; the default config is the default path,
+    and the shipped library names no GHS_* environment variable (A/B launch-shape knobs exist only
+    in `make AB=1` builds)."""
+    L = _native.load()
+    assert ctypes.sizeof(_native.Config) == 40
+    c = _native.make_config()
+    assert (c.options, c.dedup_max, c.fault_rank, c.max_levels, c.num_ranks) == (0, 0, 0, 8, 1)
+    blob = open(_native.LIB_PATH, "rb").read()
+    for knob in (b"GHS_LOOKAHEAD", b"GHS_HV", b"GHS_DEDUP_MAX", b"GHS_SEED_RUNS", b"GHS_DENSE", b"GHS_SEG_G",
+                 b"GHS_MINEDGE_G", b"GHS_DEBUG", b"GHS_DETAIL", b"GHS_TIME_ROUNDS"):
+        assert knob not in blob, knob
+    del L
 
 
 def test_sizes_are_sane():

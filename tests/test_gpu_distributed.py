@@ -36,4 +36,23 @@ def test_ranks_in_separate_processes_match_oracle(world, scale, tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     v = json.loads(out.read_text())
     assert v == {"world": world, "m": v["m"], "flags_match_oracle": True, "totals_match_oracle": True,
-                 "ranks_agree": True}
+                 "ranks_agree": True, "collected_match_oracle": True}
+
+
+def test_setup_failure_fails_every_rank(tmp_path):
+    """One rank's setup fails (ghs_config_t.fault_rank): every rank raises from the constructor's
+    setup agreement — the failing one with its own error, the others GHS_E_STATE — and nothing
+    waits in a collective (the subprocess would time out)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from distributed_ghs_implementation_amd import _native
+    out = tmp_path / "verdict.json"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "gpu_workers", "dist_ranks.py"), str(out), "12", "fault"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    v = json.loads(out.read_text())
+    assert v == {"world": 3, "codes": [_native.GHS_E_STATE, _native.GHS_E_NOMEM, _native.GHS_E_STATE]}

@@ -370,78 +370,29 @@ def test_native_loop_emulated_vs_oracle(world, graph, torch_cuda):
     assert len(stats) == res.num_stats
 
 
-@pytest.mark.parametrize("dedup_max", ["128", "1000000000"])
+@pytest.mark.parametrize("dedup_max", [128, 1000000000])
 @pytest.mark.parametrize("graph,world", [("rmat", 1), ("ties", 1), ("forest", 1), ("grid", 1), ("rmat", 4),
                                          ("ties", 3)])
-def test_parallel_edge_filter_vs_oracle(graph, world, dedup_max, monkeypatch, torch_cuda):
-    """The compacting min-edge's parallel-edge filter (GHS_DEDUP_MAX: per block, survivors between
+def test_parallel_edge_filter_vs_oracle(graph, world, dedup_max, torch_cuda):
+    """The compacting min-edge's parallel-edge filter (ghs_config_t.dedup_max: per block, survivors between
     the same two fragments keep only their minimum key) at <= 128 active fragments and in every
     compacting round: the oracle's MSF, single GPU and through the multi-rank loop."""
+    from distributed_ghs_implementation_amd import _native
     from distributed_ghs_implementation_amd.device import DeviceMST, emulated_mst
-    monkeypatch.setenv("GHS_DEDUP_MAX", dedup_max)
+    cfg = _native.make_config(dedup_max=dedup_max)
     ora = _oracle()
     e = _test_graph(graph)
     g = e.to_host()
     ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
     if world == 1:
-        eng = DeviceMST(e)
+        eng = DeviceMST(e, config=cfg)
         res, _ = eng.run()
         flags = eng.in_mst_host()
     else:
-        res, _, f = emulated_mst(e, world)
+        res, _, f = emulated_mst(e, world, config=cfg)
         flags = f.cpu().numpy().astype(bool)
     assert np.array_equal(flags, ref_in.astype(bool))
     assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
-
-
-@pytest.mark.parametrize("graph,world", [("rmat", 1), ("ties", 1), ("forest", 1), ("grid", 1), ("grid-gradient", 1),
-                                         ("rmat", 4), ("ties", 3), ("forest", 2), ("rmat20", 1), ("rmat20", 3)])
-def test_heavy_buckets_vs_oracle(graph, world, monkeypatch, torch_cuda):
-    """The bucketed heavy-edge passes (k_select_hv writes the heavy edges grouped by bucket of b,
-    k_filter_hv probes b in an LDS slice of the giant bitmap), forced onto small graphs by a small
-    bucket (GHS_HV_SB: ~32 buckets): the oracle's MSF, single GPU and through the multi-rank loop,
-    and the same flags as the unbucketed passes."""
-    from distributed_ghs_implementation_amd.device import DeviceMST, emulated_mst
-    ora = _oracle()
-    e = _test_graph(graph)
-    g = e.to_host()
-    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
-    sb = max(7, int(np.ceil(np.log2(max(g.n, 2) / 32.0))))
-    assert 2 <= -(-g.n // (1 << sb)) <= 64
-
-    def solve():
-        if world == 1:
-            eng = DeviceMST(e)
-            res, _ = eng.run()
-            return res, eng.in_mst_host()
-        res, _, f = emulated_mst(e, world)
-        return res, f.cpu().numpy().astype(bool)
-
-    monkeypatch.setenv("GHS_HV", "1")
-    monkeypatch.setenv("GHS_HV_SB", str(sb))
-    res, flags = solve()
-    assert res.pass_flags & 1, "the bucketed passes did not run"
-    assert np.array_equal(flags, ref_in.astype(bool))
-    assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
-    monkeypatch.setenv("GHS_HV", "0")
-    res0, flags0 = solve()
-    assert not res0.pass_flags & 1
-    assert np.array_equal(flags0, flags) and res0.total_weight == res.total_weight
-
-
-def test_heavy_buckets_noncanonical_rejected(monkeypatch, torch_cuda):
-    """k_select_hv validates the list like k_select: a non-canonical edge fails the solve."""
-    from distributed_ghs_implementation_amd import _native
-    from distributed_ghs_implementation_amd.device import DeviceEdges, DeviceMST, generate_rmat
-    monkeypatch.setenv("GHS_HV", "1")
-    monkeypatch.setenv("GHS_HV_SB", "10")
-    e = generate_rmat(15, 16, seed=3, wseed=4)
-    for pos in (0, e.m // 2, e.m - 1):
-        v = e.v.clone()
-        v[pos] = e.u[pos]  # u == v
-        with pytest.raises(_native.GHSError) as ei:
-            DeviceMST(DeviceEdges(e.n, e.u, v, e.w)).run()
-        assert ei.value.code == _native.GHS_E_NONCANON
 
 
 def test_native_loop_emulated_noncanonical_fails_together(torch_cuda):
@@ -456,6 +407,37 @@ def test_native_loop_emulated_noncanonical_fails_together(torch_cuda):
     with pytest.raises(_native.GHSError) as ei:
         emulated_mst(DeviceEdges(e.n, e.u, v, e.w), 4)
     assert ei.value.code == _native.GHS_E_NONCANON
+
+
+@pytest.mark.parametrize("world,fault", [(4, 2), (4, 1), (3, 3), (1, 1)])
+def test_rank_setup_failure_fails_every_rank(world, fault, torch_cuda):
+    """One rank's setup fails (ghs_config_t.fault_rank = 1 + rank: its workspace is refused):
+    ghs_mst_emulated returns an error from every rank (the setup agreement before the first
+    collective) instead of hanging, and the same graph then solves normally."""
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import emulated_mst, generate_rmat
+    ora = _oracle()
+    e = generate_rmat(12, 16, seed=1, wseed=2)
+    cfg = _native.make_config(fault_rank=fault)
+    with pytest.raises(_native.GHSError) as ei:
+        emulated_mst(e, world, config=cfg)
+    assert ei.value.code in (_native.GHS_E_NOMEM, _native.GHS_E_STATE)
+    res, _, flags = emulated_mst(e, world)
+    g = e.to_host()
+    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    assert np.array_equal(flags.cpu().numpy().astype(bool), ref_in.astype(bool))
+
+
+def test_multi_gpu_entry_setup_failure(torch_cuda):
+    """ghs_mst_multi (a 1-rank RCCL clique on the box's device) with its rank's setup failing:
+    the setup agreement's RCCL all-reduce runs and the call returns the error."""
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import generate_rmat
+    from distributed_ghs_implementation_amd.mst import minimum_spanning_forest
+    g = generate_rmat(12, 16, seed=1, wseed=2).to_host()
+    with pytest.raises(_native.GHSError) as ei:
+        minimum_spanning_forest(g, devices=[0], config=_native.make_config(fault_rank=1))
+    assert ei.value.code == _native.GHS_E_NOMEM
 
 
 def test_native_loop_rccl_comm_one_rank(torch_cuda):
@@ -655,19 +637,6 @@ def test_rmat_s24_full_size(torch_cuda):
     eng = DeviceMST(e)
     res, _ = eng.run()
     assert res.levels >= 2  # the default plan exercises the giant filter
-    _full_size_checks(e, eng, res, torch)
-
-
-def test_rmat_s24_full_size_heavy_buckets(monkeypatch, torch_cuda):
-    """The opt-in bucketed heavy-edge passes (GHS_HV=1: 16 buckets of 2^20 vertices, ~3 sort
-    groups per k_filter_hv wave) at BASELINE config 3's full size: the same checks."""
-    torch = torch_cuda
-    from distributed_ghs_implementation_amd.device import DeviceMST, generate_rmat
-    monkeypatch.setenv("GHS_HV", "1")
-    e = generate_rmat(24, 16, seed=1, wseed=2)
-    eng = DeviceMST(e)
-    res, _ = eng.run()
-    assert res.pass_flags & 1 and res.levels >= 2
     _full_size_checks(e, eng, res, torch)
 
 
