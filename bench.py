@@ -105,6 +105,13 @@ def launch_bytes(rec, stats, res, n):
         return 16.0 * live  # a 4 + b 4 + key 8 (roots: no gathers)
     if k == "k_minedge<COMPACT>":
         return 24.0 * live + 16.0 * _next_live(stats, r)  # + lab[a], lab[b]; survivors out
+    # bucketed rounds: a level's first round buckets its edges, later rounds their compacted
+    # survivors; an edge is at least one record (a, b, key: 16 B)
+    bucketed_edges = live if _first_round(stats, r) else _next_live(stats, r)
+    if k == "k_bucket":
+        return 40.0 * bucketed_edges  # pass A a, b (8 B) + pass B edge in (16 B) + record out (16 B)
+    if k == "k_bmin":
+        return 32.0 * bucketed_edges  # two sweeps over the records
     # rounds >= 1 of one rank with >= 1M active fragments launch both CONNECT forms and the
     # device runs one (boruvka.hip k_win / k_hook guards: edge form while the survivors are
     # fewer than 4x the active fragments)
@@ -122,7 +129,7 @@ def launch_bytes(rec, stats, res, n):
     return 0.0
 
 
-STAGE1 = ("k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>")
+STAGE1 = ("k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>", "k_bucket", "k_bmin")
 
 
 def kernel_table(records, stats, res, n):

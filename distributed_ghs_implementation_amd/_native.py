@@ -151,6 +151,8 @@ def profile_read():
 # ghs_config_t.options bits (include/ghs_mst.h GHS_OPT_*)
 OPT_NO_SEED_RUNS = 0x1
 OPT_NO_DENSE = 0x2
+OPT_BUCKETED = 0x4
+OPT_NO_BUCKETED = 0x8
 OPT_DEBUG = 0x10
 OPT_TIME_ROUNDS = 0x20
 OPT_DETAIL = 0x40

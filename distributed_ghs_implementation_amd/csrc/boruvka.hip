@@ -106,13 +106,6 @@ __device__ __forceinline__ void flush_min(uint64_t *__restrict__ best, uint32_t 
 // plain read of that slot misses too.
 // k_filter: issue the random b-probe only for edges whose a-end is in the giant (1), or for
 // every heavy edge beside the a-probes (0)
-// k_jump_ident: a lane's 4 pointer walks advance together, from 4 consecutive vertices (1), from
-// vertices 64 apart (2) or a whole grid stride apart (3: walks started together are far from each
-// other on a chain, so they do not duplicate each other's path splitting — gradient grid
-// 55.7 (1) -> 38.8 (2) -> 25.8 ms (3)), or one after another (0)
-#ifndef GHS_JUMP_ILP
-#define GHS_JUMP_ILP 3
-#endif
 // k_resolve: 4 vertices per lane with their label walks interleaved — consecutive (1) or a grid
 // stride apart (2) — or one per thread (0)
 #ifndef GHS_RESOLVE4
@@ -478,7 +471,7 @@ __device__ __forceinline__ void tile_load(EdgeTile &t, const uint32_t *__restric
 // COMPACT: survivors (inter-fragment edges) are written relabelled to this block's output
 // region (padded to a multiple of 4 with dead entries).
 // ------------------------------------------------------------------------------------------
-template <bool IDENT, bool COMPACT, bool DEDUP = false>
+template <bool IDENT, bool COMPACT, bool DEDUP = false, bool CAND = true>
 GHS_STREAM_KERNEL_6 void k_minedge(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
                                  const uint64_t *__restrict__ key, SegView in, const uint32_t *__restrict__ lab,
                                  uint64_t *__restrict__ best, uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
@@ -488,8 +481,8 @@ GHS_STREAM_KERNEL_6 void k_minedge(const uint32_t *__restrict__ src, const uint3
                                  const unsigned long long *__restrict__ dedup_nact = nullptr, uint32_t dedup_max = 0) {
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
   __shared__ uint32_t s_seg[2];
-  __shared__ uint32_t s_hl[HOT_SLOTS];
-  __shared__ unsigned long long s_hk[HOT_SLOTS];
+  __shared__ uint32_t s_hl[CAND ? HOT_SLOTS : 1];
+  __shared__ unsigned long long s_hk[CAND ? HOT_SLOTS : 1];
   __shared__ WaveStage s_stage[COMPACT ? BLOCK / WAVE : 1];
   __shared__ unsigned long long s_dp[DEDUP ? DEDUP_SLOTS : 1];  // fragment pair lo << 32 | hi
   __shared__ unsigned long long s_dk[DEDUP ? DEDUP_SLOTS : 1];  // its minimum key in this block
@@ -509,7 +502,7 @@ GHS_STREAM_KERNEL_6 void k_minedge(const uint32_t *__restrict__ src, const uint3
   // complete) — its blocks write empty regions instead of streaming every remaining edge
   const bool noop = COMPACT && guard_nact && *guard_nact <= 1;
   const uint64_t T = noop ? 0 : in.prefix[in.nseg];
-  hot_init(s_hl, s_hk);
+  if (CAND) hot_init(s_hl, s_hk);
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;  // multiple of 4
   const uint64_t vb = Q * blockIdx.x;
   const uint64_t ve = (vb + Q < T) ? vb + Q : T;
@@ -560,10 +553,12 @@ GHS_STREAM_KERNEL_6 void k_minedge(const uint32_t *__restrict__ src, const uint3
 #pragma unroll
     for (int j = 0; j < 4; ++j) smask |= (V[j] != KEY_NONE) ? (1u << j) : 0u;
     // b-side: one candidate per live edge
+    if (CAND) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (smask & (1u << j)) hot_min(s_hl, s_hk, best, D[j], V[j]);
-    if (aside) {
+      for (int j = 0; j < 4; ++j)
+        if (smask & (1u << j)) hot_min(s_hl, s_hk, best, D[j], V[j]);
+    }
+    if (CAND && aside) {
     // a-side. Deferred run of the previous iteration (wave-uniform carry): a run that reaches
     // the wave's end is not flushed but carried, and merged into the next run of the same label
     // (min is associative, contiguity is not needed).
@@ -649,9 +644,11 @@ GHS_STREAM_KERNEL_6 void k_minedge(const uint32_t *__restrict__ src, const uint3
     }
     cur = nxt;
   }
-  if (lane == 0 && carry_l != LABEL_NONE) hot_min(s_hl, s_hk, best, carry_l, carry_v);
-  __syncthreads();
-  hot_flush(s_hl, s_hk, best);
+  if (CAND) {
+    if (lane == 0 && carry_l != LABEL_NONE) hot_min(s_hl, s_hk, best, carry_l, carry_v);
+    __syncthreads();
+    hot_flush(s_hl, s_hk, best);
+  }
   if (DEDUP && dd) {  // the block's pair minima join its survivors (4 slots per lane per pass)
     for (int base = 0; base < DEDUP_SLOTS; base += BLOCK * 4) {
       uint32_t L[4], D[4], dmask = 0;
@@ -1099,11 +1096,49 @@ __global__ void k_unpack_hook(const uint32_t *__restrict__ act, const unsigned l
 // outgoing edge (their best slot is reset); keep byte -> flags[i] for k_select_lb. A root with
 // no outgoing edge is finished for the level (the reference: "best_weight == inf at the core =>
 // terminate", ghs_implementation.py:316-320).
+// A bucketed round's hooks (k_bmin) leave every mutual pair as a 2-cycle c <-> p over their
+// shared edge (the reference's equal-level merge over a core edge, ghs_implementation.py:186-196):
+// a walk that meets par[par[x]] == x ends at min(x, par[x]), the smaller label keeps the root, and
+// that member writes par[c] = c. Such pairs exist only at the tree tops and their two pointers are
+// never rewritten by path splitting (a walk at either member detects the pair first), so every
+// concurrent walk sees the same root. acc != nullptr (bucketed rounds): the jump also counts the
+// round's hooks — every fragment that ends below another root adds its best key's weight (each MSF
+// edge once: a mutual pair's smaller member adds nothing).
 // ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void add_totals(unsigned long long wsum, unsigned long long cnt,
+                                           unsigned long long *__restrict__ acc) {
+  __shared__ unsigned long long s_w[BLOCK / WAVE], s_c[BLOCK / WAVE];
+#pragma unroll
+  for (int d = WAVE / 2; d > 0; d >>= 1) {
+    wsum += __shfl_xor(wsum, d);
+    cnt += __shfl_xor(cnt, d);
+  }
+  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+  if (lane == 0) {
+    s_w[wid] = wsum;
+    s_c[wid] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long tw = 0, tc = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / WAVE; ++w) {
+      tw += s_w[w];
+      tc += s_c[w];
+    }
+    if (tc) {
+      atomicAdd(acc + 0, tw);
+      atomicAdd(acc + 1, tc);
+    }
+  }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
                                                 uint32_t *par, uint32_t *__restrict__ lab, uint64_t *__restrict__ best,
-                                                uint8_t *__restrict__ flags, unsigned long long *__restrict__ err) {
+                                                uint8_t *__restrict__ flags, unsigned long long *__restrict__ err,
+                                                unsigned long long *__restrict__ acc) {
   const uint64_t nact = *d_nact;
+  unsigned long long wsum = 0, cnt = 0;
   for (uint64_t i = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; i < nact; i += (uint64_t)gridDim.x * BLOCK) {
     const uint32_t c = act ? act[i] : (uint32_t)i;
     if (!act && lab[c] != c) {  // identity list: not a root when the level opened, never a label
@@ -1112,10 +1147,14 @@ __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act
     }
     uint32_t x = c;
     uint32_t px = par[x];
-    const bool root = px == c;
+    bool root = px == c;
     uint32_t steps = 0;
     while (px != x) {
       const uint32_t ppx = par[px];
+      if (ppx == x) {  // x <-> px: a mutual pair at the top of the tree
+        x = x < px ? x : px;
+        break;
+      }
       if (ppx != px) par[x] = ppx;
       x = px;
       px = ppx;
@@ -1124,46 +1163,43 @@ __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act
         break;
       }
     }
-    if (x != c) lab[c] = x;  // a root's label is already itself (k_resolve, then only hooks move it)
+    if (x == c && !root) {  // the smaller member of a mutual pair: it keeps the root
+      par[c] = c;
+      root = true;
+    }
+    if (x != c) {
+      lab[c] = x;  // a root's label is already itself (k_resolve, then only hooks move it)
+      if (acc) {
+        wsum += best[c] >> 32;
+        cnt += 1;
+      }
+    }
     const bool keep = root && best[c] != KEY_NONE;
     if (keep) best[c] = KEY_NONE;
     flags[i] = keep ? 1 : 0;
   }
+  if (acc) add_totals(wsum, cnt, acc);
 }
 
 // Stage 3 over the identity list (a single-rank level's first round): every vertex, 4 per thread
-// per step (a grid stride apart by default, GHS_JUMP_ILP; 16-byte loads of lab, par and best
-// when consecutive) with their walks advanced together. A vertex that was not a root when the level opened (lab[c] != c) is never a label
-// and is skipped; a root that did not hook only tests its best slot; a root that hooked walks.
+// per step, the 4 a grid stride apart (coalesced 4-B loads of lab, par and best per wave), their
+// walks advanced together: each step issues the par loads of every unfinished walk before any is
+// used, so a lane keeps 4 dependent chains in flight, and walks started together are far apart on
+// a chain (they do not duplicate each other's path splitting; gradient grid 55.7 -> 25.8 ms over
+// consecutive vertices). A vertex that was not a root when the level opened (lab[c] != c) is never
+// a label and is skipped; a root that did not hook only tests its best slot; a root that hooked
+// walks. Mutual pairs and hook counting as in k_jump.
 __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par, uint32_t *__restrict__ lab,
                                                       uint64_t *__restrict__ best, uint8_t *__restrict__ flags,
-                                                      unsigned long long *__restrict__ err) {
-  const uint64_t n4 = (uint64_t)n & ~3ull;
-  // every lane of a wave iterates while the wave's first vertex is < n (the strided variant's
-  // lanes own vertices below their own i0)
+                                                      unsigned long long *__restrict__ err,
+                                                      unsigned long long *__restrict__ acc) {
   const uint64_t tg = blockIdx.x * (uint64_t)BLOCK + threadIdx.x, S = (uint64_t)gridDim.x * BLOCK;
-  (void)tg;
-  (void)S;
-#if GHS_JUMP_ILP == 3
+  unsigned long long wsum = 0, cnt = 0;
   for (uint64_t i0 = tg * 4; i0 - tg * 4 < n; i0 += S * 4) {  // every thread while the chunk starts below n
-#else
-  for (uint64_t i0 = tg * 4; (i0 & ~255ull) < n; i0 += S * 4) {
-#endif
+    const uint64_t cb = i0 - tg * 4;                          // the grid's chunk of 4S vertices
+#define JV(k) (cb + tg + S * (uint64_t)(k))
     uint32_t lc[4], pc[4];
     uint64_t bc[4];
-#if GHS_JUMP_ILP == 2
-    const uint32_t ln = threadIdx.x & (WAVE - 1);
-    const uint64_t wb = i0 - ln * 4;  // the wave's 256 vertices
-#define JV(k) (wb + ln + 64 * (uint64_t)(k))
-#elif GHS_JUMP_ILP == 3
-    const uint64_t cb = i0 - tg * 4;  // the grid's chunk of 4S vertices
-#define JV(k) (cb + tg + S * (uint64_t)(k))
-#else
-#define JV(k) (i0 + (uint64_t)(k))
-#endif
-#if GHS_JUMP_ILP >= 2
-    // strided: the lane's 4 vertices lie 64 (2) or S (3) apart (coalesced wave loads per
-    // array), so the walks a lane advances together start from vertices that are not neighbours
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint64_t vv = JV(k);
@@ -1172,29 +1208,7 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
       pc[k] = in ? par[vv] : 0u;
       bc[k] = in ? best[vv] : KEY_NONE;
     }
-#else
-    if (i0 < n4) {
-      const uint4 l4 = *reinterpret_cast<const uint4 *>(lab + i0);
-      const uint4 p4 = *reinterpret_cast<const uint4 *>(par + i0);
-      const ulonglong2 b01 = *reinterpret_cast<const ulonglong2 *>(best + i0);
-      const ulonglong2 b23 = *reinterpret_cast<const ulonglong2 *>(best + i0 + 2);
-      lc[0] = l4.x; lc[1] = l4.y; lc[2] = l4.z; lc[3] = l4.w;
-      pc[0] = p4.x; pc[1] = p4.y; pc[2] = p4.z; pc[3] = p4.w;
-      bc[0] = b01.x; bc[1] = b01.y; bc[2] = b23.x; bc[3] = b23.y;
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool in = i0 + k < n;
-        lc[k] = in ? lab[i0 + k] : LABEL_NONE;
-        pc[k] = in ? par[i0 + k] : 0u;
-        bc[k] = in ? best[i0 + k] : KEY_NONE;
-      }
-    }
-#endif
     uint32_t kb = 0;
-#if GHS_JUMP_ILP
-    // the lane's (up to) 4 walks advance together: each step issues the par loads of every
-    // unfinished walk before any is used, so a lane keeps 4 dependent chains in flight
     uint32_t x[4], px[4], walking = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1220,6 +1234,11 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         if (!((walking >> k) & 1u)) continue;
+        if (ppx[k] == x[k]) {  // x <-> px: a mutual pair at the top of the tree
+          x[k] = x[k] < px[k] ? x[k] : px[k];
+          walking &= ~(1u << k);
+          continue;
+        }
         if (ppx[k] != px[k]) par[x[k]] = ppx[k];
         x[k] = px[k];
         px[k] = ppx[k];
@@ -1231,46 +1250,27 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
       }
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if ((hooked >> k) & 1u) lab[JV(k)] = x[k];
-#if GHS_JUMP_ILP >= 2
+    for (int k = 0; k < 4; ++k) {
+      if (!((hooked >> k) & 1u)) continue;
+      const uint32_t c = (uint32_t)JV(k);
+      if (x[k] == c) {  // the smaller member of a mutual pair: stays a root, had an edge
+        par[c] = c;
+        best[c] = KEY_NONE;
+        kb |= 1u << (8 * k);
+      } else {
+        lab[c] = x[k];
+        if (acc) {
+          wsum += bc[k] >> 32;
+          cnt += 1;
+        }
+      }
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (JV(k) < n) flags[JV(k)] = (uint8_t)(kb >> (8 * k));
-    continue;
-#endif
-#else
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t c = (uint32_t)(i0 + k);
-      if (lc[k] != c) continue;  // not a root at the level's open (or past n)
-      if (pc[k] == c) {          // still a root: kept iff it had an outgoing edge
-        if (bc[k] != KEY_NONE) {
-          best[c] = KEY_NONE;
-          kb |= 1u << (8 * k);
-        }
-        continue;
-      }
-      uint32_t x = c, px = pc[k];  // hooked: walk to the root (path splitting)
-      uint32_t steps = 0;
-      while (px != x) {
-        const uint32_t ppx = par[px];
-        if (ppx != px) par[x] = ppx;
-        x = px;
-        px = ppx;
-        if (++steps > JUMP_MAX_STEPS) {
-          atomicOr(err, 4ull);
-          break;
-        }
-      }
-      lab[c] = x;
-    }
-#endif
-    if (i0 < n4) *reinterpret_cast<uint32_t *>(flags + i0) = kb;
-    else
-      for (int k = 0; k < 4; ++k)
-        if (i0 + k < n) flags[i0 + k] = (uint8_t)(kb >> (8 * k));
+#undef JV
   }
+  if (acc) add_totals(wsum, cnt, acc);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1443,10 +1443,15 @@ __global__ __launch_bounds__(BLOCK) void k_resolve(uint32_t n, uint32_t *lab, co
 }
 
 
-__global__ void k_sample_weights(uint64_t cnt, const uint32_t *__restrict__ w, uint32_t nsamp, uint32_t *__restrict__ out) {
+// evenly spaced sample of the canonical list: weights (the level plan) and, in out[NSAMPLE_W + i],
+// edge spans v - u (the plan's locality test for the bucketed rounds)
+constexpr uint32_t NSAMPLE_W = 16384;  // edges sampled for the level plan
+__global__ void k_sample_weights(uint64_t cnt, const uint32_t *__restrict__ u, const uint32_t *__restrict__ v,
+                                 const uint32_t *__restrict__ w, uint32_t nsamp, uint32_t *__restrict__ out) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsamp; i += gridDim.x * blockDim.x) {
     const uint64_t e = ((uint64_t)i * cnt) / nsamp;
     out[i] = w[e];
+    out[NSAMPLE_W + i] = v[e] - u[e];  // canonical: u < v (unvalidated here: only a heuristic)
   }
 }
 
@@ -1454,13 +1459,24 @@ __global__ void k_sample_weights(uint64_t cnt, const uint32_t *__restrict__ w, u
 // statistics of the weight sample, the same arithmetic as a host plan would do (target =
 // level1 * n edges, x growth per level, double precision; the q-th smallest by a 4-pass radix
 // select over the sample in LDS; equal thresholds merged). thr[0..count), thr[PLAN_MAX] = count.
-constexpr uint32_t NSAMPLE_W = 16384;  // weights sampled for the level plan
 constexpr uint32_t PLAN_MAX = 33;      // 0, up to 31 interior thresholds, 2^32
-__global__ __launch_bounds__(1024) void k_plan(const uint32_t *__restrict__ sample, uint32_t ns, uint32_t n, uint64_t m,
-                                               uint32_t L, double l1, double growth, uint64_t *__restrict__ thr) {
+// thr[PLAN_LOCAL] = 1: the span sample is lattice-like (<= 1/32 of the sampled edges span more than
+// n/64 ids): the single-rank solve runs bucketed rounds
+constexpr uint32_t PLAN_LOCAL = PLAN_MAX + 1;
+__global__ __launch_bounds__(1024) void k_plan(const uint32_t *__restrict__ sample, uint32_t ns_all, uint32_t ns,
+                                               uint32_t n, uint64_t m, uint32_t L, double l1, double growth,
+                                               uint64_t *__restrict__ thr) {
   __shared__ uint32_t s_w[NSAMPLE_W];
   __shared__ uint32_t s_hist[256];
   __shared__ uint32_t s_sel[2];
+  __shared__ uint32_t s_far;
+  if (threadIdx.x == 0) s_far = 0;
+  __syncthreads();
+  {
+    uint32_t far = 0;
+    for (uint32_t i = threadIdx.x; i < ns_all; i += 1024) far += sample[NSAMPLE_W + i] > n / 64 ? 1u : 0u;
+    if (far) atomicAdd(&s_far, far);
+  }
   for (uint32_t i = threadIdx.x; i < ns; i += 1024) s_w[i] = sample[i];
   __syncthreads();
   uint32_t cnt = 1;
@@ -1519,6 +1535,7 @@ __global__ __launch_bounds__(1024) void k_plan(const uint32_t *__restrict__ samp
     thr[0] = 0;
     thr[cnt++] = 1ull << 32;
     thr[PLAN_MAX] = cnt;
+    thr[PLAN_LOCAL] = (ns_all > 0 && (uint64_t)s_far * 32 <= ns_all) ? 1 : 0;
   }
 }
 
@@ -1939,6 +1956,261 @@ GHS_STREAM_KERNEL_6 void k_level_pass(const uint32_t *__restrict__ ru, const uin
 }
 
 // ------------------------------------------------------------------------------------------
+// Bucketed rounds (lattice-like graphs: the plan's sample of edge spans says nearly every edge
+// joins vertices close in id). A round's per-fragment minima are taken in LDS instead of through
+// global 64-bit atomics, which execute at the memory side (~27 G/s on MI355X, the lattice's
+// bound): the live edges are grouped by target bucket (2^bs consecutive labels) and one workgroup
+// per bucket keeps that bucket's minima in LDS (ds_min_u64), then finds every target's winning
+// edge in a second sweep and hooks it — par[t] = other end, best[t] = key, in_mst[eid] = 1 —
+// single writer per target, no global atomics and no separate CONNECT pass (the reference's
+// TEST/ACCEPT/REPORT convergecast and CHANGEROOT/CONNECT, ghs_implementation.py:155-353, as two
+// passes over a bucket). Mutual pairs stay 2-cycles for the jump (k_jump / k_jump_ident).
+//  k_bucket  block g streams its share of the live edges twice: pass A counts records per bucket
+//            (an edge is a record of bucket(a), and of bucket(b) when that differs), one LDS
+//            scan turns the counts into offsets in the block's record region, written bucket-major
+//            (O[t][g]: a bucket's offsets are contiguous), pass B writes the records (a, b, key)
+//            at LDS cursors. On a lattice a block's edges touch a handful of buckets, so the
+//            records leave in long runs.
+//  k_bmin    one workgroup per bucket: its runs from every region (offsets and their scan in
+//            LDS), min per target in LDS, winners.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t BK_G = 512;        // k_bucket blocks = record regions
+constexpr uint32_t BK_T = 512;        // k_bucket threads
+constexpr uint32_t BK_MAX_B = 16384;  // buckets: k_bucket's LDS counters (64 KiB)
+constexpr uint32_t BM_T = 1024;       // k_bmin threads
+
+// a block's share of the T live edges (a multiple of 4: whole 4-entry tiles); region g of the
+// records starts at 2 * quota * g (an edge gives at most two records)
+__device__ __forceinline__ uint64_t bk_quota(uint64_t T) { return ((T + BK_G - 1) / BK_G + 3) & ~3ull; }
+
+// exclusive scan over the NT threads of a block (NT / 64 waves); *total = the block's sum
+template <uint32_t NT>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t mine, uint32_t *s_wsum, uint32_t *total) {
+  const uint32_t lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+  uint32_t incl = mine;
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const uint32_t o = __shfl_up(incl, d);
+    if ((int)lane >= d) incl += o;
+  }
+  if (lane == WAVE - 1) s_wsum[wid] = incl;
+  __syncthreads();
+  uint32_t before = incl - mine, t = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < NT / WAVE; ++w) {
+    if (w < wid) before += s_wsum[w];
+    t += s_wsum[w];
+  }
+  *total = t;
+  __syncthreads();
+  return before;
+}
+
+// Wave-aggregated LDS bump: every active lane (act) adds one to counter s_h[bkt]; lanes with equal
+// buckets are served by one atomic of their leader, and each lane gets its own slot (the old
+// counter value + its rank among the lanes of its bucket, in lane order: consecutive lanes of a
+// run of equal buckets get consecutive slots, so their record stores coalesce). Lattice edges put
+// one or two buckets in a wave instruction; after BK_AGG_ROUNDS distinct buckets the remaining
+// lanes take one atomic each (random graphs, forced mode). Every lane of the wave must call it.
+constexpr int BK_AGG_ROUNDS = 4;
+template <bool RET>
+__device__ __forceinline__ uint32_t lds_bump(uint32_t *s_h, uint32_t bkt, bool act) {
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint64_t pending = __ballot(act);
+  uint32_t slot = 0;
+  for (int it = 0; it < BK_AGG_ROUNDS && pending; ++it) {
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)pending) - 1;
+    const uint32_t lb = __shfl(bkt, leader);
+    const uint64_t same = __ballot(act && bkt == lb) & pending;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&s_h[lb], (uint32_t)__popcll(same));
+    if (RET) {
+      base = __shfl(base, leader);
+      if ((same >> lane) & 1ull) slot = base + (uint32_t)__popcll(same & below);
+    }
+    pending &= ~same;
+  }
+  if ((pending >> lane) & 1ull) {
+    const uint32_t b = atomicAdd(&s_h[bkt], 1u);
+    if (RET) slot = b;
+  }
+  return slot;
+}
+
+__global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
+                                                 const uint64_t *__restrict__ key, SegView in, uint32_t bs,
+                                                 uint32_t nb, uint32_t *__restrict__ ra, uint32_t *__restrict__ rb,
+                                                 uint64_t *__restrict__ rk, uint32_t *__restrict__ O,
+                                                 const unsigned long long *__restrict__ guard_nact) {
+  __shared__ uint32_t s_h[BK_MAX_B + 1];
+  __shared__ uint32_t s_seg[2];
+  __shared__ uint32_t s_wsum[BK_T / WAVE];
+  // a lookahead round past the level's end (<= 1 active fragment) writes empty regions
+  const bool noop = guard_nact && *guard_nact <= 1;
+  const uint64_t T = noop ? 0 : in.prefix[in.nseg];
+  const uint64_t Q = bk_quota(T);
+  const uint64_t vb = Q * blockIdx.x;
+  const uint64_t ve = (vb + Q < T) ? vb + Q : T;
+  for (uint32_t i = threadIdx.x; i <= nb; i += BK_T) s_h[i] = 0;
+  if (threadIdx.x == 0) {
+    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
+    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
+  }
+  __syncthreads();
+  const uint32_t slo = s_seg[0], shi = s_seg[1];
+  // pass A: records per bucket (the a and b ends only); every lane of a wave iterates while the
+  // wave's first tile is in range (the bumps are wave-collective)
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  for (uint64_t v = vb + (uint64_t)threadIdx.x * 4; v - lane * 4 < ve; v += (uint64_t)BK_T * 4) {
+    const uint64_t i0 = tile_phys(in, slo, shi, v, ve);
+    const uint4 a4 = *reinterpret_cast<const uint4 *>(src + i0), b4 = *reinterpret_cast<const uint4 *>(dst + i0);
+    const uint32_t A[4] = {a4.x, a4.y, a4.z, a4.w}, B[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool live = (v < ve) & (A[j] != LABEL_NONE);  // past the range / region padding
+      const uint32_t ba = A[j] >> bs, bb = B[j] >> bs;
+      lds_bump<false>(s_h, ba, live);
+      lds_bump<false>(s_h, bb, live && bb != ba);
+    }
+  }
+  __syncthreads();
+  // counts -> offsets in place (each thread a run of consecutive buckets), s_h[nb] = total
+  const uint32_t per = (nb + BK_T - 1) / BK_T, c0 = threadIdx.x * per;
+  uint32_t sum = 0;
+  for (uint32_t i = 0; i < per && c0 + i < nb; ++i) sum += s_h[c0 + i];
+  uint32_t tot;
+  uint32_t run = block_excl_scan<BK_T>(sum, s_wsum, &tot);
+  for (uint32_t i = 0; i < per && c0 + i < nb; ++i) {
+    const uint32_t c = s_h[c0 + i];
+    s_h[c0 + i] = run;
+    run += c;
+  }
+  if (threadIdx.x == 0) s_h[nb] = tot;
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t <= nb; t += BK_T) O[(uint64_t)t * BK_G + blockIdx.x] = s_h[t];
+  __syncthreads();  // the cursors below advance s_h
+  // pass B: the records at the cursors of their buckets
+  const uint64_t base = 2 * vb;
+  for (uint64_t v = vb + (uint64_t)threadIdx.x * 4; v - lane * 4 < ve; v += (uint64_t)BK_T * 4) {
+    const uint64_t i0 = tile_phys(in, slo, shi, v, ve);
+    const uint4 a4 = *reinterpret_cast<const uint4 *>(src + i0), b4 = *reinterpret_cast<const uint4 *>(dst + i0);
+    const ulonglong2 k01 = *reinterpret_cast<const ulonglong2 *>(key + i0);
+    const ulonglong2 k23 = *reinterpret_cast<const ulonglong2 *>(key + i0 + 2);
+    const uint32_t A[4] = {a4.x, a4.y, a4.z, a4.w}, B[4] = {b4.x, b4.y, b4.z, b4.w};
+    const uint64_t K[4] = {k01.x, k01.y, k23.x, k23.y};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool live = (v < ve) & (A[j] != LABEL_NONE);
+      const uint32_t ba = A[j] >> bs, bb = B[j] >> bs;
+      const bool two = live && bb != ba;
+      const uint32_t pa = lds_bump<true>(s_h, ba, live);
+      const uint32_t pb = lds_bump<true>(s_h, bb, two);
+      if (live) {
+        ra[base + pa] = A[j];
+        rb[base + pa] = B[j];
+        rk[base + pa] = K[j];
+      }
+      if (two) {
+        ra[base + pb] = A[j];
+        rb[base + pb] = B[j];
+        rk[base + pb] = K[j];
+      }
+    }
+  }
+}
+
+// k_bmin: BM_ILP records in flight per lane; the bucket's non-empty runs listed first (a lattice
+// bucket's records come from one to three block regions), so locating a record searches that
+// short list
+constexpr int BM_ILP = 4;
+template <uint32_t BS>
+__global__ __launch_bounds__(BM_T) void k_bmin(const uint32_t *__restrict__ ra, const uint32_t *__restrict__ rb,
+                                               const uint64_t *__restrict__ rk, const uint32_t *__restrict__ O,
+                                               SegView in, uint32_t *__restrict__ par, uint64_t *__restrict__ best,
+                                               uint8_t *__restrict__ in_mst,
+                                               const unsigned long long *__restrict__ guard_nact) {
+  constexpr uint32_t SPAN = 1u << BS;
+  __shared__ unsigned long long s_min[SPAN];
+  __shared__ uint64_t s_pos[BK_G];  // non-empty run i: its first record's position
+  __shared__ uint32_t s_pre[BK_G];  // ... and its first index in the bucket's record order
+  __shared__ uint32_t s_wsum[BM_T / WAVE];
+  const bool noop = guard_nact && *guard_nact <= 1;
+  const uint64_t T = noop ? 0 : in.prefix[in.nseg];
+  const uint64_t R2 = 2 * bk_quota(T);  // record region stride
+  const uint32_t t = blockIdx.x, tb = t << BS;
+  uint32_t cnt = 0, st = 0;
+  if (threadIdx.x < BK_G && !noop) {
+    st = O[(uint64_t)t * BK_G + threadIdx.x];
+    cnt = O[(uint64_t)(t + 1) * BK_G + threadIdx.x] - st;
+  }
+  // records before each run (scan of the counts), then the non-empty runs' slots (scan of their flags)
+  uint32_t R, NZ;
+  const uint32_t before = block_excl_scan<BM_T>(cnt, s_wsum, &R);
+  if (R == 0) return;  // block-uniform: no record of this bucket
+  const uint32_t zi = block_excl_scan<BM_T>(cnt ? 1u : 0u, s_wsum, &NZ);
+  if (cnt) {
+    s_pos[zi] = R2 * threadIdx.x + st;
+    s_pre[zi] = before;
+  }
+  for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) s_min[i] = KEY_NONE;
+  __syncthreads();
+  auto locate = [&](uint32_t r) -> uint64_t {  // the non-empty run with s_pre <= r, the last one
+    uint32_t lo = 0, hi = NZ - 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (s_pre[mid] <= r) lo = mid; else hi = mid - 1;
+    }
+    return s_pos[lo] + (r - s_pre[lo]);
+  };
+  constexpr uint32_t STEP = BM_T * BM_ILP;
+  for (uint32_t r0 = threadIdx.x; r0 < R; r0 += STEP) {
+    uint32_t a[BM_ILP], b[BM_ILP];
+    unsigned long long k[BM_ILP];
+#pragma unroll
+    for (int j = 0; j < BM_ILP; ++j) {
+      const uint32_t r = r0 + j * BM_T;
+      const uint64_t p = r < R ? locate(r) : 0;
+      a[j] = r < R ? ra[p] : LABEL_NONE;
+      b[j] = r < R ? rb[p] : LABEL_NONE;
+      k[j] = r < R ? rk[p] : KEY_NONE;
+    }
+#pragma unroll
+    for (int j = 0; j < BM_ILP; ++j) {
+      if ((a[j] >> BS) == t) atomicMin(&s_min[a[j] - tb], k[j]);
+      if ((b[j] >> BS) == t) atomicMin(&s_min[b[j] - tb], k[j]);
+    }
+  }
+  __syncthreads();
+  // winners: exactly one record per target holds its minimum (keys are unique)
+  for (uint32_t r0 = threadIdx.x; r0 < R; r0 += STEP) {
+    uint32_t a[BM_ILP], b[BM_ILP];
+    unsigned long long k[BM_ILP];
+#pragma unroll
+    for (int j = 0; j < BM_ILP; ++j) {
+      const uint32_t r = r0 + j * BM_T;
+      const uint64_t p = r < R ? locate(r) : 0;
+      a[j] = r < R ? ra[p] : LABEL_NONE;
+      b[j] = r < R ? rb[p] : LABEL_NONE;
+      k[j] = r < R ? rk[p] : KEY_NONE;
+    }
+#pragma unroll
+    for (int j = 0; j < BM_ILP; ++j) {
+      if ((a[j] >> BS) == t && s_min[a[j] - tb] == k[j]) {
+        par[a[j]] = b[j];
+        best[a[j]] = k[j];
+        in_mst[(uint32_t)k[j]] = 1;
+      }
+      if ((b[j] >> BS) == t && s_min[b[j] - tb] == k[j]) {
+        par[b[j]] = a[j];
+        best[b[j]] = k[j];
+        in_mst[(uint32_t)k[j]] = 1;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Dense levels (several ranks). Once a level's active list A (nact0 fragment roots, identical on
 // every rank) is known, the level runs in a dense label space 0..nact0-1: a root's dense label is
 // its rank among the level's flags (DenseRank: popc over the flag words + word / chunk prefixes),
@@ -2183,12 +2455,15 @@ __global__ void k_iota(uint32_t *__restrict__ a, uint64_t n) {
 }
 
 // dense all-reduce staging: int64 slot = key ^ 2^63 preserves unsigned order under signed MIN
+// `bound` slots (the host's count, >= the device's): a pipelined multi-rank round all-reduces a
+// bound on its active fragments, the slots past the device count hold "no edge" on every rank
 __global__ void k_pack_best(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
-                            const uint64_t *__restrict__ best, int64_t *__restrict__ dense) {
+                            const uint64_t *__restrict__ best, int64_t *__restrict__ dense, uint64_t bound) {
   const uint64_t nact = *d_nact;
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nact; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t c = act ? act[i] : (uint32_t)i;
-    dense[i] = (int64_t)(best[c] ^ 0x8000000000000000ull);
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < bound; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t k = KEY_NONE;
+    if (i < nact) k = best[act ? act[i] : (uint32_t)i];
+    dense[i] = (int64_t)(k ^ 0x8000000000000000ull);
   }
 }
 
@@ -2565,6 +2840,25 @@ struct ghs_solver {
   bool dense_mode = false;      // several ranks and the dense arrays exist (GHS_DENSE=0: off)
   bool level_dense = false;     // the open level runs in dense labels
   uint64_t dense_n = 0;
+  // bucketed rounds (single rank, lattice-like graphs; k_bucket / k_bmin): the record buffers,
+  // the offsets table, the bucket geometry, and the per-solve / per-round decisions
+  uint32_t *rec_a = nullptr, *rec_b = nullptr, *bk_off = nullptr;
+  uint64_t *rec_k = nullptr;
+  uint32_t bk_bs = 13, bk_nb = 0;
+  bool bucketed = false;        // this solve runs bucketed rounds (decided once the plan landed)
+  bool bucket_decided = false;
+  bool round_bucketed = false;  // the round being enqueued is bucketed
+  // pipelined rounds of a multi-rank level (ghs_solver_contract_async, rounds >= 2): issued rounds
+  // whose report is not read yet (oldest first), the latest exact active count and the level round
+  // it starts, the live edges at the start of the oldest unread round
+  struct PipeRound {
+    unsigned long long seq;
+    uint32_t round, level_round;
+  };
+  std::vector<PipeRound> pipe;
+  uint64_t pipe_exact = 0;
+  uint32_t pipe_exact_lr = 0;
+  uint64_t pipe_live = 0;
   // multi-rank failure agreement: another rank's failure ends this solver's waits (the flags are
   // read with __atomic loads; set by ghs_solver_cancel / the driver's shared group flag)
   int cancel_flag = 0;
@@ -2603,7 +2897,7 @@ static uint32_t g_prof_next_id = 0;
 static const char *const KERNEL_NAMES[GHS_K_COUNT] = {
     "k_select", "k_filter", "k_level_pass", "k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>",
     "k_win", "k_hook", "k_jump_ident", "k_jump", "k_select_lb", "k_resolve", "k_giant", "k_scan_counts",
-    "k_plan", "k_init", "k_pack_best", "k_unpack_best", "k_round_report", "k_pack_hook", "k_unpack_hook", "k_dense", "k_flag_bits"};
+    "k_plan", "k_init", "k_pack_best", "k_unpack_best", "k_round_report", "k_pack_hook", "k_unpack_hook", "k_dense", "k_flag_bits", "k_bucket", "k_bmin"};
 
 struct KtScope {
   ghs_solver *s;
@@ -2706,6 +3000,18 @@ static HostRes *pooled_res(int *rc) {
 
 static constexpr uint32_t NSAMPLE_MAX = NSAMPLE_W;
 
+// the bucketed rounds' geometry: buckets of 2^bs labels (bs 13 or 14: a k_bmin slice of 64 or 128
+// KiB of LDS), nb <= BK_MAX_B of them; false when n is too large for it (n > 2^28)
+static bool bucket_geometry(uint32_t n, uint32_t *bs, uint32_t *nb) {
+  if (n == 0) return false;
+  const uint32_t b = n <= (1u << 27) ? 13u : 14u;
+  const uint64_t k = ((uint64_t)n + (1ull << b) - 1) >> b;
+  if (k > BK_MAX_B) return false;
+  *bs = b;
+  *nb = (uint32_t)k;
+  return true;
+}
+
 static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs_solver *s, char *base) {
   size_t off = 0;
   auto carve = [&](size_t bytes) -> char * {
@@ -2735,8 +3041,8 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
   p = carve(N + 1); if (s) s->flags = (uint8_t *)p;  // + the multi-rank error byte flags[n]
   p = carve(((N + 127) / 128) * 16 + 16); if (s) s->bits = (uint64_t *)p;
   p = carve(((N + 1 + 63) / 64) * 8); if (s) s->flag_bits = (uint64_t *)p;
-  p = carve(NSAMPLE_MAX * 4); if (s) s->sample = (uint32_t *)p;
-  p = carve((PLAN_MAX + 1) * 8); if (s) s->d_thr = (uint64_t *)p;
+  p = carve(2 * NSAMPLE_MAX * 4); if (s) s->sample = (uint32_t *)p;  // weights + spans
+  p = carve((PLAN_LOCAL + 1) * 8); if (s) s->d_thr = (uint64_t *)p;
   p = carve(16); if (s) s->giant = (uint32_t *)p;
   p = carve(LB_MAX_TILES * 8); if (s) s->lb_state = (unsigned long long *)p;  // select tile granules
   for (int b = 0; b < 2; ++b) {
@@ -2757,6 +3063,19 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
   }
   if (s) s->cap_arcs = cap;
   p = carve(C_COUNT * sizeof(unsigned long long)); if (s) s->cnt = (unsigned long long *)p;
+  // bucketed rounds (single rank, n <= 2^28): records (an edge gives at most two) + offsets
+  uint32_t bs = 0, nb = 0;
+  if (local_edges == m && bucket_geometry(n, &bs, &nb)) {
+    const uint64_t rc = 2 * cap + 8 * BK_G;
+    p = carve(rc * 4); if (s) s->rec_a = (uint32_t *)p;
+    p = carve(rc * 4); if (s) s->rec_b = (uint32_t *)p;
+    p = carve(rc * 8); if (s) s->rec_k = (uint64_t *)p;
+    p = carve((size_t)(nb + 1) * BK_G * 4); if (s) s->bk_off = (uint32_t *)p;
+    if (s) {
+      s->bk_bs = bs;
+      s->bk_nb = nb;
+    }
+  }
   return off;
 }
 
@@ -2854,15 +3173,17 @@ static uint32_t plan_levels_count(const ghs_solver *s) {
 
 static int plan_levels_enqueue(ghs_solver *s) {
   const uint32_t L = plan_levels_count(s);
-  const uint32_t ns = (L > 1 && s->m > 0) ? (uint32_t)std::min<uint64_t>(NSAMPLE_W, s->m) : 0u;
+  const uint32_t ns_all = (uint32_t)std::min<uint64_t>(NSAMPLE_W, s->m);
+  const uint32_t ns = L > 1 ? ns_all : 0u;
   {
     KT(GHS_K_PLAN, ns);
-    if (ns) k_sample_weights<<<grid_for(ns, 256, 256), 256, 0, s->stream>>>(s->m, s->ew, ns, s->sample);
-    k_plan<<<1, 1024, 0, s->stream>>>(s->sample, ns, s->n, s->m, L, level1_auto(s->cfg, s->n, s->m), s->cfg.level_growth,
-                                      s->d_thr);
+    if (ns_all)
+      k_sample_weights<<<grid_for(ns_all, 256, 256), 256, 0, s->stream>>>(s->m, s->eu, s->ev, s->ew, ns_all, s->sample);
+    k_plan<<<1, 1024, 0, s->stream>>>(s->sample, ns_all, ns, s->n, s->m, L, level1_auto(s->cfg, s->n, s->m),
+                                      s->cfg.level_growth, s->d_thr);
   }
   GHS_HIP_CHECK(hipGetLastError());
-  GHS_HIP_CHECK(hipMemcpyAsync(s->h_thr, s->d_thr, (PLAN_MAX + 1) * 8, hipMemcpyDeviceToHost, s->stream));
+  GHS_HIP_CHECK(hipMemcpyAsync(s->h_thr, s->d_thr, (PLAN_LOCAL + 1) * 8, hipMemcpyDeviceToHost, s->stream));
   GHS_HIP_CHECK(hipEventRecord(s->res->plan_ev, s->stream));
   s->plan_known = false;
   return GHS_OK;
@@ -3173,30 +3494,74 @@ static void flush_scan(ghs_solver *s) {
 }
 
 // ---- one round, enqueued without a host sync (sizes on the device; s->nact is a bound) --------
+// Bucketed rounds (k_bucket + k_bmin, one rank): a level's first round, and later rounds while the
+// host's bound on the active fragments is at least BUCKET_MIN_ACTIVE (below it the min-edge
+// kernel's LDS cache of fragment minima absorbs the candidates, and k_bmin's per-bucket setup
+// would dominate).
+constexpr uint64_t BUCKET_MIN_ACTIVE = 1u << 20;
+
+static void enqueue_bmin(ghs_solver *s, const uint32_t *a, const uint32_t *b, const uint64_t *k, SegView in,
+                         const unsigned long long *guard, uint64_t items) {
+  {
+    KT(GHS_K_BUCKET, items);
+    k_bucket<<<BK_G, BK_T, 0, s->stream>>>(a, b, k, in, s->bk_bs, s->bk_nb, s->rec_a, s->rec_b, s->rec_k, s->bk_off,
+                                         guard);
+  }
+  KT(GHS_K_BMIN, items);
+  if (s->bk_bs == 13)
+    k_bmin<13><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec_a, s->rec_b, s->rec_k, s->bk_off, in, s->par, s->best,
+                                                s->in_mst, guard);
+  else
+    k_bmin<14><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec_a, s->rec_b, s->rec_k, s->bk_off, in, s->par, s->best,
+                                                s->in_mst, guard);
+}
+
 static int enqueue_minedge(ghs_solver *s) {
   const bool timed = s->detail || (s->time_rounds && s->level_round >= 1);
   if (timed) record(s, 0);
   const ArcBuf &I = s->buf[s->cur];
   ArcBuf &O = s->buf[s->cur ^ 1];
   SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
+  // GHS_OPT_BUCKETED (forced) runs every round bucketed: the test suite's coverage of them
+  s->round_bucketed = s->bucketed && (s->level_round == 0 || s->nact >= BUCKET_MIN_ACTIVE ||
+                                      (s->cfg.options & GHS_OPT_BUCKETED));
   if (s->level_round == 0) {
     if (s->cur_arcs || !s->arcs_known) {
       const unsigned g = s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->ident_g) : s->ident_g;
-      // level 0 (labels are the vertices): a-side runs seeded first, mostly by plain stores
-      const bool seed = s->level == 0 && s->seed_runs;
       const uint64_t items = s->arcs_known ? s->cur_arcs : 0;
-      if (seed) {
-        KT(GHS_K_SEED_RUNS, items);
-        k_seed_runs<<<g, BLOCK, 0, s->stream>>>(I.src, I.key, in, s->best);
+      if (s->round_bucketed) {
+        enqueue_bmin(s, I.src, I.dst, I.key, in, nullptr, items);  // the level's edges carry roots
+      } else {
+        // level 0 (labels are the vertices): a-side runs seeded first, mostly by plain stores
+        const bool seed = s->level == 0 && s->seed_runs;
+        if (seed) {
+          KT(GHS_K_SEED_RUNS, items);
+          k_seed_runs<<<g, BLOCK, 0, s->stream>>>(I.src, I.key, in, s->best);
+        }
+        KT(GHS_K_MINEDGE_IDENT, items);
+        k_minedge<true, false><<<g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, nullptr, nullptr,
+                                                           nullptr, nullptr, nullptr, !seed, nullptr);
       }
-      KT(GHS_K_MINEDGE_IDENT, items);
-      k_minedge<true, false><<<g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, nullptr, nullptr,
-                                                         nullptr, nullptr, nullptr, !seed, nullptr);
     }
+  } else if (s->round_bucketed) {
+    // relabel + drop intra-fragment edges (no candidates), scan the survivors' regions, bucket them
+    const unsigned long long *guard = cur_act_count(s);
+    {
+      KT(GHS_K_MINEDGE_COMPACT, 0);
+      k_minedge<false, true, false, false><<<s->cmp_g, BLOCK, 0, s->stream>>>(
+          I.src, I.dst, I.key, in, s->lab, s->best, O.src, O.dst, O.key, O.seg_start, O.seg_count, false, guard);
+    }
+    s->scan_pending = true;
+    s->scan_buf = &O;
+    flush_scan(s);
+    SegView oin{O.seg_start, O.seg_prefix, s->cmp_g};
+    enqueue_bmin(s, O.src, O.dst, O.key, oin, guard, 0);
   } else {
     // fixed grid: every one of the seg_g blocks writes its region's count
     KT(GHS_K_MINEDGE_COMPACT, 0);
-    const unsigned long long *guard = s->cfg.num_ranks <= 1 ? cur_act_count(s) : nullptr;
+    // a round that starts with <= 1 active fragment is a discarded lookahead round (one rank, or the
+    // pipelined rounds of several): it streams nothing
+    const unsigned long long *guard = cur_act_count(s);
     if (s->dedup_max && s->nact <= DEDUP_BOUND_FACTOR * s->dedup_max)  // few fragments left: the parallel-edge filter
       k_minedge<false, true, true><<<s->cmp_g, BLOCK, 0, s->stream>>>(I.src, I.dst, I.key, in, s->lab, s->best, O.src,
                                                                  O.dst, O.key, O.seg_start, O.seg_count, true, guard,
@@ -3232,7 +3597,11 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
         s->cfg.num_ranks <= 1 && s->level_round == 0 && (!s->arcs_known || s->cur_arcs < 8 * bound);
     if (edge_form && s->scan_pending) flush_scan(s);
     const bool dual = !edge_form && s->cfg.num_ranks <= 1 && s->level_round >= 1 && bound >= EDGE_HOOK_MIN_BOUND;
-    if (s->hooked) {
+    if (s->round_bucketed) {
+      // k_bmin hooked every fragment that has an outgoing edge; the jump resolves the mutual
+      // pairs and counts the hooks
+      if (s->scan_pending) flush_scan(s);
+    } else if (s->hooked) {
       // multi-rank: par / in_mst / totals already written by ghs_solver_unpack_hook
       if (s->scan_pending) flush_scan(s);
     } else if (edge_form) {
@@ -3269,14 +3638,17 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
     GHS_HIP_CHECK(hipGetLastError());
     if (s->detail) record(s, 2);
     // Stage 3, then the next active list (one launch each)
+    // a bucketed round's hooks are counted by the jump: its grid is capped (one pair of
+    // same-address atomics per block)
+    unsigned long long *acc = s->round_bucketed ? s->cnt + C_WEIGHT : nullptr;
     if (s->act_ident && (s->cfg.num_ranks <= 1 || s->level_dense)) {
       const uint32_t ni = s->level_dense ? (uint32_t)s->dense_n : s->n;
       KT(GHS_K_JUMP_IDENT, ni);
-      k_jump_ident<<<grid_for(((uint64_t)ni + 3) / 4, BLOCK, 16384), BLOCK, 0, s->stream>>>(ni, s->par, s->lab, s->best,
-                                                                                          s->flags, s->cnt + C_ERR);
+      k_jump_ident<<<grid_for(((uint64_t)ni + 3) / 4, BLOCK, acc ? HOOK_G : 16384), BLOCK, 0, s->stream>>>(
+          ni, s->par, s->lab, s->best, s->flags, s->cnt + C_ERR, acc);
     } else {
       KT(GHS_K_JUMP, 0);
-      k_jump<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->par, s->lab, s->best, s->flags, s->cnt + C_ERR);
+      k_jump<<<acc ? gh : g, BLOCK, 0, s->stream>>>(act, d_nact, s->par, s->lab, s->best, s->flags, s->cnt + C_ERR, acc);
     }
     GHS_HIP_CHECK(hipGetLastError());
     if (s->detail) record(s, 3);
@@ -3300,6 +3672,7 @@ static int wait_slot(ghs_solver *s, const RoundSlot *hs, unsigned long long seq)
   unsigned spins = 0;
   bool quiet = true;
   while (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) != seq) {
+    if ((spins & 255) == 0 && solver_cancelled(s)) GHS_FAIL(GHS_E_STATE, "cancelled: another rank of the solve failed");
     if ((++spins & 255) == 0 && quiet)
       quiet = std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(SLOT_QUIET_MS);
     if (!quiet && (spins & 255) == 0) {
@@ -3348,7 +3721,26 @@ static void close_level(ghs_solver *s) {
 // Each round copies (live, active, edges, err) to a pinned slot behind an event; the host waits
 // only for the round LOOKAHEAD back. Rounds past the last are no-ops on the device (zero active
 // fragments, zero live inter-fragment edges) and are discarded.
+// Bucketed rounds or not, once per solve (one rank): the plan's locality flag. The host waits for
+// the plan copy here — k_sample_weights / k_plan run first on the stream, so the wait overlaps the
+// first canonical pass already enqueued behind them.
+static int decide_bucketed(ghs_solver *s) {
+  s->bucket_decided = true;
+  s->bucketed = false;
+  const uint32_t opt = s->cfg.options;
+  if (s->cfg.num_ranks > 1 || !s->rec_a || (opt & GHS_OPT_NO_BUCKETED)) return GHS_OK;
+  if (opt & GHS_OPT_BUCKETED) {
+    s->bucketed = true;
+    return GHS_OK;
+  }
+  if (int rc = plan_sync(s)) return rc;
+  s->bucketed = s->h_thr[PLAN_LOCAL] != 0;
+  return GHS_OK;
+}
+
 static int run_level_pipelined(ghs_solver *s) {
+  if (!s->bucket_decided)
+    if (int rc = decide_bucketed(s)) return rc;
   const uint32_t round0 = s->round;
   uint64_t live_prev = s->cur_arcs, nact_prev = s->level_nact;  // inputs of the next checked round
   uint32_t issued = 0, checked = 0;
@@ -3670,7 +4062,7 @@ int ghs_solver_pack_best(ghs_solver_t *s, int64_t *d_dense) {
   if (s->nact) {
     const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
     KT(GHS_K_PACK, s->nact);
-    k_pack_best<<<grid_for(s->nact, 256, 16384), 256, 0, s->stream>>>(act, cur_act_count(s), s->best, d_dense);
+    k_pack_best<<<grid_for(s->nact, 256, 16384), 256, 0, s->stream>>>(act, cur_act_count(s), s->best, d_dense, s->nact);
     GHS_HIP_CHECK(hipGetLastError());
   }
   return GHS_OK;
@@ -3763,6 +4155,90 @@ int ghs_solver_contract(ghs_solver_t *s, int *done) {
   return GHS_OK;
 }
 
+}  // extern "C"
+
+// Multi-rank round loop (ghs_solver_run), pipelined: rounds >= 2 of a level are contracted without
+// a host sync. The round's last kernel reports to a pinned slot; the host reads the report of the
+// round BEFORE the one just enqueued (one round in flight), so round r + 1 is enqueued while round r
+// still runs. Round r + 1's collective count is a bound: every active fragment of a round hooks or
+// is hooked by another active one, so a round's active fragments are at most half the previous
+// round's — floor(exact >> rounds since the latest exact count); the packed slots past the device
+// count hold "no edge" on every rank, and every rank computes the same bounds. Rounds 0 and 1 keep
+// the synchronous contract (round 1's bound from round 0's count would be far too loose: R-MAT s26
+// x8, level 1: 11.7M bound vs 195K active). A level whose report shows <= 1 active fragment ends;
+// the one round already enqueued past it is a no-op on the device (guards on the device counts).
+int ghs_solver_contract_async(ghs_solver *s, int *done) {
+  if (!s) GHS_FAIL(GHS_E_ARG, "solver is NULL");
+  if (s->phase == 2) {
+    if (done) *done = 1;
+    return GHS_OK;
+  }
+  if (s->cfg.num_ranks <= 1 || s->level_round < 2) {
+    const int rc = ghs_solver_contract(s, done);
+    if (!rc && s->phase == 0 && s->level_round == 2) {  // round 2 comes next: its count is exact
+      s->pipe.clear();
+      s->pipe_exact = s->nact;
+      s->pipe_exact_lr = 2;
+      s->pipe_live = s->h_cnt[C_LIVE];
+    }
+    return rc;
+  }
+  if (s->phase != 1) GHS_FAIL(GHS_E_STATE, "contract must follow minedge");
+  s->report_final = false;
+  const unsigned long long seq = ++s->res->seq;
+  if (int rc = enqueue_contract(s, &s->d_slot[seq % SLOT_RING], seq)) return rc;
+  s->hooked = false;
+  s->pipe.push_back({seq, s->round, s->level_round});
+  advance_round(s);
+  bool level_done = false;
+  while (s->pipe.size() > 1 && !level_done) {  // read every report but the newest round's
+    const ghs_solver::PipeRound p = s->pipe.front();
+    s->pipe.erase(s->pipe.begin());
+    const RoundSlot *hs = s->h_slot + (p.seq % SLOT_RING);
+    if (int rc = wait_slot(s, hs, p.seq)) return rc;
+    const unsigned long long err = hs->err, nact_in = hs->nact_in, nact_out = hs->nact_out;
+    const unsigned long long live_out = hs->live_out, edges = hs->edges;
+    if (err) return fail_counters(s, err, ("in round " + std::to_string(p.round + 1)).c_str());
+    push_stats(s, p.level_round, s->pipe_live, nact_in, edges);
+    s->pipe_live = live_out;
+    s->pipe_exact = nact_out;  // the active fragments at the start of round p + 1
+    s->pipe_exact_lr = p.level_round + 1;
+    if (nact_out <= 1) {  // the level ended with round p: later rounds are no-ops
+      level_done = true;
+      s->round = p.round + 1;
+      s->level_round = p.level_round + 1;
+    }
+  }
+  if (level_done) {
+    s->pipe.clear();
+    if (int rc = dense_close(s)) return rc;
+    close_level(s);
+  } else {
+    s->nact = s->pipe_exact >> (s->level_round - s->pipe_exact_lr);  // bound for the next round
+    if (s->nact <= 1) {
+      // the bound says the level is over (<= 1 fragment can remain): the rounds in flight finish
+      // it; wait for them so their stats and errors are read, then close the level
+      while (!s->pipe.empty()) {
+        const ghs_solver::PipeRound p = s->pipe.front();
+        s->pipe.erase(s->pipe.begin());
+        const RoundSlot *hs = s->h_slot + (p.seq % SLOT_RING);
+        if (int rc = wait_slot(s, hs, p.seq)) return rc;
+        if (hs->err) return fail_counters(s, hs->err, ("in round " + std::to_string(p.round + 1)).c_str());
+        push_stats(s, p.level_round, s->pipe_live, hs->nact_in, hs->edges);
+        s->pipe_live = hs->live_out;
+      }
+      if (int rc = dense_close(s)) return rc;
+      close_level(s);
+    } else {
+      s->phase = 0;
+    }
+  }
+  if (done) *done = (s->phase == 2);
+  return GHS_OK;
+}
+
+extern "C" {
+
 int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *stats) {
   if (!s) GHS_FAIL(GHS_E_ARG, "solver is NULL");
   if (s->phase != 2) GHS_FAIL(GHS_E_STATE, "finish before the loop terminated");
@@ -3806,7 +4282,7 @@ int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *
     result->canon_edges = s->e_hi - s->e_lo;
     result->select_out = s->select_out;
     result->filter_out = s->filter_out;
-    result->pass_flags = 0;
+    result->pass_flags = s->bucketed ? 1u : 0u;
   }
   return GHS_OK;
 }

@@ -67,6 +67,8 @@ int ghs_solver_flag_bits_async(ghs_solver *s, uint64_t **d_bits, uint64_t *words
 // a multi-rank driver's shared failure flag: the solver's waits end once it is set
 void ghs_solver_set_group_cancel(ghs_solver *s, const int *flag);
 bool ghs_solver_cancelled_of(const ghs_solver *s);
+// the multi-rank round loop's contract: rounds >= 2 of a level pipelined (no host sync)
+int ghs_solver_contract_async(ghs_solver *s, int *done);
 
 #define GHS_HIP_CHECK(expr)                                                                     \
   do {                                                                                          \

@@ -275,7 +275,7 @@ int run_loop(ghs_solver_t *s, ghs_comm *c) {
       }
     }
     int done = 0;
-    LOOP_CHECK(ghs_solver_contract(s, &done));
+    LOOP_CHECK(ghs_solver_contract_async(s, &done));
     if (done) return GHS_OK;
   }
 }

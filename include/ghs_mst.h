@@ -68,7 +68,7 @@ typedef struct ghs_result {
   uint32_t rounds;            /* Boruvka rounds executed (all levels) */
   uint32_t num_stats;         /* entries filled in the stats array (<= GHS_MAX_ROUND_STATS) */
   uint32_t levels;            /* weight levels planned */
-  uint32_t pass_flags;        /* reserved (0); ABI 4's bucketed heavy-edge passes were removed */
+  uint32_t pass_flags;        /* bit 0: the solve ran bucketed rounds (k_bucket / k_bmin) */
   double ms_total;            /* host wall time of the solve (device-resident input -> flags) */
   /* The two full streams over the canonical list (HIP events on the solve's stream). */
   float ms_select;            /* k_select: validation + level-0 split */
@@ -89,6 +89,10 @@ typedef struct ghs_result {
 #define GHS_OPT_NO_SEED_RUNS 0x1u  /* level 0, round 0: a-side minima through the min-edge kernel
                                       instead of the single-writer run seeding */
 #define GHS_OPT_NO_DENSE 0x2u      /* several ranks: levels in vertex labels, not dense labels */
+#define GHS_OPT_BUCKETED 0x4u      /* one rank: every round bucketed, whatever the graph (default:
+                                      a lattice-like graph's rounds with >= 2^20 active fragments,
+                                      decided from the plan's span sample; tests force it) */
+#define GHS_OPT_NO_BUCKETED 0x8u   /* one rank: never bucketed rounds */
 #define GHS_OPT_DEBUG 0x10u        /* per-level sizes on stderr (diagnostic) */
 #define GHS_OPT_TIME_ROUNDS 0x20u  /* HIP events around the compacting min-edge launches
                                       (ghs_round_stats_t.ms_minedge; idles the GPU ~6 us each) */
@@ -263,7 +267,7 @@ enum ghs_kernel_id {
   GHS_K_SELECT = 0, GHS_K_FILTER, GHS_K_LEVEL_PASS, GHS_K_SEED_RUNS, GHS_K_MINEDGE_IDENT, GHS_K_MINEDGE_COMPACT,
   GHS_K_WIN, GHS_K_HOOK, GHS_K_JUMP_IDENT, GHS_K_JUMP, GHS_K_SELECT_LB, GHS_K_RESOLVE, GHS_K_GIANT, GHS_K_SCAN,
   GHS_K_PLAN, GHS_K_INIT, GHS_K_PACK, GHS_K_UNPACK, GHS_K_ROUND_REPORT, GHS_K_PACK_HOOK, GHS_K_UNPACK_HOOK,
-  GHS_K_DENSE, GHS_K_FLAG_BITS, GHS_K_COUNT
+  GHS_K_DENSE, GHS_K_FLAG_BITS, GHS_K_BUCKET, GHS_K_BMIN, GHS_K_COUNT
 };
 typedef struct ghs_kernel_record {
   uint32_t kernel;  /* ghs_kernel_id */

@@ -368,6 +368,9 @@ def test_native_loop_emulated_vs_oracle(world, graph, torch_cuda):
     assert np.array_equal(flags.cpu().numpy().astype(bool), ref_in.astype(bool))
     assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
     assert len(stats) == res.num_stats
+    # rounds >= 2 of a level are pipelined (read from the round reports): every round's stats once
+    assert sum(st["hooks"] for st in stats) == ref_k or res.rounds > len(stats)
+    assert res.rounds == len(stats) or res.rounds > 64
 
 
 @pytest.mark.parametrize("dedup_max", [128, 1000000000])
@@ -740,3 +743,50 @@ def test_cli_generator_and_multi_gpu_flag(tmp_path, torch_cuda):
     n, u, v, w = ora.rmat_canonical(12, 16, 1, 2)
     _, ref_tw, ref_k = ora.kruskal_c(n, u, v, w)
     assert res["total_weight"] == ref_tw and res["num_edges"] == ref_k
+
+
+@pytest.mark.parametrize("graph", ["rmat", "rmat20", "ties", "forest", "readme", "grid", "grid-gradient"])
+@pytest.mark.parametrize("levels", [None, 1])
+def test_bucketed_rounds_vs_oracle(graph, levels, torch_cuda):
+    """Bucketed rounds (k_bucket groups the live edges by target bucket, k_bmin takes every
+    fragment's minimum in LDS and hooks it; mutual pairs resolved by the jump) forced onto every
+    round of every graph kind (GHS_OPT_BUCKETED): the oracle's MSF and totals, the same flags as
+    the unbucketed rounds, and pass_flags says they ran."""
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import DeviceMST
+    ora = _oracle()
+    e = _test_graph(graph)
+    g = e.to_host()
+    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    kw = {} if levels is None else {"max_levels": levels}
+    on = DeviceMST(e, config=_native.make_config(options=_native.OPT_BUCKETED, **kw))
+    res, _ = on.run()
+    assert res.pass_flags & 1
+    assert np.array_equal(on.in_mst_host(), ref_in.astype(bool))
+    assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
+    res2, _ = on.run()  # repeat on the same workspace
+    assert (res2.total_weight, res2.num_mst_edges) == (ref_tw, ref_k)
+    off = DeviceMST(e, config=_native.make_config(options=_native.OPT_NO_BUCKETED, **kw))
+    res0, _ = off.run()
+    assert not res0.pass_flags & 1
+    assert np.array_equal(off.in_mst_host(), ref_in.astype(bool))
+
+
+@pytest.mark.parametrize("k,mode", [(2048, 0), (2048, 1), (1500, 0)])
+def test_bucketed_auto_on_lattices(k, mode, torch_cuda):
+    """The default path picks bucketed rounds for lattices (the plan's span sample) and not for
+    R-MAT; grids large enough for bucketed rounds past the first (>= 2^20 active fragments) match
+    the oracle."""
+    from distributed_ghs_implementation_amd.device import DeviceMST, generate_grid, generate_rmat
+    ora = _oracle()
+    e = generate_grid(k, mode)
+    eng = DeviceMST(e)
+    res, stats = eng.run()
+    assert res.pass_flags & 1
+    g = e.to_host()
+    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    assert np.array_equal(eng.in_mst_host(), ref_in.astype(bool))
+    assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k) and ref_k == g.n - 1
+    r = generate_rmat(16, 16, seed=1, wseed=2)
+    res_r, _ = DeviceMST(r).run()
+    assert not res_r.pass_flags & 1
