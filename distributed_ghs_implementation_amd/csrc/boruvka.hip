@@ -1978,6 +1978,10 @@ constexpr uint32_t BK_G = 512;        // k_bucket blocks = record regions
 constexpr uint32_t BK_T = 512;        // k_bucket threads
 constexpr uint32_t BK_MAX_B = 16384;  // buckets: k_bucket's LDS counters (64 KiB)
 constexpr uint32_t BM_T = 1024;       // k_bmin threads
+#ifndef GHS_BK_TILES
+#define GHS_BK_TILES 2
+#endif
+constexpr int BK_TILES = GHS_BK_TILES;  // k_bucket: 4-edge tiles per lane in flight
 
 // a block's share of the T live edges (a multiple of 4: whole 4-entry tiles); region g of the
 // records starts at 2 * quota * g (an edge gives at most two records)
@@ -2060,18 +2064,29 @@ __global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ sr
   __syncthreads();
   const uint32_t slo = s_seg[0], shi = s_seg[1];
   // pass A: records per bucket (the a and b ends only); every lane of a wave iterates while the
-  // wave's first tile is in range (the bumps are wave-collective)
+  // wave's first tile is in range (the bumps are wave-collective); BK_TILES 4-edge tiles per lane
+  // per iteration, all loads issued before the first bump
   const uint32_t lane = threadIdx.x & (WAVE - 1);
-  for (uint64_t v = vb + (uint64_t)threadIdx.x * 4; v - lane * 4 < ve; v += (uint64_t)BK_T * 4) {
-    const uint64_t i0 = tile_phys(in, slo, shi, v, ve);
-    const uint4 a4 = *reinterpret_cast<const uint4 *>(src + i0), b4 = *reinterpret_cast<const uint4 *>(dst + i0);
-    const uint32_t A[4] = {a4.x, a4.y, a4.z, a4.w}, B[4] = {b4.x, b4.y, b4.z, b4.w};
+  constexpr uint64_t STRIDE = (uint64_t)BK_T * 4;
+  for (uint64_t v0 = vb + (uint64_t)threadIdx.x * 4; v0 - lane * 4 < ve; v0 += STRIDE * BK_TILES) {
+    uint4 a4[BK_TILES], b4[BK_TILES];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bool live = (v < ve) & (A[j] != LABEL_NONE);  // past the range / region padding
-      const uint32_t ba = A[j] >> bs, bb = B[j] >> bs;
-      lds_bump<false>(s_h, ba, live);
-      lds_bump<false>(s_h, bb, live && bb != ba);
+    for (int q = 0; q < BK_TILES; ++q) {
+      const uint64_t i0 = tile_phys(in, slo, shi, v0 + STRIDE * q, ve);
+      a4[q] = *reinterpret_cast<const uint4 *>(src + i0);
+      b4[q] = *reinterpret_cast<const uint4 *>(dst + i0);
+    }
+#pragma unroll
+    for (int q = 0; q < BK_TILES; ++q) {
+      const uint64_t v = v0 + STRIDE * q;
+      const uint32_t A[4] = {a4[q].x, a4[q].y, a4[q].z, a4[q].w}, B[4] = {b4[q].x, b4[q].y, b4[q].z, b4[q].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool live = (v < ve) & (A[j] != LABEL_NONE);  // past the range / region padding
+        const uint32_t ba = A[j] >> bs, bb = B[j] >> bs;
+        lds_bump<false>(s_h, ba, live);
+        lds_bump<false>(s_h, bb, live && bb != ba);
+      }
     }
   }
   __syncthreads();
@@ -2092,29 +2107,39 @@ __global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ sr
   __syncthreads();  // the cursors below advance s_h
   // pass B: the records at the cursors of their buckets
   const uint64_t base = 2 * vb;
-  for (uint64_t v = vb + (uint64_t)threadIdx.x * 4; v - lane * 4 < ve; v += (uint64_t)BK_T * 4) {
-    const uint64_t i0 = tile_phys(in, slo, shi, v, ve);
-    const uint4 a4 = *reinterpret_cast<const uint4 *>(src + i0), b4 = *reinterpret_cast<const uint4 *>(dst + i0);
-    const ulonglong2 k01 = *reinterpret_cast<const ulonglong2 *>(key + i0);
-    const ulonglong2 k23 = *reinterpret_cast<const ulonglong2 *>(key + i0 + 2);
-    const uint32_t A[4] = {a4.x, a4.y, a4.z, a4.w}, B[4] = {b4.x, b4.y, b4.z, b4.w};
-    const uint64_t K[4] = {k01.x, k01.y, k23.x, k23.y};
+  for (uint64_t v0 = vb + (uint64_t)threadIdx.x * 4; v0 - lane * 4 < ve; v0 += STRIDE * BK_TILES) {
+    uint4 a4[BK_TILES], b4[BK_TILES];
+    ulonglong2 k01[BK_TILES], k23[BK_TILES];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bool live = (v < ve) & (A[j] != LABEL_NONE);
-      const uint32_t ba = A[j] >> bs, bb = B[j] >> bs;
-      const bool two = live && bb != ba;
-      const uint32_t pa = lds_bump<true>(s_h, ba, live);
-      const uint32_t pb = lds_bump<true>(s_h, bb, two);
-      if (live) {
-        ra[base + pa] = A[j];
-        rb[base + pa] = B[j];
-        rk[base + pa] = K[j];
-      }
-      if (two) {
-        ra[base + pb] = A[j];
-        rb[base + pb] = B[j];
-        rk[base + pb] = K[j];
+    for (int q = 0; q < BK_TILES; ++q) {
+      const uint64_t i0 = tile_phys(in, slo, shi, v0 + STRIDE * q, ve);
+      a4[q] = *reinterpret_cast<const uint4 *>(src + i0);
+      b4[q] = *reinterpret_cast<const uint4 *>(dst + i0);
+      k01[q] = *reinterpret_cast<const ulonglong2 *>(key + i0);
+      k23[q] = *reinterpret_cast<const ulonglong2 *>(key + i0 + 2);
+    }
+#pragma unroll
+    for (int q = 0; q < BK_TILES; ++q) {
+      const uint64_t v = v0 + STRIDE * q;
+      const uint32_t A[4] = {a4[q].x, a4[q].y, a4[q].z, a4[q].w}, B[4] = {b4[q].x, b4[q].y, b4[q].z, b4[q].w};
+      const uint64_t K[4] = {k01[q].x, k01[q].y, k23[q].x, k23[q].y};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool live = (v < ve) & (A[j] != LABEL_NONE);
+        const uint32_t ba = A[j] >> bs, bb = B[j] >> bs;
+        const bool two = live && bb != ba;
+        const uint32_t pa = lds_bump<true>(s_h, ba, live);
+        const uint32_t pb = lds_bump<true>(s_h, bb, two);
+        if (live) {
+          ra[base + pa] = A[j];
+          rb[base + pa] = B[j];
+          rk[base + pa] = K[j];
+        }
+        if (two) {
+          ra[base + pb] = A[j];
+          rb[base + pb] = B[j];
+          rk[base + pb] = K[j];
+        }
       }
     }
   }
@@ -2123,7 +2148,10 @@ __global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ sr
 // k_bmin: BM_ILP records in flight per lane; the bucket's non-empty runs listed first (a lattice
 // bucket's records come from one to three block regions), so locating a record searches that
 // short list
-constexpr int BM_ILP = 4;
+#ifndef GHS_BM_ILP
+#define GHS_BM_ILP 8
+#endif
+constexpr int BM_ILP = GHS_BM_ILP;
 template <uint32_t BS>
 __global__ __launch_bounds__(BM_T) void k_bmin(const uint32_t *__restrict__ ra, const uint32_t *__restrict__ rb,
                                                const uint64_t *__restrict__ rk, const uint32_t *__restrict__ O,
@@ -3494,11 +3522,21 @@ static void flush_scan(ghs_solver *s) {
 }
 
 // ---- one round, enqueued without a host sync (sizes on the device; s->nact is a bound) --------
-// Bucketed rounds (k_bucket + k_bmin, one rank): a level's first round, and later rounds while the
-// host's bound on the active fragments is at least BUCKET_MIN_ACTIVE (below it the min-edge
-// kernel's LDS cache of fragment minima absorbs the candidates, and k_bmin's per-bucket setup
-// would dominate).
-constexpr uint64_t BUCKET_MIN_ACTIVE = 1u << 20;
+// Bucketed rounds (k_bucket + k_bmin, one rank): level 0's rounds while the host's bound on the
+// active fragments is at least BUCKET_MIN_ACTIVE. Past level 0 a giant fragment exists, and its
+// bucket's records all land on one k_bmin workgroup (16384^2 grid, level 1 round 0: k_bmin 10.0
+// ms vs 5.6 ms for the atomic min-edge + CONNECT); below the bound large fragments do the same
+// (the grid's level-0 rounds 4 and 5: 0.84 / 0.52 ms vs 0.55 / 0.17 ms), and the min-edge kernel's
+// LDS cache of fragment minima absorbs their candidates anyway.
+#ifndef GHS_BUCKET_MIN_ACTIVE
+#define GHS_BUCKET_MIN_ACTIVE (1u << 23)
+#endif
+constexpr uint64_t BUCKET_MIN_ACTIVE = GHS_BUCKET_MIN_ACTIVE;
+// k_jump_ident's grid when it counts the round's hooks (one pair of same-address atomics per block)
+#ifndef GHS_JUMP_COUNT_G
+#define GHS_JUMP_COUNT_G 2048
+#endif
+constexpr unsigned JUMP_COUNT_G = GHS_JUMP_COUNT_G;
 
 static void enqueue_bmin(ghs_solver *s, const uint32_t *a, const uint32_t *b, const uint64_t *k, SegView in,
                          const unsigned long long *guard, uint64_t items) {
@@ -3523,7 +3561,7 @@ static int enqueue_minedge(ghs_solver *s) {
   ArcBuf &O = s->buf[s->cur ^ 1];
   SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
   // GHS_OPT_BUCKETED (forced) runs every round bucketed: the test suite's coverage of them
-  s->round_bucketed = s->bucketed && (s->level_round == 0 || s->nact >= BUCKET_MIN_ACTIVE ||
+  s->round_bucketed = s->bucketed && ((s->level == 0 && s->nact >= BUCKET_MIN_ACTIVE) ||
                                       (s->cfg.options & GHS_OPT_BUCKETED));
   if (s->level_round == 0) {
     if (s->cur_arcs || !s->arcs_known) {
@@ -3644,7 +3682,7 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
     if (s->act_ident && (s->cfg.num_ranks <= 1 || s->level_dense)) {
       const uint32_t ni = s->level_dense ? (uint32_t)s->dense_n : s->n;
       KT(GHS_K_JUMP_IDENT, ni);
-      k_jump_ident<<<grid_for(((uint64_t)ni + 3) / 4, BLOCK, acc ? HOOK_G : 16384), BLOCK, 0, s->stream>>>(
+      k_jump_ident<<<grid_for(((uint64_t)ni + 3) / 4, BLOCK, acc ? JUMP_COUNT_G : 16384), BLOCK, 0, s->stream>>>(
           ni, s->par, s->lab, s->best, s->flags, s->cnt + C_ERR, acc);
     } else {
       KT(GHS_K_JUMP, 0);

@@ -370,8 +370,19 @@ void rank_release(Rank &d) {
   if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
-// first failing rank's error, then the totals agree on every rank
+// a rank's error that only reports another rank's failure (a cancelled wait, a failed agreement)
+bool peer_error(const Rank &x) {
+  return x.rc == GHS_E_STATE && (x.err.rfind("cancelled", 0) == 0 || x.err.rfind("another rank", 0) == 0);
+}
+
+// the first failing rank's own error (over those that only saw a peer fail), then the totals agree
+// on every rank
 int collect(std::vector<Rank> &d, ghs_result_t *result, ghs_round_stats_t *stats, std::string *err) {
+  for (auto &x : d)
+    if (x.rc && !peer_error(x)) {
+      *err = x.err;
+      return x.rc;
+    }
   for (auto &x : d)
     if (x.rc) {
       *err = x.err;

@@ -53,6 +53,7 @@ int oracle_boruvka_omp(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t
     return ORC_E_NOMEM;
   }
   uint64_t tw = 0, ne = 0, round_hooks = 0;
+  int moved = 0; /* pointer doubling: some parent moved this pass */
   uint32_t rounds = 0;
 #pragma omp parallel num_threads(T)
   {
@@ -110,13 +111,38 @@ int oracle_boruvka_omp(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t
       round_hooks += my_e;
 #pragma omp barrier
       if (round_hooks == 0) break; /* every thread reads the same total */
-      /* new root of every old root (parent chains are acyclic after the mutual break) */
+      /* new root of every old root (parent chains are acyclic after the mutual break): pointer
+       * doubling until no parent moves — chains can be long (gradient grids: thousands of hops),
+       * where a plain walk per root would be quadratic. par only moves to an ancestor, so the
+       * racy in-place updates converge to the roots. */
+      for (;;) {
+#pragma omp single
+        moved = 0;
+        int my_moved = 0;
+#pragma omp for schedule(static)
+        for (uint64_t x = 0; x < n; ++x) {
+          if (comp[x] != (uint32_t)x) continue;
+          const uint32_t p = par[x], pp = par[p];
+          if (pp != p) {
+            par[x] = pp;
+            my_moved = 1;
+          }
+        }
+        if (my_moved) {
+#pragma omp atomic write
+          moved = 1;
+        }
+#pragma omp barrier
+        int any;
+#pragma omp atomic read
+        any = moved;
+#pragma omp barrier
+        if (!any) break;
+      }
 #pragma omp for schedule(static)
       for (uint64_t x = 0; x < n; ++x) {
         if (comp[x] != (uint32_t)x) continue;
-        uint32_t r = (uint32_t)x;
-        while (par[r] != r) r = par[r];
-        nr[x] = r;
+        nr[x] = par[x];
         best[x] = UINT64_MAX;
       }
       /* every vertex's label is an old root: one lookup resolves it */
