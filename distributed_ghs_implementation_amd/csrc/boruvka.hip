@@ -248,6 +248,17 @@ __device__ __forceinline__ uint4 ld_b128(__amdgpu_buffer_rsrc_t r, uint32_t byte
   return make_uint4(x.x, x.y, x.z, x.w);
 }
 
+// The same as a non-temporal (streaming) load: the canonical list is read once per pass, and
+// default-policy lines of a 3-12 GB stream evict the L2-resident giant bitmap that the pass's
+// random probes need (R-MAT s26: 8 MiB bitmap, 4 MiB L2 per XCD). cache policy bits: nt = 2.
+#ifndef GHS_FILTER_NT
+#define GHS_FILTER_NT 1
+#endif
+__device__ __forceinline__ uint4 ld_b128_nt(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, GHS_FILTER_NT ? 2 : 0);
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
+
 __device__ __forceinline__ uint32_t ld_b32(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
   return __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, 0, 0);
 }
@@ -1684,7 +1695,7 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
   const uint32_t giant = giant_ptr[0];
   bool touch_giant = false;  // a level edge of this block has an end in the giant
   uint64_t nlev = 0, nrem = 0;
-  uint4 ca = ld_b128(ru, lane_off), cb = ld_b128(rv, lane_off), cw = ld_b128(rw, lane_off);
+  uint4 ca = ld_b128_nt(ru, lane_off), cb = ld_b128_nt(rv, lane_off), cw = ld_b128_nt(rw, lane_off);
   for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
     const uint64_t v = v0 + (uint64_t)threadIdx.x * 4;
     const uint64_t e0 = E0 + v;
@@ -1728,9 +1739,9 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
 #endif
     // next tile (out-of-range offsets read 0)
     const uint32_t noff = (uint32_t)(v0 + ARCS_PER_BLOCK - vb) * 4u + lane_off;
-    ca = ld_b128(ru, noff);
-    cb = ld_b128(rv, noff);
-    cw = ld_b128(rw, noff);
+    ca = ld_b128_nt(ru, noff);
+    cb = ld_b128_nt(rv, noff);
+    cw = ld_b128_nt(rw, noff);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
 #if !GHS_FILTER_GATED
@@ -2972,12 +2983,15 @@ static int event_wait(ghs_solver *s, hipEvent_t ev) {
     GHS_HIP_CHECK(hipEventSynchronize(ev));
     return GHS_OK;
   }
+  // a few tight polls, then a short sleep between polls: every poll is a runtime call, and several
+  // rank threads of one process (ghs_mst_multi / ghs_mst_emulated) polling back to back contend
+  // for the runtime's locks with each other's launches
   for (uint32_t spins = 0;; ++spins) {
     const hipError_t q = hipEventQuery(ev);
     if (q == hipSuccess) return GHS_OK;
     if (q != hipErrorNotReady) GHS_HIP_CHECK(q);
     if (solver_cancelled(s)) GHS_FAIL(GHS_E_STATE, "cancelled: another rank of the solve failed");
-    if (spins > 4096) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    if (spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(10));
   }
 }
 
@@ -3713,7 +3727,11 @@ static int wait_slot(ghs_solver *s, const RoundSlot *hs, unsigned long long seq)
     if ((spins & 255) == 0 && solver_cancelled(s)) GHS_FAIL(GHS_E_STATE, "cancelled: another rank of the solve failed");
     if ((++spins & 255) == 0 && quiet)
       quiet = std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(SLOT_QUIET_MS);
-    if (!quiet && (spins & 255) == 0) {
+    if (!quiet) {
+      // a long wait (a multi-rank solve's peers share the device, or the stream failed): check the
+      // stream now and then, sleeping between checks (a runtime call per spin from several rank
+      // threads starved the other ranks' launches: one emulated s26 x8 solve took 5.7 s)
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
       const hipError_t q = hipStreamQuery(s->stream);
       if (q != hipSuccess && q != hipErrorNotReady) GHS_HIP_CHECK(q);
       if (q == hipSuccess && __atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) != seq)
@@ -4211,7 +4229,10 @@ int ghs_solver_contract_async(ghs_solver *s, int *done) {
     if (done) *done = 1;
     return GHS_OK;
   }
-  if (s->cfg.num_ranks <= 1 || s->level_round < 2) {
+#ifndef GHS_PIPE_MULTI
+#define GHS_PIPE_MULTI 1
+#endif
+  if (s->cfg.num_ranks <= 1 || s->level_round < 2 || !GHS_PIPE_MULTI) {
     const int rc = ghs_solver_contract(s, done);
     if (!rc && s->phase == 0 && s->level_round == 2) {  // round 2 comes next: its count is exact
       s->pipe.clear();
