@@ -59,6 +59,8 @@ def parse():
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse ranks sharing a GPU)")
     ap.add_argument("--verify-ranks", action="store_true", help="N>1: check every rank holds the same MSF")
     ap.add_argument("--no-scaling-base", action="store_true", help="N=1: skip the s26 strong-scaling point")
+    ap.add_argument("--options", type=lambda x: int(x, 0), default=0,
+                    help="ghs_config_t.options bits for N=1 (A/B of path options; 0 = the default path)")
     return ap.parse_args()
 
 
@@ -382,7 +384,11 @@ def main():
     n, m = edges.n, edges.m
     cfg.update({"n": n, "m": m, "partition": f"canonical edge ranges x{world}", "parallelism": f"edges{world}"})
 
-    eng = DistributedMST(edges, rank, world) if world > 1 else DeviceMST(edges)
+    if world > 1:
+        eng = DistributedMST(edges, rank, world)
+    else:
+        from distributed_ghs_implementation_amd import _native
+        eng = DeviceMST(edges, config=_native.make_config(options=args.options) if args.options else None)
     step = eng.run
     if world > 1:
         # N > 1: a step ends with the MSF on rank 0, as the reference's MPI run ends with

@@ -156,6 +156,7 @@ OPT_NO_BUCKETED = 0x8
 OPT_DEBUG = 0x10
 OPT_TIME_ROUNDS = 0x20
 OPT_DETAIL = 0x40
+OPT_BUCKETED_FIRST = 0x80
 
 
 class Config(ctypes.Structure):

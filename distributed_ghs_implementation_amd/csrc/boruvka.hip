@@ -1116,8 +1116,15 @@ __global__ void k_unpack_hook(const uint32_t *__restrict__ act, const unsigned l
 // round's hooks — every fragment that ends below another root adds its best key's weight (each MSF
 // edge once: a mutual pair's smaller member adds nothing).
 // ------------------------------------------------------------------------------------------
+// The jump's hook totals go to HOOK_SHARDS address pairs (one 64-B line each, by block) instead of
+// one pair: same-address device atomics serialise at ~12 ns each, which capped the counting jump's
+// grid at 2048 blocks (R-MAT s24: k_jump_ident 0.28 -> 0.46 ms in bucketed rounds). The last
+// select tile of the round folds the shards into the totals (k_select_lb).
+constexpr int HOOK_SHARDS = 64;   // == WAVE: one lane per shard in the fold
+constexpr int SHARD_STRIDE = 8;   // u64 per shard (64 B)
 __device__ __forceinline__ void add_totals(unsigned long long wsum, unsigned long long cnt,
                                            unsigned long long *__restrict__ acc) {
+  acc += SHARD_STRIDE * (blockIdx.x % HOOK_SHARDS);
   __shared__ unsigned long long s_w[BLOCK / WAVE], s_c[BLOCK / WAVE];
 #pragma unroll
   for (int d = WAVE / 2; d > 0; d >>= 1) {
@@ -2055,14 +2062,20 @@ __device__ __forceinline__ uint32_t lds_bump(uint32_t *s_h, uint32_t bkt, bool a
 
 __global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
                                                  const uint64_t *__restrict__ key, SegView in, uint32_t bs,
-                                                 uint32_t nb, uint32_t *__restrict__ ra, uint32_t *__restrict__ rb,
-                                                 uint64_t *__restrict__ rk, uint32_t *__restrict__ O,
-                                                 const unsigned long long *__restrict__ guard_nact) {
+                                                 uint32_t nb, uint4 *__restrict__ rec, uint32_t *__restrict__ O,
+                                                 const unsigned long long *__restrict__ guard_nact,
+                                                 const uint32_t *__restrict__ giant_ptr, uint64_t *__restrict__ best) {
   __shared__ uint32_t s_h[BK_MAX_B + 1];
   __shared__ uint32_t s_seg[2];
   __shared__ uint32_t s_wsum[BK_T / WAVE];
+  __shared__ unsigned long long s_gmin;
   // a lookahead round past the level's end (<= 1 active fragment) writes empty regions
   const bool noop = guard_nact && *guard_nact <= 1;
+  // a level's first round past level 0: the giant fragment's candidates (most of the level's
+  // edges have one end in it) are reduced in LDS and leave the block as one atomicMin on
+  // best[giant] instead of filling one bucket that a single k_bmin workgroup would have to sweep
+  const uint32_t giant = giant_ptr ? *giant_ptr : LABEL_NONE;
+  if (threadIdx.x == 0) s_gmin = KEY_NONE;
   const uint64_t T = noop ? 0 : in.prefix[in.nseg];
   const uint64_t Q = bk_quota(T);
   const uint64_t vb = Q * blockIdx.x;
@@ -2095,8 +2108,9 @@ __global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ sr
       for (int j = 0; j < 4; ++j) {
         const bool live = (v < ve) & (A[j] != LABEL_NONE);  // past the range / region padding
         const uint32_t ba = A[j] >> bs, bb = B[j] >> bs;
-        lds_bump<false>(s_h, ba, live);
-        lds_bump<false>(s_h, bb, live && bb != ba);
+        const bool ea = live && A[j] != giant;
+        lds_bump<false>(s_h, ba, ea);
+        lds_bump<false>(s_h, bb, live && B[j] != giant && (bb != ba || !ea));
       }
     }
   }
@@ -2138,21 +2152,20 @@ __global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ sr
       for (int j = 0; j < 4; ++j) {
         const bool live = (v < ve) & (A[j] != LABEL_NONE);
         const uint32_t ba = A[j] >> bs, bb = B[j] >> bs;
-        const bool two = live && bb != ba;
-        const uint32_t pa = lds_bump<true>(s_h, ba, live);
-        const uint32_t pb = lds_bump<true>(s_h, bb, two);
-        if (live) {
-          ra[base + pa] = A[j];
-          rb[base + pa] = B[j];
-          rk[base + pa] = K[j];
-        }
-        if (two) {
-          ra[base + pb] = A[j];
-          rb[base + pb] = B[j];
-          rk[base + pb] = K[j];
-        }
+        const bool ea = live && A[j] != giant;
+        const bool eb = live && B[j] != giant && (bb != ba || !ea);
+        const uint32_t pa = lds_bump<true>(s_h, ba, ea);
+        const uint32_t pb = lds_bump<true>(s_h, bb, eb);
+        const uint4 r = make_uint4(A[j], B[j], (uint32_t)K[j], (uint32_t)(K[j] >> 32));
+        if (ea) rec[base + pa] = r;
+        if (eb) rec[base + pb] = r;
+        if (live && (A[j] == giant || B[j] == giant) && K[j] < s_gmin) atomicMin(&s_gmin, (unsigned long long)K[j]);
       }
     }
+  }
+  if (giant != LABEL_NONE) {
+    __syncthreads();
+    if (threadIdx.x == 0 && s_gmin != KEY_NONE) flush_min(best, giant, s_gmin);
   }
 }
 
@@ -2163,12 +2176,13 @@ __global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ sr
 #define GHS_BM_ILP 8
 #endif
 constexpr int BM_ILP = GHS_BM_ILP;
+
 template <uint32_t BS>
-__global__ __launch_bounds__(BM_T) void k_bmin(const uint32_t *__restrict__ ra, const uint32_t *__restrict__ rb,
-                                               const uint64_t *__restrict__ rk, const uint32_t *__restrict__ O,
+__global__ __launch_bounds__(BM_T) void k_bmin(const uint4 *__restrict__ rec, const uint32_t *__restrict__ O,
                                                SegView in, uint32_t *__restrict__ par, uint64_t *__restrict__ best,
                                                uint8_t *__restrict__ in_mst,
-                                               const unsigned long long *__restrict__ guard_nact) {
+                                               const unsigned long long *__restrict__ guard_nact,
+                                               const uint32_t *__restrict__ giant_ptr) {
   constexpr uint32_t SPAN = 1u << BS;
   __shared__ unsigned long long s_min[SPAN];
   __shared__ uint64_t s_pos[BK_G];  // non-empty run i: its first record's position
@@ -2178,6 +2192,9 @@ __global__ __launch_bounds__(BM_T) void k_bmin(const uint32_t *__restrict__ ra, 
   const uint64_t T = noop ? 0 : in.prefix[in.nseg];
   const uint64_t R2 = 2 * bk_quota(T);  // record region stride
   const uint32_t t = blockIdx.x, tb = t << BS;
+  // the giant's candidates never became records (k_bucket reduced them), but a record of this
+  // bucket may still have the giant as its other end: it is no target here
+  const uint32_t giant = giant_ptr ? *giant_ptr : LABEL_NONE;
   uint32_t cnt = 0, st = 0;
   if (threadIdx.x < BK_G && !noop) {
     st = O[(uint64_t)t * BK_G + threadIdx.x];
@@ -2210,18 +2227,35 @@ __global__ __launch_bounds__(BM_T) void k_bmin(const uint32_t *__restrict__ ra, 
     for (int j = 0; j < BM_ILP; ++j) {
       const uint32_t r = r0 + j * BM_T;
       const uint64_t p = r < R ? locate(r) : 0;
-      a[j] = r < R ? ra[p] : LABEL_NONE;
-      b[j] = r < R ? rb[p] : LABEL_NONE;
-      k[j] = r < R ? rk[p] : KEY_NONE;
+      const uint4 x = rec[p];
+      a[j] = r < R ? x.x : LABEL_NONE;
+      b[j] = r < R ? x.y : LABEL_NONE;
+      k[j] = r < R ? ((unsigned long long)x.w << 32 | x.z) : KEY_NONE;
     }
 #pragma unroll
     for (int j = 0; j < BM_ILP; ++j) {
-      if ((a[j] >> BS) == t) atomicMin(&s_min[a[j] - tb], k[j]);
-      if ((b[j] >> BS) == t) atomicMin(&s_min[b[j] - tb], k[j]);
+      if ((a[j] >> BS) == t && a[j] != giant) atomicMin(&s_min[a[j] - tb], k[j]);
+      if ((b[j] >> BS) == t && b[j] != giant) atomicMin(&s_min[b[j] - tb], k[j]);
     }
   }
   __syncthreads();
-  // winners: exactly one record per target holds its minimum (keys are unique)
+  // the bucket's minima leave LDS in target order (one writer per target, consecutive lanes on
+  // consecutive slots): best[] and the MSF flag of every target's minimum edge. Scattered per-winner
+  // stores from the record sweep below measured 22 GB of HBM writes per 16384^2-grid solve for
+  // ~5 GB of payload (record order is not target order, and the records' stream evicts the
+  // partially written lines).
+  for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) {
+    const uint64_t v = s_min[i];
+    if (v != KEY_NONE) {
+      best[tb + i] = v;
+      in_mst[(uint32_t)v] = 1;
+    }
+  }
+  __syncthreads();
+  // winners: exactly one record per target holds its minimum (keys are unique); it replaces the
+  // slot by a tag carrying the other end (bit 31 set: a key's eid is < 2^31, so a tag never equals
+  // a key, and KEY_NONE's low word is not the tag's)
+  constexpr uint64_t TAG = 0x80000000ull;
   for (uint32_t r0 = threadIdx.x; r0 < R; r0 += STEP) {
     uint32_t a[BM_ILP], b[BM_ILP];
     unsigned long long k[BM_ILP];
@@ -2229,24 +2263,39 @@ __global__ __launch_bounds__(BM_T) void k_bmin(const uint32_t *__restrict__ ra, 
     for (int j = 0; j < BM_ILP; ++j) {
       const uint32_t r = r0 + j * BM_T;
       const uint64_t p = r < R ? locate(r) : 0;
-      a[j] = r < R ? ra[p] : LABEL_NONE;
-      b[j] = r < R ? rb[p] : LABEL_NONE;
-      k[j] = r < R ? rk[p] : KEY_NONE;
+      const uint4 x = rec[p];
+      a[j] = r < R ? x.x : LABEL_NONE;
+      b[j] = r < R ? x.y : LABEL_NONE;
+      k[j] = r < R ? ((unsigned long long)x.w << 32 | x.z) : KEY_NONE;
     }
 #pragma unroll
     for (int j = 0; j < BM_ILP; ++j) {
-      if ((a[j] >> BS) == t && s_min[a[j] - tb] == k[j]) {
-        par[a[j]] = b[j];
-        best[a[j]] = k[j];
-        in_mst[(uint32_t)k[j]] = 1;
-      }
-      if ((b[j] >> BS) == t && s_min[b[j] - tb] == k[j]) {
-        par[b[j]] = a[j];
-        best[b[j]] = k[j];
-        in_mst[(uint32_t)k[j]] = 1;
-      }
+      if ((a[j] >> BS) == t && s_min[a[j] - tb] == k[j]) s_min[a[j] - tb] = ((uint64_t)b[j] << 32) | TAG;
+      if ((b[j] >> BS) == t && s_min[b[j] - tb] == k[j]) s_min[b[j] - tb] = ((uint64_t)a[j] << 32) | TAG;
     }
   }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) {
+    const uint64_t v = s_min[i];
+    if ((uint32_t)v == (uint32_t)TAG) par[tb + i] = (uint32_t)(v >> 32);
+  }
+}
+
+// The giant fragment's CONNECT in a bucketed level-first round: its minimum (reduced by k_bucket)
+// is edge eid; the level's labels are resolved roots, so the other end's label is one read. A
+// mutual pair stays a 2-cycle for the jump, as in k_bmin.
+__global__ void k_giant_hook(const uint32_t *__restrict__ giant_ptr, const uint64_t *__restrict__ best,
+                             const uint32_t *__restrict__ eu, const uint32_t *__restrict__ ev,
+                             const uint32_t *__restrict__ lab, uint32_t *__restrict__ par, uint8_t *__restrict__ in_mst,
+                             unsigned long long *__restrict__ err) {
+  const uint32_t g = *giant_ptr;
+  const uint64_t k = best[g];
+  if (k == KEY_NONE) return;
+  const uint32_t eid = (uint32_t)k;
+  const uint32_t la = lab[eu[eid]], lb = lab[ev[eid]];
+  if (la != g && lb != g) atomicOr(err, 2ull);
+  par[g] = la == g ? lb : la;
+  in_mst[eid] = 1;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2632,7 +2681,8 @@ __global__ __launch_bounds__(BLOCK) void k_select_lb(const uint8_t *__restrict__
                                                      const unsigned long long *__restrict__ d_count, uint32_t groups,
                                                      uint32_t *__restrict__ out, unsigned long long *__restrict__ d_total,
                                                      unsigned long long *state, uint32_t tag, RoundSlot *slot,
-                                                     unsigned long long seq, unsigned long long *cnt) {
+                                                     unsigned long long seq, unsigned long long *cnt,
+                                                     unsigned long long *shards) {
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
   __shared__ uint64_t s_excl;
   __shared__ int s_ok;
@@ -2679,9 +2729,26 @@ __global__ __launch_bounds__(BLOCK) void k_select_lb(const uint8_t *__restrict__
     }
     run += gt;
   }
-  if (t == gridDim.x - 1 && threadIdx.x == 0) {
-    *d_total = s_excl + tot;
-    if (slot) write_report(slot, seq, cnt, s_excl + tot, count);
+  if (t == gridDim.x - 1 && threadIdx.x < WAVE) {
+    // a counting jump ran before (bucketed rounds): its sharded hook totals join the counters
+    // (read and cleared by device atomics: the shards live at the memory side like the adds)
+    if (shards) {
+      unsigned long long fw = atomicExch(shards + SHARD_STRIDE * threadIdx.x, 0ull);
+      unsigned long long fc = atomicExch(shards + SHARD_STRIDE * threadIdx.x + 1, 0ull);
+#pragma unroll
+      for (int d = WAVE / 2; d > 0; d >>= 1) {
+        fw += __shfl_xor(fw, d);
+        fc += __shfl_xor(fc, d);
+      }
+      if (threadIdx.x == 0 && fc) {
+        (void)atomicAdd(cnt + 2, fw);  // C_WEIGHT, C_EDGES (returning: complete before the report)
+        (void)atomicAdd(cnt + 3, fc);
+      }
+    }
+    if (threadIdx.x == 0) {
+      *d_total = s_excl + tot;
+      if (slot) write_report(slot, seq, cnt, s_excl + tot, count);
+    }
   }
 }
 
@@ -2734,7 +2801,8 @@ constexpr uint32_t LEVEL_ROUND_CAP = 64;  // hang guard: a level takes O(log n) 
 // more than a small solve (page-pinning, event objects), so the one-shot entry point keeps one
 // set per device for the process and reuses it; a stepwise solver handle owns its own.
 // counters: all zero, C_N = n (the vertex count as a device-side item count)
-__global__ void k_init_counters(unsigned long long *cnt, uint32_t n) {
+__global__ void k_init_counters(unsigned long long *cnt, uint32_t n, unsigned long long *shards) {
+  for (int i = threadIdx.x; i < HOOK_SHARDS * SHARD_STRIDE; i += blockDim.x) shards[i] = 0ull;
   for (int i = threadIdx.x; i < C_COUNT; i += blockDim.x) cnt[i] = (i == C_N) ? (unsigned long long)n : 0ull;
 }
 
@@ -2799,6 +2867,7 @@ struct ghs_solver {
   uint32_t *sample = nullptr;
   uint32_t *giant = nullptr;  // device [0] giant label, [1] its sampled vertex count
   unsigned long long *lb_state = nullptr;  // single-pass select: tile granules (zeroed at create)
+  unsigned long long *hook_acc = nullptr;  // sharded hook totals of the counting jumps (bucketed rounds)
   uint32_t lb_epoch = 0;                   // tag of the last select launch
   ArcBuf buf[2];             // a level's edges (regions) and the round double buffer
   ArcBuf rem[2];             // pending (not yet levelled) edges: u, v, key as regions
@@ -2881,11 +2950,14 @@ struct ghs_solver {
   uint64_t dense_n = 0;
   // bucketed rounds (single rank, lattice-like graphs; k_bucket / k_bmin): the record buffers,
   // the offsets table, the bucket geometry, and the per-solve / per-round decisions
-  uint32_t *rec_a = nullptr, *rec_b = nullptr, *bk_off = nullptr;
-  uint64_t *rec_k = nullptr;
+  uint4 *rec = nullptr;         // records (a, b, key): 16 B each
+  uint32_t *bk_off = nullptr;
   uint32_t bk_bs = 13, bk_nb = 0;
   bool bucketed = false;        // this solve runs bucketed rounds (decided once the plan landed)
   bool bucket_decided = false;
+  bool bucket_first_only = false;  // only the levels' first rounds (random-like graphs)
+  bool lattice = false;            // the plan's span sample says lattice-like
+  unsigned jump_ident_g = 16384;   // k_jump_ident's grid cap
   bool round_bucketed = false;  // the round being enqueued is bucketed
   // pipelined rounds of a multi-rank level (ghs_solver_contract_async, rounds >= 2): issued rounds
   // whose report is not read yet (oldest first), the latest exact active count and the level round
@@ -3087,6 +3159,7 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
   p = carve((PLAN_LOCAL + 1) * 8); if (s) s->d_thr = (uint64_t *)p;
   p = carve(16); if (s) s->giant = (uint32_t *)p;
   p = carve(LB_MAX_TILES * 8); if (s) s->lb_state = (unsigned long long *)p;  // select tile granules
+  p = carve(HOOK_SHARDS * SHARD_STRIDE * 8); if (s) s->hook_acc = (unsigned long long *)p;  // jump totals
   for (int b = 0; b < 2; ++b) {
     p = carve(cap * 4); if (s) s->buf[b].src = (uint32_t *)p;
     p = carve(cap * 4); if (s) s->buf[b].dst = (uint32_t *)p;
@@ -3109,9 +3182,7 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
   uint32_t bs = 0, nb = 0;
   if (local_edges == m && bucket_geometry(n, &bs, &nb)) {
     const uint64_t rc = 2 * cap + 8 * BK_G;
-    p = carve(rc * 4); if (s) s->rec_a = (uint32_t *)p;
-    p = carve(rc * 4); if (s) s->rec_b = (uint32_t *)p;
-    p = carve(rc * 8); if (s) s->rec_k = (uint64_t *)p;
+    p = carve(rc * 16); if (s) s->rec = (uint4 *)p;
     p = carve((size_t)(nb + 1) * BK_G * 4); if (s) s->bk_off = (uint32_t *)p;
     if (s) {
       s->bk_bs = bs;
@@ -3153,7 +3224,8 @@ static uint32_t next_tag(ghs_solver *s) {
 // (bound >= *d_count on the host sizes the grid). *d_total = kept items.
 // slot != nullptr: the kernel also reports the round (seq) to the pinned slot.
 static int select_lb(ghs_solver *s, const uint32_t *act, const unsigned long long *d_count, uint64_t bound,
-                     uint32_t *out, unsigned long long *d_total, RoundSlot *slot = nullptr, unsigned long long seq = 0) {
+                     uint32_t *out, unsigned long long *d_total, RoundSlot *slot = nullptr, unsigned long long seq = 0,
+                     bool fold_hooks = false) {
   if (bound == 0) {
     GHS_HIP_CHECK(hipMemsetAsync(d_total, 0, 8, s->stream));
     if (slot) {
@@ -3170,7 +3242,7 @@ static int select_lb(ghs_solver *s, const uint32_t *act, const unsigned long lon
   if (nb > LB_MAX_TILES || G >= (1ull << 20)) GHS_FAIL(GHS_E_STATE, "select: bad tiling");
   KT(GHS_K_SELECT_LB, bound);
   k_select_lb<<<(unsigned)nb, BLOCK, 0, s->stream>>>(s->flags, act, d_count, (uint32_t)G, out, d_total, s->lb_state,
-                                                     next_tag(s), slot, seq, s->cnt);
+                                                     next_tag(s), slot, seq, s->cnt, fold_hooks ? s->hook_acc : nullptr);
   GHS_HIP_CHECK(hipGetLastError());
   return GHS_OK;
 }
@@ -3546,26 +3618,48 @@ static void flush_scan(ghs_solver *s) {
 #define GHS_BUCKET_MIN_ACTIVE (1u << 23)
 #endif
 constexpr uint64_t BUCKET_MIN_ACTIVE = GHS_BUCKET_MIN_ACTIVE;
-// k_jump_ident's grid when it counts the round's hooks (one pair of same-address atomics per block)
-#ifndef GHS_JUMP_COUNT_G
-#define GHS_JUMP_COUNT_G 2048
+// a lattice-like solve also buckets the first round of every later level (the giant excluded).
+// Off: on the 16384^2 grid level 0 stops at the bond-percolation point, so level 1 has many large
+// fragments besides the sampled giant, each filling one bucket (k_bmin 7.1 -> 17.1 ms per solve,
+// step 43.1 -> 50.7 ms, same box).
+#ifndef GHS_BK_LEVEL_FIRST
+#define GHS_BK_LEVEL_FIRST 0
 #endif
-constexpr unsigned JUMP_COUNT_G = GHS_JUMP_COUNT_G;
+constexpr bool BK_LEVEL_FIRST = GHS_BK_LEVEL_FIRST;
+// k_jump_ident's grid cap on lattice-like solves. Path-splitting walks on long hook chains (the
+// gradient grid's columns) duplicate each other's work when too many start at once: the gradient
+// grid's level-0 jump took 1.8 ms at 2048 blocks and 3.6 ms at 16384; random graphs (short
+// chains) want every walk in flight (R-MAT s24 bucketed rounds: 0.46 ms at 2048 blocks, 0.34 at
+// 16384).
+#ifndef GHS_JUMP_LATTICE_G
+#define GHS_JUMP_LATTICE_G 2048
+#endif
+constexpr unsigned JUMP_LATTICE_G = GHS_JUMP_LATTICE_G;
+// a random-like graph's level 0 round 0 bucketed too (1) or by the a-run seeding + atomic min-edge +
+// k_win (0). Level 0 has no giant to reduce, so nearly every edge becomes two records in random
+// buckets, each a scattered 16-B store: R-MAT s26 round 0 2.56 ms bucketed vs 2.37 ms (s24 0.50
+// vs 0.52 ms), same box (profiles/r03/l0ab).
+#ifndef GHS_BK_RANDOM_L0
+#define GHS_BK_RANDOM_L0 0
+#endif
+constexpr bool BK_RANDOM_L0 = GHS_BK_RANDOM_L0;
 
+// giant != nullptr (a level's first round past level 0): the giant's candidates are reduced by
+// k_bucket into best[giant]; k_giant_hook then hooks it like k_bmin hooks a bucket's targets
 static void enqueue_bmin(ghs_solver *s, const uint32_t *a, const uint32_t *b, const uint64_t *k, SegView in,
-                         const unsigned long long *guard, uint64_t items) {
+                         const unsigned long long *guard, uint64_t items, const uint32_t *giant) {
   {
     KT(GHS_K_BUCKET, items);
-    k_bucket<<<BK_G, BK_T, 0, s->stream>>>(a, b, k, in, s->bk_bs, s->bk_nb, s->rec_a, s->rec_b, s->rec_k, s->bk_off,
-                                         guard);
+    k_bucket<<<BK_G, BK_T, 0, s->stream>>>(a, b, k, in, s->bk_bs, s->bk_nb, s->rec, s->bk_off, guard, giant, s->best);
   }
-  KT(GHS_K_BMIN, items);
-  if (s->bk_bs == 13)
-    k_bmin<13><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec_a, s->rec_b, s->rec_k, s->bk_off, in, s->par, s->best,
-                                                s->in_mst, guard);
-  else
-    k_bmin<14><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec_a, s->rec_b, s->rec_k, s->bk_off, in, s->par, s->best,
-                                                s->in_mst, guard);
+  {
+    KT(GHS_K_BMIN, items);
+    if (s->bk_bs == 13)
+      k_bmin<13><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard, giant);
+    else
+      k_bmin<14><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard, giant);
+  }
+  if (giant) k_giant_hook<<<1, 1, 0, s->stream>>>(giant, s->best, s->eu, s->ev, s->lab, s->par, s->in_mst, s->cnt + C_ERR);
 }
 
 static int enqueue_minedge(ghs_solver *s) {
@@ -3575,14 +3669,17 @@ static int enqueue_minedge(ghs_solver *s) {
   ArcBuf &O = s->buf[s->cur ^ 1];
   SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
   // GHS_OPT_BUCKETED (forced) runs every round bucketed: the test suite's coverage of them
-  s->round_bucketed = s->bucketed && ((s->level == 0 && s->nact >= BUCKET_MIN_ACTIVE) ||
-                                      (s->cfg.options & GHS_OPT_BUCKETED));
+  s->round_bucketed = s->bucketed && (s->bucket_first_only ? (s->level_round == 0 && (BK_RANDOM_L0 || s->level > 0))
+                                      : ((s->level == 0 && s->nact >= BUCKET_MIN_ACTIVE) ||
+                                         (BK_LEVEL_FIRST && s->level > 0 && s->level_round == 0) ||
+                                         (s->cfg.options & GHS_OPT_BUCKETED)));
   if (s->level_round == 0) {
     if (s->cur_arcs || !s->arcs_known) {
       const unsigned g = s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->ident_g) : s->ident_g;
       const uint64_t items = s->arcs_known ? s->cur_arcs : 0;
       if (s->round_bucketed) {
-        enqueue_bmin(s, I.src, I.dst, I.key, in, nullptr, items);  // the level's edges carry roots
+        // the level's edges carry roots (past level 0: resolved, and the giant is one of them)
+        enqueue_bmin(s, I.src, I.dst, I.key, in, nullptr, items, s->level > 0 ? s->giant : nullptr);
       } else {
         // level 0 (labels are the vertices): a-side runs seeded first, mostly by plain stores
         const bool seed = s->level == 0 && s->seed_runs;
@@ -3607,7 +3704,7 @@ static int enqueue_minedge(ghs_solver *s) {
     s->scan_buf = &O;
     flush_scan(s);
     SegView oin{O.seg_start, O.seg_prefix, s->cmp_g};
-    enqueue_bmin(s, O.src, O.dst, O.key, oin, guard, 0);
+    enqueue_bmin(s, O.src, O.dst, O.key, oin, guard, 0, nullptr);
   } else {
     // fixed grid: every one of the seg_g blocks writes its region's count
     KT(GHS_K_MINEDGE_COMPACT, 0);
@@ -3692,19 +3789,19 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
     // Stage 3, then the next active list (one launch each)
     // a bucketed round's hooks are counted by the jump: its grid is capped (one pair of
     // same-address atomics per block)
-    unsigned long long *acc = s->round_bucketed ? s->cnt + C_WEIGHT : nullptr;
+    unsigned long long *acc = s->round_bucketed ? s->hook_acc : nullptr;
     if (s->act_ident && (s->cfg.num_ranks <= 1 || s->level_dense)) {
       const uint32_t ni = s->level_dense ? (uint32_t)s->dense_n : s->n;
       KT(GHS_K_JUMP_IDENT, ni);
-      k_jump_ident<<<grid_for(((uint64_t)ni + 3) / 4, BLOCK, acc ? JUMP_COUNT_G : 16384), BLOCK, 0, s->stream>>>(
+      k_jump_ident<<<grid_for(((uint64_t)ni + 3) / 4, BLOCK, s->jump_ident_g), BLOCK, 0, s->stream>>>(
           ni, s->par, s->lab, s->best, s->flags, s->cnt + C_ERR, acc);
     } else {
       KT(GHS_K_JUMP, 0);
-      k_jump<<<acc ? gh : g, BLOCK, 0, s->stream>>>(act, d_nact, s->par, s->lab, s->best, s->flags, s->cnt + C_ERR, acc);
+      k_jump<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->par, s->lab, s->best, s->flags, s->cnt + C_ERR, acc);
     }
     GHS_HIP_CHECK(hipGetLastError());
     if (s->detail) record(s, 3);
-    if (int rc = select_lb(s, act, d_nact, bound, s->act[nb], act_count(s, nb), slot, seq)) return rc;
+    if (int rc = select_lb(s, act, d_nact, bound, s->act[nb], act_count(s, nb), slot, seq, acc != nullptr)) return rc;
   } else {
     if (s->scan_pending) flush_scan(s);
     if (int rc = select_lb(s, act, d_nact, 0, s->act[nb], act_count(s, nb), slot, seq)) return rc;
@@ -3783,14 +3880,22 @@ static void close_level(ghs_solver *s) {
 static int decide_bucketed(ghs_solver *s) {
   s->bucket_decided = true;
   s->bucketed = false;
+  s->bucket_first_only = false;
+  s->lattice = false;
+  s->jump_ident_g = 16384;
   const uint32_t opt = s->cfg.options;
-  if (s->cfg.num_ranks > 1 || !s->rec_a || (opt & GHS_OPT_NO_BUCKETED)) return GHS_OK;
+  if (s->cfg.num_ranks > 1 || !s->rec || (opt & GHS_OPT_NO_BUCKETED)) return GHS_OK;
   if (opt & GHS_OPT_BUCKETED) {
     s->bucketed = true;
     return GHS_OK;
   }
   if (int rc = plan_sync(s)) return rc;
-  s->bucketed = s->h_thr[PLAN_LOCAL] != 0;
+  s->lattice = s->h_thr[PLAN_LOCAL] != 0;
+  if (s->lattice) s->jump_ident_g = JUMP_LATTICE_G;
+  // lattice-like: level 0's rounds while >= BUCKET_MIN_ACTIVE fragments; otherwise (or forced by
+  // GHS_OPT_BUCKETED_FIRST) the first round of every level
+  s->bucketed = true;
+  s->bucket_first_only = !s->lattice || (opt & GHS_OPT_BUCKETED_FIRST);
   return GHS_OK;
 }
 
@@ -3932,7 +4037,7 @@ static int solver_begin(ghs_solver *s) {
   // only the solver's own edge range: it never writes a flag outside [e_lo, e_hi)
   if (s->e_hi > s->e_lo && (e = hipMemsetAsync(s->in_mst + s->e_lo, 0, s->e_hi - s->e_lo, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset in_mst: ") + hipGetErrorString(e));
   if ((e = hipMemsetAsync(s->lb_state, 0, LB_MAX_TILES * 8, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset select state: ") + hipGetErrorString(e));
-  k_init_counters<<<1, 64, 0, s->stream>>>(s->cnt, n);
+  k_init_counters<<<1, 64, 0, s->stream>>>(s->cnt, n, s->hook_acc);
   if ((e = hipGetLastError()) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("init kernels: ") + hipGetErrorString(e));
   s->level = 0;
   s->level_open = false;
@@ -4341,7 +4446,7 @@ int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *
     result->canon_edges = s->e_hi - s->e_lo;
     result->select_out = s->select_out;
     result->filter_out = s->filter_out;
-    result->pass_flags = s->bucketed ? 1u : 0u;
+    result->pass_flags = (s->bucketed ? 1u : 0u) | (s->lattice ? 2u : 0u);
   }
   return GHS_OK;
 }

@@ -68,7 +68,8 @@ typedef struct ghs_result {
   uint32_t rounds;            /* Boruvka rounds executed (all levels) */
   uint32_t num_stats;         /* entries filled in the stats array (<= GHS_MAX_ROUND_STATS) */
   uint32_t levels;            /* weight levels planned */
-  uint32_t pass_flags;        /* bit 0: the solve ran bucketed rounds (k_bucket / k_bmin) */
+  uint32_t pass_flags;        /* bit 0: the solve ran bucketed rounds (k_bucket / k_bmin);
+                                 bit 1: the plan's span sample found the graph lattice-like */
   double ms_total;            /* host wall time of the solve (device-resident input -> flags) */
   /* The two full streams over the canonical list (HIP events on the solve's stream). */
   float ms_select;            /* k_select: validation + level-0 split */
@@ -90,13 +91,16 @@ typedef struct ghs_result {
                                       instead of the single-writer run seeding */
 #define GHS_OPT_NO_DENSE 0x2u      /* several ranks: levels in vertex labels, not dense labels */
 #define GHS_OPT_BUCKETED 0x4u      /* one rank: every round bucketed, whatever the graph (default:
-                                      a lattice-like graph's rounds with >= 2^20 active fragments,
+                                      a lattice-like graph's level-0 rounds with >= 2^23 active
+                                      fragments, another graph's first round of every level —
                                       decided from the plan's span sample; tests force it) */
 #define GHS_OPT_NO_BUCKETED 0x8u   /* one rank: never bucketed rounds */
 #define GHS_OPT_DEBUG 0x10u        /* per-level sizes on stderr (diagnostic) */
 #define GHS_OPT_TIME_ROUNDS 0x20u  /* HIP events around the compacting min-edge launches
                                       (ghs_round_stats_t.ms_minedge; idles the GPU ~6 us each) */
 #define GHS_OPT_DETAIL 0x40u       /* HIP events around every stage of every round (diagnostic) */
+#define GHS_OPT_BUCKETED_FIRST 0x80u /* one rank: bucketed first rounds of every level (whatever the
+                                        graph), the other rounds unbucketed */
 typedef struct ghs_config {
   uint32_t max_levels;
   uint32_t num_ranks;         /* ranks sharing the solve (1 = single GPU; >1: identical rounds on

@@ -747,11 +747,14 @@ def test_cli_generator_and_multi_gpu_flag(tmp_path, torch_cuda):
 
 @pytest.mark.parametrize("graph", ["rmat", "rmat20", "ties", "forest", "readme", "grid", "grid-gradient"])
 @pytest.mark.parametrize("levels", [None, 1])
-def test_bucketed_rounds_vs_oracle(graph, levels, torch_cuda):
+@pytest.mark.parametrize("mode", ["every", "first"])
+def test_bucketed_rounds_vs_oracle(graph, levels, mode, torch_cuda):
     """Bucketed rounds (k_bucket groups the live edges by target bucket, k_bmin takes every
     fragment's minimum in LDS and hooks it; mutual pairs resolved by the jump) forced onto every
-    round of every graph kind (GHS_OPT_BUCKETED): the oracle's MSF and totals, the same flags as
-    the unbucketed rounds, and pass_flags says they ran."""
+    round of every graph kind (GHS_OPT_BUCKETED), or onto every level's first round
+    (GHS_OPT_BUCKETED_FIRST; past level 0 the giant fragment's candidates are reduced per block
+    and hooked by k_giant_hook): the oracle's MSF and totals, the same flags as the unbucketed
+    rounds, and pass_flags says they ran."""
     from distributed_ghs_implementation_amd import _native
     from distributed_ghs_implementation_amd.device import DeviceMST
     ora = _oracle()
@@ -759,7 +762,8 @@ def test_bucketed_rounds_vs_oracle(graph, levels, torch_cuda):
     g = e.to_host()
     ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
     kw = {} if levels is None else {"max_levels": levels}
-    on = DeviceMST(e, config=_native.make_config(options=_native.OPT_BUCKETED, **kw))
+    opt = _native.OPT_BUCKETED if mode == "every" else _native.OPT_BUCKETED_FIRST
+    on = DeviceMST(e, config=_native.make_config(options=opt, **kw))
     res, _ = on.run()
     assert res.pass_flags & 1
     assert np.array_equal(on.in_mst_host(), ref_in.astype(bool))
@@ -774,19 +778,25 @@ def test_bucketed_rounds_vs_oracle(graph, levels, torch_cuda):
 
 @pytest.mark.parametrize("k,mode", [(2048, 0), (2048, 1), (1500, 0)])
 def test_bucketed_auto_on_lattices(k, mode, torch_cuda):
-    """The default path picks bucketed rounds for lattices (the plan's span sample) and not for
-    R-MAT; grids large enough for bucketed rounds past the first (>= 2^20 active fragments) match
-    the oracle."""
+    """The default path finds lattices lattice-like (the plan's span sample: bucketed level-0
+    rounds) and R-MAT not (bucketed first rounds of every level, the giant excluded past level 0);
+    grids large enough for bucketed rounds past the first (>= 2^20 active fragments) and the
+    R-MAT graph match the oracle."""
     from distributed_ghs_implementation_amd.device import DeviceMST, generate_grid, generate_rmat
     ora = _oracle()
     e = generate_grid(k, mode)
     eng = DeviceMST(e)
     res, stats = eng.run()
-    assert res.pass_flags & 1
+    assert res.pass_flags & 1 and res.pass_flags & 2
     g = e.to_host()
     ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
     assert np.array_equal(eng.in_mst_host(), ref_in.astype(bool))
     assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k) and ref_k == g.n - 1
     r = generate_rmat(16, 16, seed=1, wseed=2)
-    res_r, _ = DeviceMST(r).run()
-    assert not res_r.pass_flags & 1
+    eng_r = DeviceMST(r)
+    res_r, _ = eng_r.run()
+    assert res_r.pass_flags & 1 and not res_r.pass_flags & 2
+    h = r.to_host()
+    ref_in, ref_tw, ref_k = ora.kruskal_c(h.n, h.u, h.v, h.w)
+    assert np.array_equal(eng_r.in_mst_host(), ref_in.astype(bool))
+    assert (res_r.total_weight, res_r.num_mst_edges) == (ref_tw, ref_k)

@@ -13,3 +13,5 @@ for g in "${GS[@]}"; do
   timeout -s KILL 120 rocprofv3 --pmc $g --kernel-include-regex "$KRE" -d "$OUT/p$i" -o run -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${BENCH_ARGS} > "$OUT/p$i.json" 2> "$OUT/p$i.err" || { echo "pmc pass $i ($g) failed"; tail -5 "$OUT/p$i.err"; exit 1; }
 done
 python3 tools/pmc_summary.py "$OUT" | tee "$OUT/pmc.md"
+# the raw rocprofv3 databases stay on the box (gpurun copies back at most 64 MiB)
+for d in "$OUT"/p*/; do rm -rf "$d"; done
