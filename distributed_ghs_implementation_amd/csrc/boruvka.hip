@@ -1300,14 +1300,29 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
 // ------------------------------------------------------------------------------------------
 constexpr uint32_t NSAMPLE = 2048;  // the giant holds >= ~10% of the vertices: 2048 samples find it
 constexpr uint32_t GIANT_SLOTS = 4096;
+// Hot fragments: the sample's most frequent roots (at most HOT_K, each hit by >= HOT_MIN samples,
+// i.e. holding >= ~n/1024 vertices), giant included. A bucketed level-first round reduces their
+// candidates per block (k_bucket) instead of filling one bucket each. Stored after the giant's
+// two words: giant[GIANT_HOT] = count, giant[GIANT_HOT + 1 ...] = labels.
+constexpr uint32_t HOT_K = 64;
+constexpr uint32_t HOT_MIN = 2;
+constexpr uint32_t GIANT_HOT = 4;
 __global__ __launch_bounds__(1024) void k_giant(uint32_t n, const uint32_t *lab, uint32_t *__restrict__ giant,
                                                 unsigned long long *__restrict__ err) {
   __shared__ uint32_t s_lab[GIANT_SLOTS];
   __shared__ uint32_t s_cnt[GIANT_SLOTS];
+  __shared__ uint32_t s_hist[NSAMPLE + 1];  // labels per sample count
+  __shared__ uint32_t s_wsum[1024 / WAVE];
+  __shared__ uint32_t s_thr, s_nhot;
   __shared__ unsigned long long s_best[1024 / WAVE];
   for (uint32_t i = threadIdx.x; i < GIANT_SLOTS; i += 1024) {
     s_lab[i] = LABEL_NONE;
     s_cnt[i] = 0;
+  }
+  for (uint32_t i = threadIdx.x; i <= NSAMPLE; i += 1024) s_hist[i] = 0;
+  if (threadIdx.x == 0) {
+    s_thr = NSAMPLE + 1;
+    s_nhot = 0;
   }
   __syncthreads();
   const uint32_t ns = n < NSAMPLE ? n : NSAMPLE;
@@ -1349,6 +1364,33 @@ __global__ __launch_bounds__(1024) void k_giant(uint32_t n, const uint32_t *lab,
     giant[0] = 0xffffffffu - (uint32_t)b;
     giant[1] = (uint32_t)(b >> 32);  // sampled vertices in the giant (stats / debug)
   }
+  // hot list: the smallest count threshold T >= HOT_MIN with at most HOT_K labels counted >= T
+  // (suffix sums of the count histogram: thread t holds counts 2048 - 2t and 2047 - 2t)
+  for (uint32_t i = threadIdx.x; i < GIANT_SLOTS; i += 1024)
+    if (s_lab[i] != LABEL_NONE) atomicAdd(&s_hist[s_cnt[i]], 1u);
+  __syncthreads();
+  const uint32_t c0 = NSAMPLE - 2 * threadIdx.x, c1 = c0 - 1;
+  const uint32_t h0 = s_hist[c0], h1 = s_hist[c1];
+  const uint32_t lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+  uint32_t incl = h0 + h1;
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const uint32_t o = __shfl_up(incl, d);
+    if ((int)lane >= d) incl += o;
+  }
+  if (lane == WAVE - 1) s_wsum[wid] = incl;
+  __syncthreads();
+  uint32_t before = incl - h0 - h1;
+  for (uint32_t w = 0; w < wid; ++w) before += s_wsum[w];
+  const uint32_t S0 = before + h0, S1 = S0 + h1, S2 = S1 + (c1 > 1 ? s_hist[c1 - 1] : 0u);  // S(c0), S(c1), S(c1 - 1)
+  if (c0 >= HOT_MIN && S0 <= HOT_K && (c0 == HOT_MIN || S1 > HOT_K)) s_thr = c0;
+  if (c1 >= HOT_MIN && S1 <= HOT_K && (c1 == HOT_MIN || S2 > HOT_K)) s_thr = c1;
+  __syncthreads();
+  const uint32_t T = s_thr;
+  for (uint32_t i = threadIdx.x; i < GIANT_SLOTS; i += 1024)
+    if (s_lab[i] != LABEL_NONE && s_cnt[i] >= T) giant[GIANT_HOT + 1 + atomicAdd(&s_nhot, 1u)] = s_lab[i];
+  __syncthreads();
+  if (threadIdx.x == 0) giant[GIANT_HOT] = s_nhot;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_resolve(uint32_t n, uint32_t *lab, const uint32_t *__restrict__ giant_ptr,
@@ -2005,6 +2047,28 @@ constexpr int BK_TILES = GHS_BK_TILES;  // k_bucket: 4-edge tiles per lane in fl
 // records starts at 2 * quota * g (an edge gives at most two records)
 __device__ __forceinline__ uint64_t bk_quota(uint64_t T) { return ((T + BK_G - 1) / BK_G + 3) & ~3ull; }
 
+// the hot fragments of a level-first round in an LDS hash (HOT_K labels in HOT_HASH slots)
+constexpr uint32_t HOT_HASH = 4 * HOT_K;
+constexpr uint32_t HOT_MARK = 0x80000000u;  // a record's hot end (labels < n <= 2^28)
+__device__ __forceinline__ uint32_t hot_slot(uint32_t x) { return (x * 0x9E3779B1u) >> 24; }
+static_assert(HOT_HASH == 256, "hot_slot yields 8 bits");
+__device__ __forceinline__ void hot_insert(uint32_t *s_hl, uint32_t *s_hi, uint32_t x, uint32_t idx) {
+  for (uint32_t h = hot_slot(x);; h = (h + 1) & (HOT_HASH - 1)) {
+    if (atomicCAS(&s_hl[h], LABEL_NONE, x) == LABEL_NONE) {
+      s_hi[h] = idx;
+      return;
+    }
+  }
+}
+// index of x among the hot labels, or -1 (the caller synchronised after the inserts)
+__device__ __forceinline__ int hot_find(const uint32_t *s_hl, const uint32_t *s_hi, uint32_t x) {
+  for (uint32_t h = hot_slot(x);; h = (h + 1) & (HOT_HASH - 1)) {
+    const uint32_t l = s_hl[h];
+    if (l == x) return (int)s_hi[h];
+    if (l == LABEL_NONE) return -1;
+  }
+}
+
 // exclusive scan over the NT threads of a block (NT / 64 waves); *total = the block's sum
 template <uint32_t NT>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t mine, uint32_t *s_wsum, uint32_t *total) {
@@ -2064,18 +2128,26 @@ __global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ sr
                                                  const uint64_t *__restrict__ key, SegView in, uint32_t bs,
                                                  uint32_t nb, uint4 *__restrict__ rec, uint32_t *__restrict__ O,
                                                  const unsigned long long *__restrict__ guard_nact,
-                                                 const uint32_t *__restrict__ giant_ptr, uint64_t *__restrict__ best) {
+                                                 const uint32_t *__restrict__ hot, uint64_t *__restrict__ best) {
   __shared__ uint32_t s_h[BK_MAX_B + 1];
   __shared__ uint32_t s_seg[2];
   __shared__ uint32_t s_wsum[BK_T / WAVE];
-  __shared__ unsigned long long s_gmin;
+  __shared__ uint32_t s_hl[HOT_HASH];          // hot label -> its index (linear probing)
+  __shared__ uint32_t s_hi[HOT_HASH];
+  __shared__ unsigned long long s_hmin[HOT_K];  // this block's minimum per hot fragment
   // a lookahead round past the level's end (<= 1 active fragment) writes empty regions
   const bool noop = guard_nact && *guard_nact <= 1;
-  // a level's first round past level 0: the giant fragment's candidates (most of the level's
-  // edges have one end in it) are reduced in LDS and leave the block as one atomicMin on
-  // best[giant] instead of filling one bucket that a single k_bmin workgroup would have to sweep
-  const uint32_t giant = giant_ptr ? *giant_ptr : LABEL_NONE;
-  if (threadIdx.x == 0) s_gmin = KEY_NONE;
+  // a level's first round past level 0: the hot fragments' candidates (the giant's: most of the
+  // level's edges) are reduced in LDS and leave the block as one atomicMin on best[] each, instead
+  // of filling one bucket each that a single k_bmin workgroup would have to sweep. A record's hot
+  // end is marked (bit 31: bucketed solves have n <= 2^28), so k_bmin never takes it as a target.
+  const uint32_t nhot = hot ? hot[0] : 0u;
+  const uint32_t hot0 = nhot ? hot[1] : LABEL_NONE;  // one hot fragment (R-MAT: the giant): a compare
+  for (uint32_t i = threadIdx.x; i < HOT_HASH; i += BK_T) s_hl[i] = LABEL_NONE;
+  if (threadIdx.x < HOT_K) s_hmin[threadIdx.x] = KEY_NONE;
+  __syncthreads();
+  if (threadIdx.x < nhot) hot_insert(s_hl, s_hi, hot[1 + threadIdx.x], threadIdx.x);
+  auto hidx = [&](uint32_t x) -> int { return nhot == 1 ? (x == hot0 ? 0 : -1) : hot_find(s_hl, s_hi, x); };
   const uint64_t T = noop ? 0 : in.prefix[in.nseg];
   const uint64_t Q = bk_quota(T);
   const uint64_t vb = Q * blockIdx.x;
@@ -2108,9 +2180,10 @@ __global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ sr
       for (int j = 0; j < 4; ++j) {
         const bool live = (v < ve) & (A[j] != LABEL_NONE);  // past the range / region padding
         const uint32_t ba = A[j] >> bs, bb = B[j] >> bs;
-        const bool ea = live && A[j] != giant;
+        const bool ea = live && (!nhot || hidx(A[j]) < 0);
+        const bool eb = live && (!nhot || hidx(B[j]) < 0) && (bb != ba || !ea);
         lds_bump<false>(s_h, ba, ea);
-        lds_bump<false>(s_h, bb, live && B[j] != giant && (bb != ba || !ea));
+        lds_bump<false>(s_h, bb, eb);
       }
     }
   }
@@ -2152,20 +2225,24 @@ __global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ sr
       for (int j = 0; j < 4; ++j) {
         const bool live = (v < ve) & (A[j] != LABEL_NONE);
         const uint32_t ba = A[j] >> bs, bb = B[j] >> bs;
-        const bool ea = live && A[j] != giant;
-        const bool eb = live && B[j] != giant && (bb != ba || !ea);
+        const int ha = (live && nhot) ? hidx(A[j]) : -1;
+        const int hb = (live && nhot) ? hidx(B[j]) : -1;
+        const bool ea = live && ha < 0;
+        const bool eb = live && hb < 0 && (bb != ba || !ea);
         const uint32_t pa = lds_bump<true>(s_h, ba, ea);
         const uint32_t pb = lds_bump<true>(s_h, bb, eb);
-        const uint4 r = make_uint4(A[j], B[j], (uint32_t)K[j], (uint32_t)(K[j] >> 32));
+        const uint4 r = make_uint4(A[j] | (ha >= 0 ? HOT_MARK : 0u), B[j] | (hb >= 0 ? HOT_MARK : 0u), (uint32_t)K[j],
+                                   (uint32_t)(K[j] >> 32));
         if (ea) rec[base + pa] = r;
         if (eb) rec[base + pb] = r;
-        if (live && (A[j] == giant || B[j] == giant) && K[j] < s_gmin) atomicMin(&s_gmin, (unsigned long long)K[j]);
+        if (ha >= 0 && K[j] < s_hmin[ha]) atomicMin(&s_hmin[ha], (unsigned long long)K[j]);
+        if (hb >= 0 && K[j] < s_hmin[hb]) atomicMin(&s_hmin[hb], (unsigned long long)K[j]);
       }
     }
   }
-  if (giant != LABEL_NONE) {
+  if (nhot) {
     __syncthreads();
-    if (threadIdx.x == 0 && s_gmin != KEY_NONE) flush_min(best, giant, s_gmin);
+    if (threadIdx.x < nhot && s_hmin[threadIdx.x] != KEY_NONE) flush_min(best, hot[1 + threadIdx.x], s_hmin[threadIdx.x]);
   }
 }
 
@@ -2176,13 +2253,15 @@ __global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ sr
 #define GHS_BM_ILP 8
 #endif
 constexpr int BM_ILP = GHS_BM_ILP;
+#ifndef GHS_BM_COMPRESS
+#define GHS_BM_COMPRESS 1
+#endif
 
 template <uint32_t BS>
 __global__ __launch_bounds__(BM_T) void k_bmin(const uint4 *__restrict__ rec, const uint32_t *__restrict__ O,
                                                SegView in, uint32_t *__restrict__ par, uint64_t *__restrict__ best,
                                                uint8_t *__restrict__ in_mst,
-                                               const unsigned long long *__restrict__ guard_nact,
-                                               const uint32_t *__restrict__ giant_ptr) {
+                                               const unsigned long long *__restrict__ guard_nact) {
   constexpr uint32_t SPAN = 1u << BS;
   __shared__ unsigned long long s_min[SPAN];
   __shared__ uint64_t s_pos[BK_G];  // non-empty run i: its first record's position
@@ -2192,9 +2271,6 @@ __global__ __launch_bounds__(BM_T) void k_bmin(const uint4 *__restrict__ rec, co
   const uint64_t T = noop ? 0 : in.prefix[in.nseg];
   const uint64_t R2 = 2 * bk_quota(T);  // record region stride
   const uint32_t t = blockIdx.x, tb = t << BS;
-  // the giant's candidates never became records (k_bucket reduced them), but a record of this
-  // bucket may still have the giant as its other end: it is no target here
-  const uint32_t giant = giant_ptr ? *giant_ptr : LABEL_NONE;
   uint32_t cnt = 0, st = 0;
   if (threadIdx.x < BK_G && !noop) {
     st = O[(uint64_t)t * BK_G + threadIdx.x];
@@ -2234,8 +2310,11 @@ __global__ __launch_bounds__(BM_T) void k_bmin(const uint4 *__restrict__ rec, co
     }
 #pragma unroll
     for (int j = 0; j < BM_ILP; ++j) {
-      if ((a[j] >> BS) == t && a[j] != giant) atomicMin(&s_min[a[j] - tb], k[j]);
-      if ((b[j] >> BS) == t && b[j] != giant) atomicMin(&s_min[b[j] - tb], k[j]);
+      // a hot end (HOT_MARK) is never this bucket's target. A plain read first (slots only
+      // decrease): records of a large fragment all target one slot, and same-address LDS atomics
+      // of a wave serialise
+      if ((a[j] >> BS) == t && k[j] < s_min[a[j] - tb]) atomicMin(&s_min[a[j] - tb], k[j]);
+      if ((b[j] >> BS) == t && k[j] < s_min[b[j] - tb]) atomicMin(&s_min[b[j] - tb], k[j]);
     }
   }
   __syncthreads();
@@ -2270,25 +2349,61 @@ __global__ __launch_bounds__(BM_T) void k_bmin(const uint4 *__restrict__ rec, co
     }
 #pragma unroll
     for (int j = 0; j < BM_ILP; ++j) {
-      if ((a[j] >> BS) == t && s_min[a[j] - tb] == k[j]) s_min[a[j] - tb] = ((uint64_t)b[j] << 32) | TAG;
-      if ((b[j] >> BS) == t && s_min[b[j] - tb] == k[j]) s_min[b[j] - tb] = ((uint64_t)a[j] << 32) | TAG;
+      if ((a[j] >> BS) == t && s_min[a[j] - tb] == k[j]) s_min[a[j] - tb] = ((uint64_t)(b[j] & ~HOT_MARK) << 32) | TAG;
+      if ((b[j] >> BS) == t && s_min[b[j] - tb] == k[j]) s_min[b[j] - tb] = ((uint64_t)(a[j] & ~HOT_MARK) << 32) | TAG;
     }
   }
   __syncthreads();
+  // Hook chains inside the bucket, compressed here so the jump walks fewer random steps (a
+  // lattice's horizontal hooks stay in their row's bucket). First a mutual pair inside the bucket
+  // keeps its smaller member as the root (its slot is cleared: par is not written, so it stays a
+  // root); pairs across buckets stay 2-cycles for the jump. Then pointer jumping over the tags:
+  // a slot whose parent lies in the bucket and hooked too takes the parent's parent — pointers
+  // only move to ancestors, so concurrent updates are safe. par then points at the first
+  // ancestor outside the bucket, the in-bucket root, or a member of a cross-bucket pair.
+  auto in_bucket = [&](uint64_t v) -> bool { return (uint32_t)v == (uint32_t)TAG && ((uint32_t)(v >> 32) >> BS) == t; };
+  if (GHS_BM_COMPRESS) {
+  for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) {
+    const uint64_t v = s_min[i];
+    if (!in_bucket(v)) continue;
+    const uint32_t o = (uint32_t)(v >> 32) - tb;
+    if (s_min[o] == (((uint64_t)(tb + i) << 32) | TAG) && i < o) s_min[i] = KEY_NONE;  // the pair's root
+  }
+  __syncthreads();
+  __shared__ int s_more;
+  for (int it = 0; it < (int)BS + 1; ++it) {
+    if (threadIdx.x == 0) s_more = 0;
+    __syncthreads();
+    int more = 0;
+    for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) {
+      const uint64_t v = s_min[i];
+      if (!in_bucket(v)) continue;
+      const uint64_t pv = s_min[(uint32_t)(v >> 32) - tb];
+      if ((uint32_t)pv == (uint32_t)TAG) {  // the parent hooked: skip it
+        s_min[i] = pv;
+        more |= in_bucket(pv) ? 1 : 0;
+      }
+    }
+    if (more) s_more = 1;
+    __syncthreads();
+    if (!s_more) break;
+  }
+  }  // GHS_BM_COMPRESS
   for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) {
     const uint64_t v = s_min[i];
     if ((uint32_t)v == (uint32_t)TAG) par[tb + i] = (uint32_t)(v >> 32);
   }
 }
 
-// The giant fragment's CONNECT in a bucketed level-first round: its minimum (reduced by k_bucket)
-// is edge eid; the level's labels are resolved roots, so the other end's label is one read. A
-// mutual pair stays a 2-cycle for the jump, as in k_bmin.
-__global__ void k_giant_hook(const uint32_t *__restrict__ giant_ptr, const uint64_t *__restrict__ best,
-                             const uint32_t *__restrict__ eu, const uint32_t *__restrict__ ev,
-                             const uint32_t *__restrict__ lab, uint32_t *__restrict__ par, uint8_t *__restrict__ in_mst,
-                             unsigned long long *__restrict__ err) {
-  const uint32_t g = *giant_ptr;
+// The hot fragments' CONNECT in a bucketed level-first round (one thread each): a fragment's
+// minimum (reduced by k_bucket) is edge eid; the level's labels are resolved roots, so the other
+// end's label is one read. A mutual pair stays a 2-cycle for the jump, as in k_bmin.
+__global__ void k_hot_hook(const uint32_t *__restrict__ hot, const uint64_t *__restrict__ best,
+                           const uint32_t *__restrict__ eu, const uint32_t *__restrict__ ev,
+                           const uint32_t *__restrict__ lab, uint32_t *__restrict__ par, uint8_t *__restrict__ in_mst,
+                           unsigned long long *__restrict__ err) {
+  if (threadIdx.x >= hot[0]) return;
+  const uint32_t g = hot[1 + threadIdx.x];
   const uint64_t k = best[g];
   if (k == KEY_NONE) return;
   const uint32_t eid = (uint32_t)k;
@@ -3157,7 +3272,7 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
   p = carve(((N + 1 + 63) / 64) * 8); if (s) s->flag_bits = (uint64_t *)p;
   p = carve(2 * NSAMPLE_MAX * 4); if (s) s->sample = (uint32_t *)p;  // weights + spans
   p = carve((PLAN_LOCAL + 1) * 8); if (s) s->d_thr = (uint64_t *)p;
-  p = carve(16); if (s) s->giant = (uint32_t *)p;
+  p = carve((GIANT_HOT + 1 + HOT_K) * 4); if (s) s->giant = (uint32_t *)p;  // giant, hot list
   p = carve(LB_MAX_TILES * 8); if (s) s->lb_state = (unsigned long long *)p;  // select tile granules
   p = carve(HOOK_SHARDS * SHARD_STRIDE * 8); if (s) s->hook_acc = (unsigned long long *)p;  // jump totals
   for (int b = 0; b < 2; ++b) {
@@ -3618,10 +3733,10 @@ static void flush_scan(ghs_solver *s) {
 #define GHS_BUCKET_MIN_ACTIVE (1u << 23)
 #endif
 constexpr uint64_t BUCKET_MIN_ACTIVE = GHS_BUCKET_MIN_ACTIVE;
-// a lattice-like solve also buckets the first round of every later level (the giant excluded).
-// Off: on the 16384^2 grid level 0 stops at the bond-percolation point, so level 1 has many large
-// fragments besides the sampled giant, each filling one bucket (k_bmin 7.1 -> 17.1 ms per solve,
-// step 43.1 -> 50.7 ms, same box).
+// a lattice-like solve also buckets the first round of every later level (the hot fragments
+// excluded). Off: on the 16384^2 grid level 0 stops at the bond-percolation point, so level 1 has
+// many large fragments below the hot list's size threshold, each filling one bucket (grid step
+// 43.6 -> 48.3 ms, gradient grid 18.8 -> 20.5 ms, same box; profiles/r03/hot2).
 #ifndef GHS_BK_LEVEL_FIRST
 #define GHS_BK_LEVEL_FIRST 0
 #endif
@@ -3644,22 +3759,23 @@ constexpr unsigned JUMP_LATTICE_G = GHS_JUMP_LATTICE_G;
 #endif
 constexpr bool BK_RANDOM_L0 = GHS_BK_RANDOM_L0;
 
-// giant != nullptr (a level's first round past level 0): the giant's candidates are reduced by
-// k_bucket into best[giant]; k_giant_hook then hooks it like k_bmin hooks a bucket's targets
+// hot != nullptr (a level's first round past level 0: the hot list of k_giant): the hot fragments'
+// candidates are reduced by k_bucket into best[]; k_hot_hook then hooks them like k_bmin hooks a
+// bucket's targets
 static void enqueue_bmin(ghs_solver *s, const uint32_t *a, const uint32_t *b, const uint64_t *k, SegView in,
-                         const unsigned long long *guard, uint64_t items, const uint32_t *giant) {
+                         const unsigned long long *guard, uint64_t items, const uint32_t *hot) {
   {
     KT(GHS_K_BUCKET, items);
-    k_bucket<<<BK_G, BK_T, 0, s->stream>>>(a, b, k, in, s->bk_bs, s->bk_nb, s->rec, s->bk_off, guard, giant, s->best);
+    k_bucket<<<BK_G, BK_T, 0, s->stream>>>(a, b, k, in, s->bk_bs, s->bk_nb, s->rec, s->bk_off, guard, hot, s->best);
   }
   {
     KT(GHS_K_BMIN, items);
     if (s->bk_bs == 13)
-      k_bmin<13><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard, giant);
+      k_bmin<13><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard);
     else
-      k_bmin<14><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard, giant);
+      k_bmin<14><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard);
   }
-  if (giant) k_giant_hook<<<1, 1, 0, s->stream>>>(giant, s->best, s->eu, s->ev, s->lab, s->par, s->in_mst, s->cnt + C_ERR);
+  if (hot) k_hot_hook<<<1, HOT_K, 0, s->stream>>>(hot, s->best, s->eu, s->ev, s->lab, s->par, s->in_mst, s->cnt + C_ERR);
 }
 
 static int enqueue_minedge(ghs_solver *s) {
@@ -3679,7 +3795,7 @@ static int enqueue_minedge(ghs_solver *s) {
       const uint64_t items = s->arcs_known ? s->cur_arcs : 0;
       if (s->round_bucketed) {
         // the level's edges carry roots (past level 0: resolved, and the giant is one of them)
-        enqueue_bmin(s, I.src, I.dst, I.key, in, nullptr, items, s->level > 0 ? s->giant : nullptr);
+        enqueue_bmin(s, I.src, I.dst, I.key, in, nullptr, items, s->level > 0 ? s->giant + GIANT_HOT : nullptr);
       } else {
         // level 0 (labels are the vertices): a-side runs seeded first, mostly by plain stores
         const bool seed = s->level == 0 && s->seed_runs;
