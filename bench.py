@@ -164,7 +164,8 @@ def stage1_roofline(records, stats):
 
 # profile name -> the PMC file's kernel-name prefix (rocprofv3 prints every template argument:
 # k_minedge<false, true, false>; any later template parameter still matches the prefix)
-PMC_NAMES = {"k_minedge<IDENT>": "k_minedge<true, false", "k_minedge<COMPACT>": "k_minedge<false, true"}
+PMC_NAMES = {"k_minedge<IDENT>": "k_minedge<true, false", "k_minedge<COMPACT>": "k_minedge<false, true",
+             "k_bmin": "k_bmin<"}
 
 
 def _pmc_match(name, key):
@@ -173,6 +174,8 @@ def _pmc_match(name, key):
     want = PMC_NAMES.get(name, name)
     if key == want:
         return True
+    if want.endswith("<"):  # any template arguments (k_bmin<13u>, k_bmin<14u>)
+        return key.startswith(want)
     return "<" in want and key.startswith(want) and key[len(want):len(want) + 1] in (">", ",")
 
 
