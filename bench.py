@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--no-scaling-base", action="store_true", help="N=1: skip the s26 strong-scaling point")
     ap.add_argument("--options", type=lambda x: int(x, 0), default=0,
                     help="ghs_config_t.options bits for N=1 (A/B of path options; 0 = the default path)")
+    ap.add_argument("--dedup-max", type=int, default=None,
+                    help="ghs_config_t.dedup_max for N=1 (parallel-edge filter at <= F fragments; A/B)")
     return ap.parse_args()
 
 
@@ -391,7 +393,9 @@ def main():
         eng = DistributedMST(edges, rank, world)
     else:
         from distributed_ghs_implementation_amd import _native
-        eng = DeviceMST(edges, config=_native.make_config(options=args.options) if args.options else None)
+        custom = args.options or args.dedup_max is not None
+        eng = DeviceMST(edges, config=_native.make_config(options=args.options, dedup_max=args.dedup_max)
+                        if custom else None)
     step = eng.run
     if world > 1:
         # N > 1: a step ends with the MSF on rank 0, as the reference's MPI run ends with

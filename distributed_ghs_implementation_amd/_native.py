@@ -40,6 +40,7 @@ EXPORTED_SYMBOLS = (
     "ghs_solver_unpack_best", "ghs_solver_best_slots",
     "ghs_solver_contract", "ghs_solver_finish", "ghs_solver_reset", "ghs_solver_cancel", "ghs_solver_destroy",
     "ghs_solver_hook_local", "ghs_solver_unpack_hook",
+    "ghs_solver_hook_slots", "ghs_solver_hook_owner", "ghs_solver_apply_hooks",
     "ghs_rmat_temp_bytes", "ghs_rmat_generate", "ghs_rmat_tuples", "ghs_grid_generate",
     "ghs_profile_enable", "ghs_profile_read", "ghs_kernel_name",
     "ghs_comm_unique_id", "ghs_comm_init", "ghs_comm_destroy", "ghs_solver_run", "ghs_mst_emulated",
@@ -95,7 +96,7 @@ class RoundStatsList(collections.abc.Sequence):
         return repr(list(self))
 
 
-ABI_VERSION = 5  # include/ghs_mst.h GHS_MST_ABI_VERSION
+ABI_VERSION = 6  # include/ghs_mst.h GHS_MST_ABI_VERSION
 
 
 class Result(ctypes.Structure):
@@ -157,6 +158,7 @@ OPT_DEBUG = 0x10
 OPT_TIME_ROUNDS = 0x20
 OPT_DETAIL = 0x40
 OPT_BUCKETED_FIRST = 0x80
+OPT_NO_WINDOW = 0x100
 
 
 class Config(ctypes.Structure):
@@ -241,6 +243,9 @@ def load():
             "ghs_solver_finish": (i32, [vp, P(Result), P(RoundStats)]),
             "ghs_solver_hook_local": (i32, [vp, vp, P(ctypes.c_uint64)]),
             "ghs_solver_unpack_hook": (i32, [vp, vp]),
+            "ghs_solver_hook_slots": (i32, [vp, u32, P(vp), P(u64)]),
+            "ghs_solver_hook_owner": (i32, [vp, u32, u64, vp]),
+            "ghs_solver_apply_hooks": (i32, [vp, vp]),
             "ghs_solver_reset": (i32, [vp]),
             "ghs_solver_cancel": (i32, [vp]),
             "ghs_solver_destroy": (i32, [vp]),

@@ -1099,6 +1099,86 @@ __global__ void k_unpack_hook(const uint32_t *__restrict__ act, const unsigned l
   }
 }
 
+// A dense level's opening round with the reduce-scatter protocol (the library loop, ABI 6): after a
+// MIN reduce-scatter of the best slots, rank r holds the final minimum of its slot range only; it
+// computes those fragments' hooks from the replicated canonical list (the edge's ends, their
+// level-open roots vlab, their dense labels) as pairs eid << 32 | other; an all-gather of the pairs
+// gives every rank every hook, and k_apply_pairs sets par (a mutual pair keeps its smaller member
+// as the root), the MSF flags of the rank's own edge range and the totals — 8 + 8 bytes per slot
+// on the wire instead of the all-reduce protocol's 2 x (8 + 4).
+__device__ __forceinline__ void add_totals_one(unsigned long long wsum, unsigned long long cnt,
+                                               unsigned long long *__restrict__ acc) {
+  __shared__ unsigned long long s_w[BLOCK / WAVE], s_c[BLOCK / WAVE];
+#pragma unroll
+  for (int d = WAVE / 2; d > 0; d >>= 1) {
+    wsum += __shfl_xor(wsum, d);
+    cnt += __shfl_xor(cnt, d);
+  }
+  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+  if (lane == 0) {
+    s_w[wid] = wsum;
+    s_c[wid] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long tw = 0, tc = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / WAVE; ++w) {
+      tw += s_w[w];
+      tc += s_c[w];
+    }
+    if (tc) {
+      atomicAdd(acc + 0, tw);
+      atomicAdd(acc + 1, tc);
+    }
+  }
+}
+
+__global__ void k_pad_slots(uint64_t *__restrict__ best, const unsigned long long *__restrict__ d_nact, uint64_t padded) {
+  const uint64_t i = *d_nact + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i < padded) best[i] = KEY_NONE;
+}
+
+__global__ void k_hook_owner(const uint64_t *__restrict__ best, uint64_t lo, uint64_t hi,
+                             const uint32_t *__restrict__ eu, const uint32_t *__restrict__ ev,
+                             const uint32_t *__restrict__ vlab, DenseRank dr, uint64_t *__restrict__ pairs,
+                             unsigned long long *__restrict__ err) {
+  for (uint64_t c = lo + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < hi; c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = best[c];
+    uint64_t out = KEY_NONE;
+    if (k != KEY_NONE) {
+      const uint32_t eid = (uint32_t)k;
+      const uint32_t da = dense_rank(dr, vlab[eu[eid]]), db = dense_rank(dr, vlab[ev[eid]]);
+      if (da != (uint32_t)c && db != (uint32_t)c) atomicOr(err, 2ull);  // the chosen edge must leave c
+      out = ((uint64_t)eid << 32) | (da == (uint32_t)c ? db : da);
+    }
+    pairs[c] = out;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_apply_pairs(const uint64_t *__restrict__ pairs,
+                                                       const unsigned long long *__restrict__ d_nact,
+                                                       const uint32_t *__restrict__ ew, uint32_t *__restrict__ par,
+                                                       uint64_t *__restrict__ best, uint8_t *__restrict__ in_mst,
+                                                       uint32_t own_lo, uint32_t own_hi,
+                                                       unsigned long long *__restrict__ acc) {
+  unsigned long long wsum = 0, cnt = 0;
+  const uint64_t nact = *d_nact;
+  for (uint64_t c = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; c < nact; c += (uint64_t)gridDim.x * BLOCK) {
+    const uint64_t p = pairs[c];
+    best[c] = p;  // every rank the same "had an outgoing edge" for the jump's keep test
+    if (p == KEY_NONE) continue;
+    const uint32_t o = (uint32_t)p, eid = (uint32_t)(p >> 32);
+    const bool mutual = (uint32_t)pairs[o] == (uint32_t)c;
+    if (mutual && (uint32_t)c < o) continue;  // the pair's root: its partner hooks over the edge
+    par[c] = o;
+    if (eid >= own_lo && eid < own_hi) in_mst[eid] = 1;
+    wsum += ew[eid];
+    cnt += 1;
+  }
+  add_totals_one(wsum, cnt, acc);
+}
+
 // ------------------------------------------------------------------------------------------
 // Stage 3: pointer jumping (INITIATE broadcast of the new fragment id), one fragment per thread
 // (every walk of the round in flight at once). Path splitting on par: concurrent compression
@@ -1615,8 +1695,13 @@ GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, cons
                                 const uint64_t *__restrict__ w_hi_p,
                                 uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst, uint64_t *__restrict__ okey,
                                 uint64_t *__restrict__ ostart, uint64_t *__restrict__ ocount,
-                                uint8_t *__restrict__ mark, unsigned long long *__restrict__ err) {
+                                uint8_t *__restrict__ mark, unsigned long long *__restrict__ err,
+                                const uint64_t *__restrict__ local_flag, uint32_t bs,
+                                unsigned long long *__restrict__ long_flag) {
   const uint64_t w_hi = *w_hi_p;  // the level plan lives on the device (k_plan)
+  // a lattice-like plan (k_plan's span sample): note any level-0 edge whose ends lie more than one
+  // bucket (2^bs ids) apart — the windowed round 0 (k_wmin) then falls back to k_bucket / k_bmin
+  const bool check_span = local_flag && *local_flag;
   __shared__ WaveStage s_stage[BLOCK / WAVE];
   // the wave index through readfirstlane: uniform in an SGPR, so every value derived from it
   // (the slice, its buffer descriptors) is scalar — a VGPR descriptor makes hipcc wrap each
@@ -1644,7 +1729,7 @@ GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, cons
   const uint32_t lane_off = lane * 16u;  // byte offset of the lane's tile in an iteration
   WaveOut wo;
   wo.pos = vb;
-  bool bad = false;
+  bool bad = false, far = false;
   uint4 ca = ld_b128(ru, lane_off), cb = ld_b128(rv, lane_off), cw = ld_b128(rw, lane_off);
   uint32_t cpa = ld_b32(ru, lane_off - 4), cpb = ld_b32(rv, lane_off - 4);
   // Every tile's loads are consumed at the END of the iteration that issued them (the empty asm
@@ -1680,6 +1765,7 @@ GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, cons
       pa = a[j];
       pb = b[j];
       out[j] = live[j] & ((uint64_t)w[j] < w_hi);
+      far |= out[j] & ((b[j] >> bs) > (a[j] >> bs) + 1u);
     }
     cpa = npa;
     cpb = npb;
@@ -1698,6 +1784,7 @@ GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, cons
     asm volatile("" ::"v"(ca.x), "v"(cb.x), "v"(cw.x), "v"(cpa), "v"(cpb));  // next tile landed (see above)
   }
   if (bad) atomicOr(err, 8ull);
+  if (check_span && __any(far) && lane == 0 && !*long_flag) atomicOr(long_flag, 1ull);
   wave_finish(s_stage[wid], wo, osrc, odst, okey, vb, vb < T, ostart, ocount, gw);
 }
 
@@ -2128,7 +2215,8 @@ __global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ sr
                                                  const uint64_t *__restrict__ key, SegView in, uint32_t bs,
                                                  uint32_t nb, uint4 *__restrict__ rec, uint32_t *__restrict__ O,
                                                  const unsigned long long *__restrict__ guard_nact,
-                                                 const uint32_t *__restrict__ hot, uint64_t *__restrict__ best) {
+                                                 const uint32_t *__restrict__ hot, uint64_t *__restrict__ best,
+                                                 const unsigned long long *__restrict__ only_if) {
   __shared__ uint32_t s_h[BK_MAX_B + 1];
   __shared__ uint32_t s_seg[2];
   __shared__ uint32_t s_wsum[BK_T / WAVE];
@@ -2141,6 +2229,7 @@ __global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ sr
   // level's edges) are reduced in LDS and leave the block as one atomicMin on best[] each, instead
   // of filling one bucket each that a single k_bmin workgroup would have to sweep. A record's hot
   // end is marked (bit 31: bucketed solves have n <= 2^28), so k_bmin never takes it as a target.
+  if (only_if && !*only_if) return;  // the windowed round ran (k_wmin)
   const uint32_t nhot = hot ? hot[0] : 0u;
   const uint32_t hot0 = nhot ? hot[1] : LABEL_NONE;  // one hot fragment (R-MAT: the giant): a compare
   for (uint32_t i = threadIdx.x; i < HOT_HASH; i += BK_T) s_hl[i] = LABEL_NONE;
@@ -2257,16 +2346,93 @@ constexpr int BM_ILP = GHS_BM_ILP;
 #define GHS_BM_COMPRESS 1
 #endif
 
+// The LDS core of a bucketed round (k_bmin over records, k_wmin over a window of the level's edge
+// list): `sweep(f)` calls f(a, b, key) for every candidate edge of bucket t (block-wide: every
+// thread calls it, each thread gets its share); s_min holds KEY_NONE in every slot.
+template <uint32_t BS, class Sweep>
+__device__ __forceinline__ void bucket_round(uint32_t t, unsigned long long *s_min, Sweep sweep,
+                                             uint32_t *__restrict__ par, uint64_t *__restrict__ best,
+                                             uint8_t *__restrict__ in_mst) {
+  constexpr uint32_t SPAN = 1u << BS;
+  const uint32_t tb = t << BS;
+  // sweep 1: every target's minimum. A hot end (HOT_MARK) is never this bucket's target. A plain
+  // read first (slots only decrease): records of a large fragment all target one slot, and
+  // same-address LDS atomics of a wave serialise
+  sweep([&](uint32_t a, uint32_t b, unsigned long long k) {
+    if ((a >> BS) == t && k < s_min[a - tb]) atomicMin(&s_min[a - tb], k);
+    if ((b >> BS) == t && k < s_min[b - tb]) atomicMin(&s_min[b - tb], k);
+  });
+  __syncthreads();
+  // the bucket's minima leave LDS in target order (one writer per target, consecutive lanes on
+  // consecutive slots): best[] and the MSF flag of every target's minimum edge. Scattered per-winner
+  // stores from the record sweep below measured 22 GB of HBM writes per 16384^2-grid solve for
+  // ~5 GB of payload (record order is not target order, and the records' stream evicts the
+  // partially written lines).
+  for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) {
+    const uint64_t v = s_min[i];
+    if (v != KEY_NONE) {
+      best[tb + i] = v;
+      in_mst[(uint32_t)v] = 1;
+    }
+  }
+  __syncthreads();
+  // winners: exactly one record per target holds its minimum (keys are unique); it replaces the
+  // slot by a tag carrying the other end (bit 31 set: a key's eid is < 2^31, so a tag never equals
+  // a key, and KEY_NONE's low word is not the tag's)
+  constexpr uint64_t TAG = 0x80000000ull;
+  sweep([&](uint32_t a, uint32_t b, unsigned long long k) {
+    if ((a >> BS) == t && s_min[a - tb] == k) s_min[a - tb] = ((uint64_t)(b & ~HOT_MARK) << 32) | TAG;
+    if ((b >> BS) == t && s_min[b - tb] == k) s_min[b - tb] = ((uint64_t)(a & ~HOT_MARK) << 32) | TAG;
+  });
+  __syncthreads();
+  // Hook chains inside the bucket, compressed here so the jump walks fewer random steps (a
+  // lattice's horizontal hooks stay in their row's bucket). First a mutual pair inside the bucket
+  // keeps its smaller member as the root (its slot is cleared: par is not written, so it stays a
+  // root); pairs across buckets stay 2-cycles for the jump. Then pointer jumping over the tags:
+  // a slot whose parent lies in the bucket and hooked too takes the parent's parent — pointers
+  // only move to ancestors, so concurrent updates are safe. par then points at the first
+  // ancestor outside the bucket, the in-bucket root, or a member of a cross-bucket pair.
+  auto in_bucket = [&](uint64_t v) -> bool { return (uint32_t)v == (uint32_t)TAG && ((uint32_t)(v >> 32) >> BS) == t; };
+  if (GHS_BM_COMPRESS) {
+  for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) {
+    const uint64_t v = s_min[i];
+    if (!in_bucket(v)) continue;
+    const uint32_t o = (uint32_t)(v >> 32) - tb;
+    if (s_min[o] == (((uint64_t)(tb + i) << 32) | TAG) && i < o) s_min[i] = KEY_NONE;  // the pair's root
+  }
+  __syncthreads();
+  for (int it = 0; it < (int)BS + 1; ++it) {
+    int more = 0;
+    for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) {
+      const uint64_t v = s_min[i];
+      if (!in_bucket(v)) continue;
+      const uint64_t pv = s_min[(uint32_t)(v >> 32) - tb];
+      if ((uint32_t)pv == (uint32_t)TAG) {  // the parent hooked: skip it
+        s_min[i] = pv;
+        more |= in_bucket(pv) ? 1 : 0;
+      }
+    }
+    if (!__syncthreads_or(more)) break;  // one barrier: every thread sees the same answer
+  }
+  }  // GHS_BM_COMPRESS
+  for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) {
+    const uint64_t v = s_min[i];
+    if ((uint32_t)v == (uint32_t)TAG) par[tb + i] = (uint32_t)(v >> 32);
+  }
+}
+
 template <uint32_t BS>
 __global__ __launch_bounds__(BM_T) void k_bmin(const uint4 *__restrict__ rec, const uint32_t *__restrict__ O,
                                                SegView in, uint32_t *__restrict__ par, uint64_t *__restrict__ best,
                                                uint8_t *__restrict__ in_mst,
-                                               const unsigned long long *__restrict__ guard_nact) {
+                                               const unsigned long long *__restrict__ guard_nact,
+                                               const unsigned long long *__restrict__ only_if) {
   constexpr uint32_t SPAN = 1u << BS;
   __shared__ unsigned long long s_min[SPAN];
   __shared__ uint64_t s_pos[BK_G];  // non-empty run i: its first record's position
   __shared__ uint32_t s_pre[BK_G];  // ... and its first index in the bucket's record order
   __shared__ uint32_t s_wsum[BM_T / WAVE];
+  if (only_if && !*only_if) return;  // the windowed round ran (k_wmin)
   const bool noop = guard_nact && *guard_nact <= 1;
   const uint64_t T = noop ? 0 : in.prefix[in.nseg];
   const uint64_t R2 = 2 * bk_quota(T);  // record region stride
@@ -2296,103 +2462,119 @@ __global__ __launch_bounds__(BM_T) void k_bmin(const uint4 *__restrict__ rec, co
     return s_pos[lo] + (r - s_pre[lo]);
   };
   constexpr uint32_t STEP = BM_T * BM_ILP;
-  for (uint32_t r0 = threadIdx.x; r0 < R; r0 += STEP) {
-    uint32_t a[BM_ILP], b[BM_ILP];
-    unsigned long long k[BM_ILP];
+  auto sweep = [&](auto f) {
+    for (uint32_t r0 = threadIdx.x; r0 < R; r0 += STEP) {
+      uint32_t a[BM_ILP], b[BM_ILP];
+      unsigned long long k[BM_ILP];
 #pragma unroll
-    for (int j = 0; j < BM_ILP; ++j) {
-      const uint32_t r = r0 + j * BM_T;
-      const uint64_t p = r < R ? locate(r) : 0;
-      const uint4 x = rec[p];
-      a[j] = r < R ? x.x : LABEL_NONE;
-      b[j] = r < R ? x.y : LABEL_NONE;
-      k[j] = r < R ? ((unsigned long long)x.w << 32 | x.z) : KEY_NONE;
-    }
+      for (int j = 0; j < BM_ILP; ++j) {
+        const uint32_t r = r0 + j * BM_T;
+        const uint64_t p = r < R ? locate(r) : 0;
+        const uint4 x = rec[p];
+        a[j] = r < R ? x.x : LABEL_NONE;
+        b[j] = r < R ? x.y : LABEL_NONE;
+        k[j] = r < R ? ((unsigned long long)x.w << 32 | x.z) : KEY_NONE;
+      }
 #pragma unroll
-    for (int j = 0; j < BM_ILP; ++j) {
-      // a hot end (HOT_MARK) is never this bucket's target. A plain read first (slots only
-      // decrease): records of a large fragment all target one slot, and same-address LDS atomics
-      // of a wave serialise
-      if ((a[j] >> BS) == t && k[j] < s_min[a[j] - tb]) atomicMin(&s_min[a[j] - tb], k[j]);
-      if ((b[j] >> BS) == t && k[j] < s_min[b[j] - tb]) atomicMin(&s_min[b[j] - tb], k[j]);
+      for (int j = 0; j < BM_ILP; ++j) f(a[j], b[j], k[j]);
     }
+  };
+  bucket_round<BS>(t, s_min, sweep, par, best, in_mst);
+}
+
+// ------------------------------------------------------------------------------------------
+// Windowed round 0 of level 0 on a lattice-like graph. The level-0 edge list is in canonical order
+// (a = u ascending) and its labels are the vertices, so bucket t's candidates are the edges with a
+// in bucket t and the edges with b in bucket t; when no level-0 edge has its ends more than one
+// bucket apart (k_select's span flag), all of them lie in the list's run of buckets t - 1 and t.
+// k_wmin reads that window straight from the edge list — no k_bucket records, no region search —
+// and runs the bucketed round's LDS core on it. Blocks take buckets in XCD order (workgroup i runs
+// on XCD i % 8): consecutive buckets run together on one XCD, so the row they share is read from
+// HBM about once. If the span flag is set, k_wstarts / k_wmin exit and the k_bucket / k_bmin
+// launches enqueued behind them run the round instead.
+// k_wstarts: start[t] = the first virtual index whose edge has a >= t << bs (start[nb] = total):
+// a search over the regions' first edges, then inside one region (its padding is at its end).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_wstarts(SegView in, const uint32_t *__restrict__ src, uint32_t bs, uint32_t nb,
+                                                 uint64_t *__restrict__ start,
+                                                 const unsigned long long *__restrict__ long_flag) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t > nb || *long_flag) return;
+  const uint64_t T = in.prefix[in.nseg];
+  const uint64_t x = (uint64_t)t << bs;
+  if (t == 0 || T == 0) {
+    start[t] = t == 0 ? 0 : T;
+    return;
   }
-  __syncthreads();
-  // the bucket's minima leave LDS in target order (one writer per target, consecutive lanes on
-  // consecutive slots): best[] and the MSF flag of every target's minimum edge. Scattered per-winner
-  // stores from the record sweep below measured 22 GB of HBM writes per 16384^2-grid solve for
-  // ~5 GB of payload (record order is not target order, and the records' stream evicts the
-  // partially written lines).
-  for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) {
-    const uint64_t v = s_min[i];
-    if (v != KEY_NONE) {
-      best[tb + i] = v;
-      in_mst[(uint32_t)v] = 1;
-    }
+  if (t == nb) {
+    start[t] = T;
+    return;
   }
+  // the first edge of region s (regions may be empty: the next non-empty one's, or "none")
+  auto first_a = [&](uint32_t r) -> uint64_t {
+    while (r < in.nseg && in.prefix[r + 1] == in.prefix[r]) ++r;
+    return r < in.nseg ? (uint64_t)src[in.start[r]] : ~0ull;
+  };
+  // last region whose first edge has a < x (region 0 if none)
+  uint32_t lo = 0, hi = in.nseg - 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (first_a(mid) < x) lo = mid; else hi = mid - 1;
+  }
+  const uint64_t p0 = in.start[lo], cnt = in.prefix[lo + 1] - in.prefix[lo];
+  uint64_t l = 0, h = cnt;  // first entry of region lo with a >= x (padding: LABEL_NONE >= x)
+  while (l < h) {
+    const uint64_t mid = (l + h) >> 1;
+    if ((uint64_t)src[p0 + mid] < x) l = mid + 1; else h = mid;
+  }
+  start[t] = in.prefix[lo] + l;  // l == cnt: the next region's first edge (a >= x by the search)
+}
+
+template <uint32_t BS>
+__global__ __launch_bounds__(BM_T) void k_wmin(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
+                                               const uint64_t *__restrict__ key, SegView in, uint32_t nb,
+                                               const uint64_t *__restrict__ start, uint32_t *__restrict__ par,
+                                               uint64_t *__restrict__ best, uint8_t *__restrict__ in_mst,
+                                               const unsigned long long *__restrict__ long_flag) {
+  constexpr uint32_t SPAN = 1u << BS;
+  __shared__ unsigned long long s_min[SPAN];
+  __shared__ uint32_t s_seg[2];
+  const uint32_t per = (nb + 7) / 8;  // XCD order
+  const uint32_t t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (t >= nb || *long_flag) return;
+  const uint64_t wlo = start[t ? t - 1 : 0], whi = start[t + 1 < nb ? t + 1 : nb];
+  if (whi <= wlo) return;  // block-uniform: no edge with an end in this bucket
+  if (threadIdx.x == 0) {
+    s_seg[0] = seg_find(in.prefix, 0, in.nseg - 1, wlo);
+    s_seg[1] = seg_find(in.prefix, 0, in.nseg - 1, whi - 1);
+  }
+  for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) s_min[i] = KEY_NONE;
   __syncthreads();
-  // winners: exactly one record per target holds its minimum (keys are unique); it replaces the
-  // slot by a tag carrying the other end (bit 31 set: a key's eid is < 2^31, so a tag never equals
-  // a key, and KEY_NONE's low word is not the tag's)
-  constexpr uint64_t TAG = 0x80000000ull;
-  for (uint32_t r0 = threadIdx.x; r0 < R; r0 += STEP) {
-    uint32_t a[BM_ILP], b[BM_ILP];
-    unsigned long long k[BM_ILP];
+  const uint32_t slo = s_seg[0], shi = s_seg[1];
+  auto sweep = [&](auto f) {
+    for (uint32_t sg = slo; sg <= shi; ++sg) {  // the window's part of each region it touches
+      const uint64_t v0 = wlo > in.prefix[sg] ? wlo : in.prefix[sg];
+      const uint64_t v1 = whi < in.prefix[sg + 1] ? whi : in.prefix[sg + 1];
+      const uint64_t p0 = in.start[sg] + (v0 - in.prefix[sg]), len = v1 > v0 ? v1 - v0 : 0;
+      constexpr uint32_t STEP = BM_T * BM_ILP;
+      for (uint64_t r0 = threadIdx.x; r0 < len; r0 += STEP) {
+        uint32_t a[BM_ILP], b[BM_ILP];
+        unsigned long long k[BM_ILP];
 #pragma unroll
-    for (int j = 0; j < BM_ILP; ++j) {
-      const uint32_t r = r0 + j * BM_T;
-      const uint64_t p = r < R ? locate(r) : 0;
-      const uint4 x = rec[p];
-      a[j] = r < R ? x.x : LABEL_NONE;
-      b[j] = r < R ? x.y : LABEL_NONE;
-      k[j] = r < R ? ((unsigned long long)x.w << 32 | x.z) : KEY_NONE;
-    }
+        for (int j = 0; j < BM_ILP; ++j) {
+          const uint64_t r = r0 + (uint64_t)j * BM_T;
+          const uint64_t p = r < len ? p0 + r : p0;
+          a[j] = src[p];
+          b[j] = dst[p];
+          k[j] = key[p];
+          if (r >= len) a[j] = b[j] = LABEL_NONE;  // padding entries carry a == LABEL_NONE too
+        }
 #pragma unroll
-    for (int j = 0; j < BM_ILP; ++j) {
-      if ((a[j] >> BS) == t && s_min[a[j] - tb] == k[j]) s_min[a[j] - tb] = ((uint64_t)(b[j] & ~HOT_MARK) << 32) | TAG;
-      if ((b[j] >> BS) == t && s_min[b[j] - tb] == k[j]) s_min[b[j] - tb] = ((uint64_t)(a[j] & ~HOT_MARK) << 32) | TAG;
-    }
-  }
-  __syncthreads();
-  // Hook chains inside the bucket, compressed here so the jump walks fewer random steps (a
-  // lattice's horizontal hooks stay in their row's bucket). First a mutual pair inside the bucket
-  // keeps its smaller member as the root (its slot is cleared: par is not written, so it stays a
-  // root); pairs across buckets stay 2-cycles for the jump. Then pointer jumping over the tags:
-  // a slot whose parent lies in the bucket and hooked too takes the parent's parent — pointers
-  // only move to ancestors, so concurrent updates are safe. par then points at the first
-  // ancestor outside the bucket, the in-bucket root, or a member of a cross-bucket pair.
-  auto in_bucket = [&](uint64_t v) -> bool { return (uint32_t)v == (uint32_t)TAG && ((uint32_t)(v >> 32) >> BS) == t; };
-  if (GHS_BM_COMPRESS) {
-  for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) {
-    const uint64_t v = s_min[i];
-    if (!in_bucket(v)) continue;
-    const uint32_t o = (uint32_t)(v >> 32) - tb;
-    if (s_min[o] == (((uint64_t)(tb + i) << 32) | TAG) && i < o) s_min[i] = KEY_NONE;  // the pair's root
-  }
-  __syncthreads();
-  __shared__ int s_more;
-  for (int it = 0; it < (int)BS + 1; ++it) {
-    if (threadIdx.x == 0) s_more = 0;
-    __syncthreads();
-    int more = 0;
-    for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) {
-      const uint64_t v = s_min[i];
-      if (!in_bucket(v)) continue;
-      const uint64_t pv = s_min[(uint32_t)(v >> 32) - tb];
-      if ((uint32_t)pv == (uint32_t)TAG) {  // the parent hooked: skip it
-        s_min[i] = pv;
-        more |= in_bucket(pv) ? 1 : 0;
+        for (int j = 0; j < BM_ILP; ++j) f(a[j], a[j] == LABEL_NONE ? LABEL_NONE : b[j], k[j]);
       }
     }
-    if (more) s_more = 1;
-    __syncthreads();
-    if (!s_more) break;
-  }
-  }  // GHS_BM_COMPRESS
-  for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) {
-    const uint64_t v = s_min[i];
-    if ((uint32_t)v == (uint32_t)TAG) par[tb + i] = (uint32_t)(v >> 32);
-  }
+  };
+  bucket_round<BS>(t, s_min, sweep, par, best, in_mst);
 }
 
 // The hot fragments' CONNECT in a bucketed level-first round (one thread each): a fragment's
@@ -2901,6 +3083,7 @@ enum : int {
   C_N = 6,        // n (the count of the identity active list)
   C_NDENSE = 7,   // fragments of a dense level (several ranks): the count of its identity list
   C_ACT = 8,      // [8], [9]: lengths of the active lists act[0], act[1]
+  C_LONG = 10,    // a level-0 edge spans more than one bucket (k_select, lattice-like plans)
   C_COUNT = 16
 };
 static_assert(C_WEIGHT == 2 && C_EDGES == 3 && C_ERR == 4 && C_PENDING == 5, "write_report reads the counters by index");
@@ -3066,6 +3249,8 @@ struct ghs_solver {
   // bucketed rounds (single rank, lattice-like graphs; k_bucket / k_bmin): the record buffers,
   // the offsets table, the bucket geometry, and the per-solve / per-round decisions
   uint4 *rec = nullptr;         // records (a, b, key): 16 B each
+  uint64_t *wstart = nullptr;   // windowed round 0: each bucket's first edge (nb + 1)
+  bool windowed = true;         // level 0 round 0 of a lattice-like solve windowed (k_wmin)
   uint32_t *bk_off = nullptr;
   uint32_t bk_bs = 13, bk_nb = 0;
   bool bucketed = false;        // this solve runs bucketed rounds (decided once the plan landed)
@@ -3123,7 +3308,7 @@ static uint32_t g_prof_next_id = 0;
 static const char *const KERNEL_NAMES[GHS_K_COUNT] = {
     "k_select", "k_filter", "k_level_pass", "k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>",
     "k_win", "k_hook", "k_jump_ident", "k_jump", "k_select_lb", "k_resolve", "k_giant", "k_scan_counts",
-    "k_plan", "k_init", "k_pack_best", "k_unpack_best", "k_round_report", "k_pack_hook", "k_unpack_hook", "k_dense", "k_flag_bits", "k_bucket", "k_bmin"};
+    "k_plan", "k_init", "k_pack_best", "k_unpack_best", "k_round_report", "k_pack_hook", "k_unpack_hook", "k_dense", "k_flag_bits", "k_bucket", "k_bmin", "k_wstarts", "k_wmin", "k_hot_hook"};
 
 struct KtScope {
   ghs_solver *s;
@@ -3260,7 +3445,7 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
   if (local_edges < m) {  // a rank of a multi-rank solve: the dense-level arrays
     p = carve(N * 4); if (s) s->dlab = (uint32_t *)p;
     p = carve(N * 4); if (s) s->dpar = (uint32_t *)p;
-    p = carve(N * 8); if (s) s->dbest = (uint64_t *)p;
+    p = carve((N + 64) * 8); if (s) s->dbest = (uint64_t *)p;  // + padding of the reduce-scatter slots
     const size_t W = (N + 63) / 64;
     p = carve(W * 8); if (s) s->drank_bits = (uint64_t *)p;
     p = carve(W * 4); if (s) s->drank_wpre = (uint32_t *)p;
@@ -3299,6 +3484,7 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
     const uint64_t rc = 2 * cap + 8 * BK_G;
     p = carve(rc * 16); if (s) s->rec = (uint4 *)p;
     p = carve((size_t)(nb + 1) * BK_G * 4); if (s) s->bk_off = (uint32_t *)p;
+    p = carve((size_t)(nb + 1) * 8); if (s) s->wstart = (uint64_t *)p;
     if (s) {
       s->bk_bs = bs;
       s->bk_nb = nb;
@@ -3494,7 +3680,8 @@ static int open_level(ghs_solver *s, bool async_open = false) {
       {
         KT(GHS_K_SELECT, TC);
         k_select<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range + 1, Y.src, Y.dst, Y.key,
-                                      Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR);
+                                      Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR,
+                                      s->wstart ? s->d_thr + PLAN_LOCAL : nullptr, s->bk_bs, s->cnt + C_LONG);
       }
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[1], st));
       GHS_HIP_CHECK(hipGetLastError());
@@ -3763,19 +3950,24 @@ constexpr bool BK_RANDOM_L0 = GHS_BK_RANDOM_L0;
 // candidates are reduced by k_bucket into best[]; k_hot_hook then hooks them like k_bmin hooks a
 // bucket's targets
 static void enqueue_bmin(ghs_solver *s, const uint32_t *a, const uint32_t *b, const uint64_t *k, SegView in,
-                         const unsigned long long *guard, uint64_t items, const uint32_t *hot) {
+                         const unsigned long long *guard, uint64_t items, const uint32_t *hot,
+                         const unsigned long long *only_if = nullptr) {
   {
     KT(GHS_K_BUCKET, items);
-    k_bucket<<<BK_G, BK_T, 0, s->stream>>>(a, b, k, in, s->bk_bs, s->bk_nb, s->rec, s->bk_off, guard, hot, s->best);
+    k_bucket<<<BK_G, BK_T, 0, s->stream>>>(a, b, k, in, s->bk_bs, s->bk_nb, s->rec, s->bk_off, guard, hot, s->best,
+                                         only_if);
   }
   {
     KT(GHS_K_BMIN, items);
     if (s->bk_bs == 13)
-      k_bmin<13><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard);
+      k_bmin<13><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard, only_if);
     else
-      k_bmin<14><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard);
+      k_bmin<14><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard, only_if);
   }
-  if (hot) k_hot_hook<<<1, HOT_K, 0, s->stream>>>(hot, s->best, s->eu, s->ev, s->lab, s->par, s->in_mst, s->cnt + C_ERR);
+  if (hot) {
+    KT(GHS_K_HOT_HOOK, 0);
+    k_hot_hook<<<1, HOT_K, 0, s->stream>>>(hot, s->best, s->eu, s->ev, s->lab, s->par, s->in_mst, s->cnt + C_ERR);
+  }
 }
 
 static int enqueue_minedge(ghs_solver *s) {
@@ -3793,7 +3985,26 @@ static int enqueue_minedge(ghs_solver *s) {
     if (s->cur_arcs || !s->arcs_known) {
       const unsigned g = s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->ident_g) : s->ident_g;
       const uint64_t items = s->arcs_known ? s->cur_arcs : 0;
-      if (s->round_bucketed) {
+      if (s->round_bucketed && s->level == 0 && s->lattice && s->windowed) {
+        // windowed round 0 (k_wmin over the edge list); k_bucket / k_bmin run instead only if a
+        // level-0 edge spans more than one bucket (k_select's flag)
+        const unsigned long long *far = s->cnt + C_LONG;
+        {
+          KT(GHS_K_WSTARTS, s->bk_nb);
+          k_wstarts<<<(s->bk_nb + 1 + 255) / 256, 256, 0, s->stream>>>(in, I.src, s->bk_bs, s->bk_nb, s->wstart, far);
+        }
+        {
+          KT(GHS_K_WMIN, items);
+          const unsigned wg = 8 * ((s->bk_nb + 7) / 8);
+          if (s->bk_bs == 13)
+            k_wmin<13><<<wg, BM_T, 0, s->stream>>>(I.src, I.dst, I.key, in, s->bk_nb, s->wstart, s->par, s->best,
+                                                  s->in_mst, far);
+          else
+            k_wmin<14><<<wg, BM_T, 0, s->stream>>>(I.src, I.dst, I.key, in, s->bk_nb, s->wstart, s->par, s->best,
+                                                  s->in_mst, far);
+        }
+        enqueue_bmin(s, I.src, I.dst, I.key, in, nullptr, items, nullptr, far);
+      } else if (s->round_bucketed) {
         // the level's edges carry roots (past level 0: resolved, and the giant is one of them)
         enqueue_bmin(s, I.src, I.dst, I.key, in, nullptr, items, s->level > 0 ? s->giant + GIANT_HOT : nullptr);
       } else {
@@ -3820,7 +4031,7 @@ static int enqueue_minedge(ghs_solver *s) {
     s->scan_buf = &O;
     flush_scan(s);
     SegView oin{O.seg_start, O.seg_prefix, s->cmp_g};
-    enqueue_bmin(s, O.src, O.dst, O.key, oin, guard, 0, nullptr);
+    enqueue_bmin(s, O.src, O.dst, O.key, oin, guard, 0, nullptr, nullptr);
   } else {
     // fixed grid: every one of the seg_g blocks writes its region's count
     KT(GHS_K_MINEDGE_COMPACT, 0);
@@ -4193,6 +4404,7 @@ static int solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint
   s->detail = (opt & GHS_OPT_DETAIL) != 0;
   s->time_rounds = (opt & GHS_OPT_TIME_ROUNDS) != 0;
   s->seed_runs = (opt & GHS_OPT_NO_SEED_RUNS) == 0;
+  s->windowed = (opt & GHS_OPT_NO_WINDOW) == 0;
   s->dedup_max = s->cfg.dedup_max;
   {
     std::lock_guard<std::mutex> lock(g_prof_mutex);
@@ -4397,6 +4609,53 @@ int ghs_solver_unpack_hook(ghs_solver_t *s, const int32_t *d_dense) {
     KT(GHS_K_UNPACK_HOOK, s->nact);
     k_unpack_hook<<<grid_for(s->nact, BLOCK, HOOK_G), BLOCK, 0, s->stream>>>(act, cur_act_count(s), d_dense, s->best,
                                                                             s->par, s->cnt + C_WEIGHT);
+    GHS_HIP_CHECK(hipGetLastError());
+  }
+  s->hooked = true;
+  return GHS_OK;
+}
+
+int ghs_solver_hook_slots(ghs_solver_t *s, uint32_t nranks, uint64_t **d_slots, uint64_t *padded) {
+  if (!s || !d_slots || !padded || nranks == 0) GHS_FAIL(GHS_E_ARG, "solver/slots/padded is NULL or nranks == 0");
+  *d_slots = nullptr;
+  *padded = 0;
+  if (s->phase != 1) GHS_FAIL(GHS_E_STATE, "hook_slots must follow minedge");
+  // a dense level's opening round (its slots are best itself, in dense-label order)
+  if (s->cfg.num_ranks <= 1 || s->level_round != 0 || !s->nact || s->hooked || !s->act_ident || !s->level_dense)
+    return GHS_OK;
+  const uint64_t S = (s->nact + nranks - 1) / nranks * nranks;
+  if (S > s->nact) {
+    k_pad_slots<<<(unsigned)((S - s->nact + 255) / 256 + 1), 256, 0, s->stream>>>(s->best, cur_act_count(s), S);
+    GHS_HIP_CHECK(hipGetLastError());
+  }
+  *d_slots = s->best;
+  *padded = S;
+  return GHS_OK;
+}
+
+int ghs_solver_hook_owner(ghs_solver_t *s, uint32_t rank, uint64_t per, uint64_t *d_pairs) {
+  if (!s || !d_pairs) GHS_FAIL(GHS_E_ARG, "solver/pairs is NULL");
+  if (s->phase != 1 || !s->level_dense || !s->act_ident || s->level_round != 0 || s->hooked)
+    GHS_FAIL(GHS_E_STATE, "hook_owner must follow hook_slots and the reduce-scatter");
+  const uint64_t lo = (uint64_t)rank * per, hi = lo + per;
+  if (per) {
+    KT(GHS_K_PACK_HOOK, per);
+    k_hook_owner<<<grid_for(per, 256, 16384), 256, 0, s->stream>>>(s->best, lo, hi, s->eu, s->ev, s->vlab,
+                                                                   dense_rank_of(s), d_pairs, s->cnt + C_ERR);
+    GHS_HIP_CHECK(hipGetLastError());
+  }
+  return GHS_OK;
+}
+
+int ghs_solver_apply_hooks(ghs_solver_t *s, const uint64_t *d_pairs) {
+  if (!s || (s->nact && !d_pairs)) GHS_FAIL(GHS_E_ARG, "solver/pairs is NULL");
+  if (s->phase != 1 || !s->level_dense || !s->act_ident || s->level_round != 0 || s->hooked)
+    GHS_FAIL(GHS_E_STATE, "apply_hooks must follow hook_owner and the all-gather");
+  if (s->nact) {
+    KT(GHS_K_UNPACK_HOOK, s->nact);
+    k_apply_pairs<<<grid_for(s->nact, BLOCK, HOOK_G), BLOCK, 0, s->stream>>>(
+        d_pairs, cur_act_count(s), s->ew, s->par, s->best, s->in_mst, (uint32_t)s->e_lo, (uint32_t)s->e_hi,
+        s->cnt + C_WEIGHT);
     GHS_HIP_CHECK(hipGetLastError());
   }
   s->hooked = true;

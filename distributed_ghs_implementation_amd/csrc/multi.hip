@@ -14,8 +14,11 @@
 // mpiexec -n <vertices> ranks exchanging pickled point-to-point messages, then Barrier + gather of
 // the BRANCH edges to rank 0, :760-779) with one rank per GPU and these collectives:
 //   level open    flags (n fragment bits + error bit)     all-gather, OR on the device
-//   every round   best keys of the active fragments       all-reduce MIN  (int64, key ^ 2^63)
-//   level round 0 owner-computed hooks (par ^ fragment)  all-reduce MAX  (int32)
+//   level round 0 best keys of the dense fragments        reduce-scatter MIN (uint64, in place)
+//                 the slot owners' hooks (eid, other)     all-gather (uint64)
+//   later rounds  best keys of the active fragments       all-reduce MIN  (int64, key ^ 2^63)
+//   (the stepwise protocol's level round 0 — all-reduce MIN of the slots, owner-computed hooks
+//   as int32 MAX all-reduce — stays available to callers driving their own collectives)
 // Each rank holds the replicated canonical list and owns the contiguous canonical-edge range
 // [r*m/N, (r+1)*m/N) (4-aligned) — the same partition as the Python driver (device.py edge_range).
 // Every rank writes the MSF flags of its own range only; the result is their concatenation.
@@ -96,11 +99,13 @@ struct ghs_comm {
   ghs::EmuGroup *emu = nullptr;
   int32_t *agree = nullptr;      // device int of the setup agreement (RCCL)
   int *group_cancel = nullptr;   // ghs_mst_multi: set by the first failing rank of the clique
+  bool rs_hooks = true;          // dense level-opening rounds: reduce-scatter protocol (ABI 6)
   // device scratch of the loop (grown on demand)
   int64_t *dense = nullptr;
   int32_t *hook = nullptr;
   uint64_t *gathered = nullptr;
-  size_t dense_cap = 0, gathered_cap = 0;
+  uint64_t *pairs = nullptr;     // the reduce-scatter protocol's hook pairs (n + 64 slots)
+  size_t dense_cap = 0, gathered_cap = 0, pairs_cap = 0;
 };
 
 namespace {
@@ -127,6 +132,13 @@ int comm_scratch(ghs_comm *c, uint32_t n) {
     GHS_HIP_CHECK(hipMalloc((void **)&c->hook, slots * 4));
     c->dense_cap = slots;
   }
+  if (c->pairs_cap < slots + 64) {
+    if (c->pairs) (void)hipFree(c->pairs);
+    c->pairs = nullptr;
+    c->pairs_cap = 0;
+    GHS_HIP_CHECK(hipMalloc((void **)&c->pairs, (slots + 64) * 8));
+    c->pairs_cap = slots + 64;
+  }
   if (c->gathered_cap < words * c->nranks) {
     if (c->gathered) (void)hipFree(c->gathered);
     c->gathered = nullptr;
@@ -145,10 +157,30 @@ int coll_allgather_u64(ghs_comm *c, const uint64_t *send, uint64_t *recv, size_t
   GHS_HIP_CHECK(hipStreamSynchronize(st));
   c->emu->ptrs[c->rank] = send;
   COMM_BARRIER(c);
-  for (int r = 0; r < c->nranks; ++r)
-    GHS_HIP_CHECK(hipMemcpyAsync(recv + (size_t)r * count, c->emu->ptrs[r], count * 8, hipMemcpyDeviceToDevice, st));
+  for (int r = 0; r < c->nranks; ++r)  // (an in-place gather's own slice is already there)
+    if (recv + (size_t)r * count != c->emu->ptrs[r] && count)
+      GHS_HIP_CHECK(hipMemcpyAsync(recv + (size_t)r * count, c->emu->ptrs[r], count * 8, hipMemcpyDeviceToDevice, st));
   GHS_HIP_CHECK(hipStreamSynchronize(st));
   COMM_BARRIER(c);  // every rank has read every send buffer
+  return GHS_OK;
+}
+
+// in-place MIN reduce-scatter over uint64: buf holds nranks x per slots; rank r keeps slice r
+int coll_reducescatter_min_u64(ghs_comm *c, uint64_t *buf, size_t per, hipStream_t st) {
+  if (c->nccl) {
+    COMM_NCCL(ncclReduceScatter(buf, buf + (size_t)c->rank * per, per, ncclUint64, ncclMin, c->nccl, st));
+    return GHS_OK;
+  }
+  GHS_HIP_CHECK(hipStreamSynchronize(st));
+  c->emu->ptrs[c->rank] = buf;
+  COMM_BARRIER(c);
+  uint64_t *mine = buf + (size_t)c->rank * per;  // every rank reduces its own slice from the others
+  for (int r = 0; r < c->nranks; ++r)
+    if (r != c->rank && per)
+      k_emu_min_u64<<<emu_grid(per), 256, 0, st>>>(mine, (const uint64_t *)c->emu->ptrs[r] + (size_t)c->rank * per, per);
+  GHS_HIP_CHECK(hipGetLastError());
+  GHS_HIP_CHECK(hipStreamSynchronize(st));
+  COMM_BARRIER(c);  // every rank has read every buffer
   return GHS_OK;
 }
 
@@ -259,7 +291,17 @@ int run_loop(ghs_solver_t *s, ghs_comm *c) {
       rc = ghs_solver_minedge(s, &count);
     }
     LOOP_CHECK(rc);
-    if (multi && count) {
+    uint64_t *hs = nullptr, S = 0;
+    if (multi && count && c->rs_hooks) LOOP_CHECK(ghs_solver_hook_slots(s, nr, &hs, &S));
+    if (S) {
+      // a dense level's opening round: reduce-scatter of the best slots, owner-computed hooks,
+      // all-gather of the (eid, other) pairs — 16 instead of 24 ring bytes per slot
+      const uint64_t per = S / nr;
+      LOOP_CHECK(coll_reducescatter_min_u64(c, hs, per, st));
+      LOOP_CHECK(ghs_solver_hook_owner(s, (uint32_t)c->rank, per, c->pairs));
+      LOOP_CHECK(coll_allgather_u64(c, c->pairs + (size_t)c->rank * per, c->pairs, per, st));
+      LOOP_CHECK(ghs_solver_apply_hooks(s, c->pairs));
+    } else if (multi && count) {
       if (uint64_t *slots = ghs_solver_best_slots_of(s)) {  // a dense level's first round: best in place
         LOOP_CHECK(coll_allreduce<uint64_t>(c, slots, count, st));
       } else {
@@ -283,7 +325,7 @@ int run_loop(ghs_solver_t *s, ghs_comm *c) {
 void comm_free(ghs_comm *c) {
   if (!c) return;
   if (hipSetDevice(c->dev) == hipSuccess) {
-    for (void *p : {(void *)c->dense, (void *)c->hook, (void *)c->gathered, (void *)c->agree})
+    for (void *p : {(void *)c->dense, (void *)c->hook, (void *)c->gathered, (void *)c->agree, (void *)c->pairs})
       if (p) (void)hipFree(p);
   }
   if (c->nccl && c->own_nccl) ncclCommDestroy(c->nccl);
@@ -548,7 +590,8 @@ extern "C" int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const ui
       comms[i].nccl = nullptr;
     }
     (void)hipSetDevice(devs[i]);
-    for (void *p : {(void *)comms[i].dense, (void *)comms[i].hook, (void *)comms[i].gathered, (void *)comms[i].agree})
+    for (void *p : {(void *)comms[i].dense, (void *)comms[i].hook, (void *)comms[i].gathered, (void *)comms[i].agree,
+                    (void *)comms[i].pairs})
       if (p) (void)hipFree(p);
   }
   (void)hipSetDevice(prev);
@@ -597,7 +640,7 @@ extern "C" int ghs_mst_emulated(uint32_t n, uint64_t m, const uint32_t *d_u, con
   const int rc = collect(d, result, stats, &err);
   for (auto &x : d) rank_release(x);
   for (auto &c : comms)
-    for (void *p : {(void *)c.dense, (void *)c.hook, (void *)c.gathered})
+    for (void *p : {(void *)c.dense, (void *)c.hook, (void *)c.gathered, (void *)c.pairs})
       if (p) (void)hipFree(p);
   (void)hipSetDevice(dev);
   if (rc) GHS_FAIL(rc, err);

@@ -107,6 +107,25 @@ class HipStepper:
     def unpack_hook(self, dense):
         _native.check(self.L.ghs_solver_unpack_hook(self.h, _ptr(dense)))
 
+    def hook_slots(self, nranks):
+        """The reduce-scatter protocol of a dense level's opening round (ABI 6): the best slots,
+        padded to a multiple of nranks, as an int64 view holding uint64 keys (MIN-reduce-scatter
+        them unsigned, in place), or None (the all-reduce protocol applies)."""
+        p = ctypes.c_void_p(0)
+        c = ctypes.c_uint64(0)
+        _native.check(self.L.ghs_solver_hook_slots(self.h, int(nranks), ctypes.byref(p), ctypes.byref(c)))
+        if not c.value:
+            return None
+        return _device_u8_view(p.value, 8 * int(c.value), self.e.edges.device, self.e.ws).view(torch.int64)
+
+    def hook_owner(self, rank, per, pairs):
+        """This rank's hooks (eid << 32 | other fragment) into pairs[rank * per:(rank + 1) * per]."""
+        _native.check(self.L.ghs_solver_hook_owner(self.h, int(rank), int(per), _ptr(pairs)))
+
+    def apply_hooks(self, pairs):
+        """Every rank's hooks (the all-gathered pairs): par, own-range MSF flags, totals."""
+        _native.check(self.L.ghs_solver_apply_hooks(self.h, _ptr(pairs)))
+
     def contract(self):
         d = ctypes.c_int(0)
         _native.check(self.L.ghs_solver_contract(self.h, ctypes.byref(d)))

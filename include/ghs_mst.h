@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GHS_MST_ABI_VERSION 5
+#define GHS_MST_ABI_VERSION 6
 
 #define GHS_OK 0
 #define GHS_NEED_EXCHANGE 1   /* ghs_solver_minedge on a multi-rank solver opened a level: OR-combine
@@ -99,6 +99,8 @@ typedef struct ghs_result {
 #define GHS_OPT_TIME_ROUNDS 0x20u  /* HIP events around the compacting min-edge launches
                                       (ghs_round_stats_t.ms_minedge; idles the GPU ~6 us each) */
 #define GHS_OPT_DETAIL 0x40u       /* HIP events around every stage of every round (diagnostic) */
+#define GHS_OPT_NO_WINDOW 0x100u   /* one rank, lattice-like: level 0 round 0 through k_bucket / k_bmin
+                                      records instead of the windowed k_wmin over the edge list */
 #define GHS_OPT_BUCKETED_FIRST 0x80u /* one rank: bucketed first rounds of every level (whatever the
                                         graph), the other rounds unbucketed */
 typedef struct ghs_config {
@@ -223,6 +225,22 @@ int ghs_solver_best_slots(ghs_solver_t *h, uint64_t **d_slots, uint64_t *count);
  * above); the totals of ghs_solver_finish are complete on every rank. */
 int ghs_solver_hook_local(ghs_solver_t *h, int32_t *d_dense, uint64_t *count);
 int ghs_solver_unpack_hook(ghs_solver_t *h, const int32_t *d_dense);
+/* optional (ABI 6), a dense level's opening round instead of best_slots / MIN all-reduce /
+ * hook_local / MAX all-reduce / unpack_hook — half the wire of a ring all-reduce per slot, the
+ * reference's collect of the CONNECT decisions (ghs_implementation_mpi.py:582-671) as 16 bytes:
+ *   hook_slots(h, N, &slots, &S)      S = 0: not applicable this round (use the calls above);
+ *                                     else `slots` = S uint64 (a multiple of N, padding = UINT64_MAX)
+ *   <caller: reduce-scatter MIN (uint64, in place): rank r keeps slots[r*S/N, (r+1)*S/N)>
+ *   hook_owner(h, r, S/N, pairs)      pairs[c] for the rank's slots: eid << 32 | the other dense
+ *                                     fragment of c's minimum edge (UINT64_MAX: no edge); the ends
+ *                                     come from the replicated canonical list
+ *   <caller: all-gather the S/N-slot slices (in place into pairs, S uint64)>
+ *   apply_hooks(h, pairs)             par (a mutual pair keeps its smaller fragment as the root),
+ *                                     the MSF flags of the rank's own edge range, the totals
+ * then contract as usual. (Replaces 2(N-1)/N x 12 bytes per slot with (N-1)/N x 16.) */
+int ghs_solver_hook_slots(ghs_solver_t *h, uint32_t nranks, uint64_t **d_slots, uint64_t *padded);
+int ghs_solver_hook_owner(ghs_solver_t *h, uint32_t rank, uint64_t per_rank, uint64_t *d_pairs);
+int ghs_solver_apply_hooks(ghs_solver_t *h, const uint64_t *d_pairs);
 /* hook + jump + next list; *done = 1 when every level is complete */
 int ghs_solver_contract(ghs_solver_t *h, int *done);
 int ghs_solver_finish(ghs_solver_t *h, ghs_result_t *result, ghs_round_stats_t *stats);
@@ -271,7 +289,7 @@ enum ghs_kernel_id {
   GHS_K_SELECT = 0, GHS_K_FILTER, GHS_K_LEVEL_PASS, GHS_K_SEED_RUNS, GHS_K_MINEDGE_IDENT, GHS_K_MINEDGE_COMPACT,
   GHS_K_WIN, GHS_K_HOOK, GHS_K_JUMP_IDENT, GHS_K_JUMP, GHS_K_SELECT_LB, GHS_K_RESOLVE, GHS_K_GIANT, GHS_K_SCAN,
   GHS_K_PLAN, GHS_K_INIT, GHS_K_PACK, GHS_K_UNPACK, GHS_K_ROUND_REPORT, GHS_K_PACK_HOOK, GHS_K_UNPACK_HOOK,
-  GHS_K_DENSE, GHS_K_FLAG_BITS, GHS_K_BUCKET, GHS_K_BMIN, GHS_K_COUNT
+  GHS_K_DENSE, GHS_K_FLAG_BITS, GHS_K_BUCKET, GHS_K_BMIN, GHS_K_WSTARTS, GHS_K_WMIN, GHS_K_HOT_HOOK, GHS_K_COUNT
 };
 typedef struct ghs_kernel_record {
   uint32_t kernel;  /* ghs_kernel_id */

@@ -156,9 +156,11 @@ def test_stepwise_solver_equals_monolithic(torch_cuda):
     assert rc.total_weight == ra.total_weight and rc.rounds == ra.rounds
 
 
-def _emulate_ranks(e, world, cfg=None, bitmaps=True):
+def _emulate_ranks(e, world, cfg=None, bitmaps=True, rs=False):
     """`world` edge-range engines on one GPU stepping in lock step, the collectives emulated with
-    torch.maximum / torch.minimum (exactly what RCCL's MAX / MIN all-reduce compute). Returns the
+    torch.maximum / torch.minimum (exactly what RCCL's MAX / MIN all-reduce compute). rs: a dense
+    level's opening round through the reduce-scatter protocol (hook_slots / reduce-scatter MIN /
+    hook_owner / all-gather / apply_hooks, ABI 6) instead of all-reduce + owner hooks. Returns the
     MSF flags assembled from the ranks' own slices (each rank writes only [e_lo, e_hi)) and every
     rank's (total weight, MSF edges)."""
     import torch
@@ -190,7 +192,26 @@ def _emulate_ranks(e, world, cfg=None, bitmaps=True):
                         b.copy_(red)
                 counts = [s.minedge() for s in steppers]
             assert len(set(counts)) == 1
-            if counts[0]:
+            slots = [s.hook_slots(world) for s in steppers] if rs and counts[0] else [None]
+            assert len(set(x is None for x in slots)) == 1
+            if slots[0] is not None:  # reduce-scatter MIN (unsigned) + the owners' pairs all-gathered
+                S = int(slots[0].numel())
+                assert S % world == 0 and S >= counts[0]
+                sign = torch.tensor(-(1 << 63), dtype=torch.int64, device=slots[0].device)
+                red = slots[0] ^ sign
+                for v in slots[1:]:
+                    red = torch.minimum(red, v ^ sign)
+                red ^= sign
+                per = S // world
+                for r, v in enumerate(slots):  # each rank receives its own slice only
+                    v[r * per:(r + 1) * per].copy_(red[r * per:(r + 1) * per])
+                pairs = torch.full((S,), -2, dtype=torch.int64, device=slots[0].device)
+                for r, st in enumerate(steppers):
+                    st.hook_owner(r, per, pairs)
+                assert not bool((pairs == -2).any())  # every slot written by its owner
+                for st in steppers:
+                    st.apply_hooks(pairs)
+            elif counts[0]:
                 dense = [s.pack(counts[0]).clone() for s in steppers]
                 red = dense[0]
                 for d in dense[1:]:
@@ -227,10 +248,15 @@ def _emulate_ranks(e, world, cfg=None, bitmaps=True):
             s.close()
 
 
-@pytest.mark.parametrize("world,graph,bitmaps", [(2, "rmat", True), (3, "rmat", False), (8, "rmat", True),
-                                                 (8, "grid", True), (5, "grid-gradient", True), (8, "readme", True),
-                                                 (8, "readme", False), (4, "ties", True), (4, "ties", False)])
-def test_partitioned_ranks_emulated_on_one_gpu(world, graph, bitmaps, torch_cuda):
+@pytest.mark.parametrize("world,graph,bitmaps,rs", [(2, "rmat", True, False), (3, "rmat", False, False),
+                                                    (8, "rmat", True, False), (8, "grid", True, False),
+                                                    (5, "grid-gradient", True, False), (8, "readme", True, False),
+                                                    (8, "readme", False, False), (4, "ties", True, False),
+                                                    (4, "ties", False, False), (2, "rmat", True, True),
+                                                    (8, "rmat", True, True), (8, "grid", True, True),
+                                                    (5, "grid-gradient", True, True), (8, "readme", True, True),
+                                                    (3, "ties", True, True), (4, "forest", True, True)])
+def test_partitioned_ranks_emulated_on_one_gpu(world, graph, bitmaps, rs, torch_cuda):
     """`world` edge-range engines on one GPU, all-reduces emulated: the OR of the ranks' flags is
     canonical Kruskal's MSF (oracle) and every rank reports the oracle's totals."""
     from distributed_ghs_implementation_amd import canonicalize
@@ -246,9 +272,11 @@ def test_partitioned_ranks_emulated_on_one_gpu(world, graph, bitmaps, torch_cuda
         n, m = 3000, 20000
         e = DeviceEdges.from_host(canonicalize(n, u=rng.integers(0, n, m), v=rng.integers(0, n, m),
                                                w=rng.integers(0, 3, m)))
+    elif graph == "forest":  # many components, isolated vertices
+        e = _test_graph("forest")
     else:
         e = generate_grid(257, 1 if graph == "grid-gradient" else 0)
-    flags, totals = _emulate_ranks(e, world, bitmaps=bitmaps)
+    flags, totals = _emulate_ranks(e, world, bitmaps=bitmaps, rs=rs)
     g = e.to_host()
     ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
     assert np.array_equal(flags.cpu().numpy().astype(bool), ref_in.astype(bool))
@@ -800,3 +828,31 @@ def test_bucketed_auto_on_lattices(k, mode, torch_cuda):
     ref_in, ref_tw, ref_k = ora.kruskal_c(h.n, h.u, h.v, h.w)
     assert np.array_equal(eng_r.in_mst_host(), ref_in.astype(bool))
     assert (res_r.total_weight, res_r.num_mst_edges) == (ref_tw, ref_k)
+
+
+@pytest.mark.parametrize("k,mode,extra", [(3000, 0, 0), (3000, 1, 0), (2900, 0, 64)])
+def test_windowed_round0_vs_oracle(k, mode, extra, torch_cuda):
+    """Level 0 round 0 of a lattice-like solve with >= 2^23 vertices runs windowed (k_wmin over the
+    level-0 edge list's run of two buckets, no records). `extra` lightest edges spanning many
+    buckets set k_select's span flag, and the round falls back to k_bucket / k_bmin on the device.
+    Both match the oracle, as does the record path forced by GHS_OPT_NO_WINDOW."""
+    from distributed_ghs_implementation_amd import _native, canonicalize
+    from distributed_ghs_implementation_amd.device import DeviceEdges, DeviceMST, generate_grid
+    ora = _oracle()
+    e = generate_grid(k, mode)
+    if extra:
+        g = e.to_host()
+        rng = np.random.default_rng(7)
+        u = rng.integers(0, g.n // 2, extra)
+        v = u + rng.integers(g.n // 4, g.n // 2, extra)
+        w = rng.integers(0, 16, extra)  # the lightest weights: level-0 edges
+        e = DeviceEdges.from_host(canonicalize(g.n, u=np.concatenate([g.u, u]), v=np.concatenate([g.v, v]),
+                                               w=np.concatenate([g.w, w])))
+    g = e.to_host()
+    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    for opt in (0, _native.OPT_NO_WINDOW):
+        eng = DeviceMST(e, config=_native.make_config(options=opt) if opt else None)
+        res, _ = eng.run()
+        assert res.pass_flags & 1 and res.pass_flags & 2  # lattice-like, bucketed level-0 rounds
+        assert np.array_equal(eng.in_mst_host(), ref_in.astype(bool))
+        assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--no-inplace", action="store_true",
                     help="pack / int64 MIN / unpack in every round (the gloo loop) instead of the library "
                          "loop's in-place uint64 MIN of a dense level's first round")
+    ap.add_argument("--allreduce-hooks", action="store_true",
+                    help="a dense level's opening round by all-reduce MIN + owner hooks as int32 MAX (the "
+                         "stepwise protocol) instead of the library loop's reduce-scatter + pair all-gather")
     ap.add_argument("--profile", action="store_true",
                     help="per-launch HIP-event profile of the last rep: kernel ms per round of the max rank")
     ap.add_argument("--max-levels", type=int, default=None)
@@ -103,7 +106,27 @@ def main():
                     counts.append(c)
                     ms[r] += t
             assert len(set(counts)) == 1
-            if counts[0]:
+            rs = [None] if args.allreduce_hooks or not counts[0] else [s.hook_slots(W) for s in steppers]
+            if rs[0] is not None:  # the library loop's reduce-scatter protocol (collectives not timed)
+                S = int(rs[0].numel())
+                per = S // W
+                sign = torch.tensor(-(1 << 63), dtype=torch.int64, device=rs[0].device)
+                red = rs[0] ^ sign
+                for v in rs[1:]:
+                    red = torch.minimum(red, v ^ sign)
+                red ^= sign
+                for v in rs:
+                    v.copy_(red)  # (a rank uses only its own slice)
+                coll.append(("reducescatter_min_u64", S * 8))
+                pairs = torch.empty(S, dtype=torch.int64, device=rs[0].device)
+                for r, s in enumerate(steppers):
+                    _, t = timed(r, lambda: s.hook_owner(r, per, pairs))
+                    ms[r] += t
+                coll.append(("allgather_pairs", per * 8))
+                for r, s in enumerate(steppers):
+                    _, t = timed(r, lambda: s.apply_hooks(pairs))
+                    ms[r] += t
+            elif counts[0]:
                 slots = [None] if args.no_inplace else [s.best_slots() for s in steppers]
                 if slots[0] is not None:  # the library loop's in-place uint64 MIN (not timed)
                     sign = torch.tensor(-(1 << 63), dtype=torch.int64, device=slots[0].device)
@@ -165,10 +188,13 @@ def main():
             assert all(r.total_weight == rres.total_weight for r in res)
         compute = sum(r["max_rank_ms"] for r in rounds)
         payload = sum(b for r in rounds for _, b in r["collectives"])
-        # ring all-reduce: every rank sends (and receives) 2 (N-1)/N of the buffer; all-gather of
-        # a b-byte contribution per rank: (N-1) b
-        wire = sum((W - 1) * b if k.startswith("allgather") else 2.0 * (W - 1) / W * b
-                   for r in rounds for k, b in r["collectives"])
+        # ring all-reduce: every rank sends (and receives) 2 (N-1)/N of the buffer; ring
+        # reduce-scatter (N-1)/N; all-gather of a b-byte contribution per rank: (N-1) b
+        def ring(k, b):
+            if k.startswith("allgather"):
+                return (W - 1) * b
+            return (1.0 if k.startswith("reducescatter") else 2.0) * (W - 1) / W * b
+        wire = sum(ring(k, b) for r in rounds for k, b in r["collectives"])
         ncoll = sum(len(r["collectives"]) for r in rounds)
         print(json.dumps({"scale": args.scale, "world": W, "rep": rep, "m": e.m, "n": e.n,
                           "single_gpu_ms": one_ms and round(one_ms, 3), "rounds": len(rounds),
