@@ -245,7 +245,7 @@ def load():
             "ghs_solver_unpack_hook": (i32, [vp, vp]),
             "ghs_solver_hook_slots": (i32, [vp, u32, P(vp), P(u64)]),
             "ghs_solver_hook_owner": (i32, [vp, u32, u64, vp]),
-            "ghs_solver_apply_hooks": (i32, [vp, vp]),
+            "ghs_solver_apply_hooks": (i32, [vp, vp, P(vp)]),
             "ghs_solver_reset": (i32, [vp]),
             "ghs_solver_cancel": (i32, [vp]),
             "ghs_solver_destroy": (i32, [vp]),

@@ -1134,6 +1134,14 @@ __device__ __forceinline__ void add_totals_one(unsigned long long wsum, unsigned
   }
 }
 
+// the reduce-scatter protocol's partial totals (all-reduced by the caller) join the totals
+__global__ void k_fold_partial(unsigned long long *__restrict__ cnt) {
+  cnt[2] += cnt[11];  // C_WEIGHT += C_RS_WEIGHT, C_EDGES += C_RS_EDGES
+  cnt[3] += cnt[12];
+  cnt[11] = 0;
+  cnt[12] = 0;
+}
+
 __global__ void k_pad_slots(uint64_t *__restrict__ best, const unsigned long long *__restrict__ d_nact, uint64_t padded) {
   const uint64_t i = *d_nact + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (i < padded) best[i] = KEY_NONE;
@@ -1169,10 +1177,12 @@ __global__ __launch_bounds__(BLOCK) void k_apply_pairs(const uint64_t *__restric
     best[c] = p;  // every rank the same "had an outgoing edge" for the jump's keep test
     if (p == KEY_NONE) continue;
     const uint32_t o = (uint32_t)p, eid = (uint32_t)(p >> 32);
-    const bool mutual = (uint32_t)pairs[o] == (uint32_t)c;
-    if (mutual && (uint32_t)c < o) continue;  // the pair's root: its partner hooks over the edge
-    par[c] = o;
-    if (eid >= own_lo && eid < own_hi) in_mst[eid] = 1;
+    par[c] = o;  // a mutual pair stays a 2-cycle: the jump keeps its smaller member as the root
+    // the MSF flag and the totals of the rank's own edges only (1/N of the random reads); the
+    // caller SUM-all-reduces the partial totals
+    if (eid < own_lo || eid >= own_hi) continue;
+    if ((uint32_t)pairs[o] == (uint32_t)c && (uint32_t)c < o) continue;  // counted by its partner's slot
+    in_mst[eid] = 1;
     wsum += ew[eid];
     cnt += 1;
   }
@@ -2495,41 +2505,73 @@ __global__ __launch_bounds__(BM_T) void k_bmin(const uint4 *__restrict__ rec, co
 // k_wstarts: start[t] = the first virtual index whose edge has a >= t << bs (start[nb] = total):
 // a search over the regions' first edges, then inside one region (its padding is at its end).
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_wstarts(SegView in, const uint32_t *__restrict__ src, uint32_t bs, uint32_t nb,
-                                                 uint64_t *__restrict__ start,
+// k_wfirst (one block): F[r] = the first edge's a of region r, an empty region taking the next
+// non-empty one's (suffix minimum; the regions are in canonical order) — level 0 of the gradient
+// grid leaves whole runs of regions empty, which a search that skips them one by one crawls over
+constexpr uint32_t WF_T = 1024;
+__global__ __launch_bounds__(WF_T) void k_wfirst(SegView in, const uint32_t *__restrict__ src, uint32_t *__restrict__ F,
+                                                 const unsigned long long *__restrict__ long_flag) {
+  __shared__ uint32_t s_w[WF_T / WAVE];
+  if (*long_flag) return;
+  const uint32_t per = (in.nseg + WF_T - 1) / WF_T, r0 = threadIdx.x * per;
+  uint32_t v[16];  // per <= 16: nseg <= SEG_MAX = 16384
+  uint32_t run = LABEL_NONE;
+#pragma unroll
+  for (int j = 15; j >= 0; --j) {  // the thread's regions, last first: suffix minimum
+    const uint32_t r = r0 + (uint32_t)j;
+    uint32_t x = LABEL_NONE;
+    if ((uint32_t)j < per && r < in.nseg && in.prefix[r + 1] > in.prefix[r]) x = src[in.start[r]];
+    run = x < run ? x : run;
+    v[j] = run;
+  }
+  // suffix minimum across threads: the minimum over the threads above (wave shuffles + LDS)
+  const uint32_t lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+  uint32_t incl = v[0];
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const uint32_t o = __shfl_down(incl, d);
+    if (lane + d < WAVE) incl = o < incl ? o : incl;
+  }
+  if (lane == 0) s_w[wid] = incl;
+  __syncthreads();
+  uint32_t after = __shfl_down(incl, 1);
+  if (lane == WAVE - 1) after = LABEL_NONE;
+  for (uint32_t w = wid + 1; w < WF_T / WAVE; ++w) after = s_w[w] < after ? s_w[w] : after;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t r = r0 + (uint32_t)j;
+    if ((uint32_t)j < per && r < in.nseg) F[r] = v[j] < after ? v[j] : after;
+  }
+}
+
+// k_wstarts: start[t] = the first virtual index whose edge has a >= t << bs (start[nb] = total):
+// the last region whose first edge lies below (F), then a search inside it (its padding is at its end)
+__global__ __launch_bounds__(256) void k_wstarts(SegView in, const uint32_t *__restrict__ src, const uint32_t *__restrict__ F,
+                                                 uint32_t bs, uint32_t nb, uint64_t *__restrict__ start,
                                                  const unsigned long long *__restrict__ long_flag) {
   const uint32_t t = blockIdx.x * 256 + threadIdx.x;
   if (t > nb || *long_flag) return;
   const uint64_t T = in.prefix[in.nseg];
   const uint64_t x = (uint64_t)t << bs;
-  if (t == 0 || T == 0) {
+  if (t == 0 || t == nb || T == 0) {
     start[t] = t == 0 ? 0 : T;
     return;
   }
-  if (t == nb) {
-    start[t] = T;
-    return;
-  }
-  // the first edge of region s (regions may be empty: the next non-empty one's, or "none")
-  auto first_a = [&](uint32_t r) -> uint64_t {
-    while (r < in.nseg && in.prefix[r + 1] == in.prefix[r]) ++r;
-    return r < in.nseg ? (uint64_t)src[in.start[r]] : ~0ull;
-  };
-  // last region whose first edge has a < x (region 0 if none)
-  uint32_t lo = 0, hi = in.nseg - 1;
+  uint32_t lo = 0, hi = in.nseg - 1;  // the last region whose first edge has a < x (region 0 if none)
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) >> 1;
-    if (first_a(mid) < x) lo = mid; else hi = mid - 1;
+    if ((uint64_t)F[mid] < x) lo = mid; else hi = mid - 1;
   }
   const uint64_t p0 = in.start[lo], cnt = in.prefix[lo + 1] - in.prefix[lo];
-  uint64_t l = 0, h = cnt;  // first entry of region lo with a >= x (padding: LABEL_NONE >= x)
+  uint64_t l = 0, h = cnt;  // an empty region lo (then F[lo] >= x or lo = 0): l = 0
   while (l < h) {
     const uint64_t mid = (l + h) >> 1;
     if ((uint64_t)src[p0 + mid] < x) l = mid + 1; else h = mid;
   }
-  start[t] = in.prefix[lo] + l;  // l == cnt: the next region's first edge (a >= x by the search)
+  start[t] = in.prefix[lo] + l;  // l == cnt: the next region's first edge (a >= x by F)
 }
 
+constexpr uint32_t WM_CHUNK = 32;
 template <uint32_t BS>
 __global__ __launch_bounds__(BM_T) void k_wmin(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
                                                const uint64_t *__restrict__ key, SegView in, uint32_t nb,
@@ -2539,8 +2581,11 @@ __global__ __launch_bounds__(BM_T) void k_wmin(const uint32_t *__restrict__ src,
   constexpr uint32_t SPAN = 1u << BS;
   __shared__ unsigned long long s_min[SPAN];
   __shared__ uint32_t s_seg[2];
-  const uint32_t per = (nb + 7) / 8;  // XCD order
-  const uint32_t t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  // XCD order: workgroup i runs on XCD i % 8; chunks of WM_CHUNK consecutive buckets go round-robin
+  // to the XCDs, so a chunk's buckets (which share rows) run together on one XCD's L2 while a
+  // spatially skewed level (the gradient grid's lighter half) still spreads over every XCD
+  const uint32_t j = blockIdx.x / 8;
+  const uint32_t t = ((j / WM_CHUNK) * 8 + blockIdx.x % 8) * WM_CHUNK + j % WM_CHUNK;
   if (t >= nb || *long_flag) return;
   const uint64_t wlo = start[t ? t - 1 : 0], whi = start[t + 1 < nb ? t + 1 : nb];
   if (whi <= wlo) return;  // block-uniform: no edge with an end in this bucket
@@ -3084,6 +3129,7 @@ enum : int {
   C_NDENSE = 7,   // fragments of a dense level (several ranks): the count of its identity list
   C_ACT = 8,      // [8], [9]: lengths of the active lists act[0], act[1]
   C_LONG = 10,    // a level-0 edge spans more than one bucket (k_select, lattice-like plans)
+  C_RS_WEIGHT = 11,  // [11], [12]: a rank's own-range part of the reduce-scatter round's totals
   C_COUNT = 16
 };
 static_assert(C_WEIGHT == 2 && C_EDGES == 3 && C_ERR == 4 && C_PENDING == 5, "write_report reads the counters by index");
@@ -3245,6 +3291,7 @@ struct ghs_solver {
   uint64_t *vbest = nullptr;
   bool dense_mode = false;      // several ranks and the dense arrays exist (GHS_DENSE=0: off)
   bool level_dense = false;     // the open level runs in dense labels
+  bool rs_fold = false;         // apply_hooks left partial totals for contract to fold in
   uint64_t dense_n = 0;
   // bucketed rounds (single rank, lattice-like graphs; k_bucket / k_bmin): the record buffers,
   // the offsets table, the bucket geometry, and the per-solve / per-round decisions
@@ -3484,7 +3531,7 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
     const uint64_t rc = 2 * cap + 8 * BK_G;
     p = carve(rc * 16); if (s) s->rec = (uint4 *)p;
     p = carve((size_t)(nb + 1) * BK_G * 4); if (s) s->bk_off = (uint32_t *)p;
-    p = carve((size_t)(nb + 1) * 8); if (s) s->wstart = (uint64_t *)p;
+    p = carve((size_t)(nb + 1) * 8 + SEG_MAX * 4); if (s) s->wstart = (uint64_t *)p;  // + region-first table
     if (s) {
       s->bk_bs = bs;
       s->bk_nb = nb;
@@ -3991,11 +4038,13 @@ static int enqueue_minedge(ghs_solver *s) {
         const unsigned long long *far = s->cnt + C_LONG;
         {
           KT(GHS_K_WSTARTS, s->bk_nb);
-          k_wstarts<<<(s->bk_nb + 1 + 255) / 256, 256, 0, s->stream>>>(in, I.src, s->bk_bs, s->bk_nb, s->wstart, far);
+          uint32_t *F = reinterpret_cast<uint32_t *>(s->wstart + s->bk_nb + 1);  // region-first table
+          k_wfirst<<<1, WF_T, 0, s->stream>>>(in, I.src, F, far);
+          k_wstarts<<<(s->bk_nb + 1 + 255) / 256, 256, 0, s->stream>>>(in, I.src, F, s->bk_bs, s->bk_nb, s->wstart, far);
         }
         {
           KT(GHS_K_WMIN, items);
-          const unsigned wg = 8 * ((s->bk_nb + 7) / 8);
+          const unsigned wg = 8 * WM_CHUNK * ((s->bk_nb + 8 * WM_CHUNK - 1) / (8 * WM_CHUNK));
           if (s->bk_bs == 13)
             k_wmin<13><<<wg, BM_T, 0, s->stream>>>(I.src, I.dst, I.key, in, s->bk_nb, s->wstart, s->par, s->best,
                                                   s->in_mst, far);
@@ -4057,6 +4106,11 @@ static int enqueue_minedge(ghs_solver *s) {
 
 // slot != nullptr: the round's last kernel reports (live, active, edges, err, seq) to it
 static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned long long seq = 0) {
+  if (s->rs_fold) {  // the reduce-scatter round's totals, summed over the ranks by the caller
+    k_fold_partial<<<1, 1, 0, s->stream>>>(s->cnt);
+    GHS_HIP_CHECK(hipGetLastError());
+    s->rs_fold = false;
+  }
   const uint32_t *act = s->act_ident ? nullptr : s->act[s->act_cur];
   const unsigned long long *d_nact = cur_act_count(s);
   const uint64_t bound = s->nact;
@@ -4647,18 +4701,20 @@ int ghs_solver_hook_owner(ghs_solver_t *s, uint32_t rank, uint64_t per, uint64_t
   return GHS_OK;
 }
 
-int ghs_solver_apply_hooks(ghs_solver_t *s, const uint64_t *d_pairs) {
-  if (!s || (s->nact && !d_pairs)) GHS_FAIL(GHS_E_ARG, "solver/pairs is NULL");
+int ghs_solver_apply_hooks(ghs_solver_t *s, const uint64_t *d_pairs, uint64_t **d_partial) {
+  if (!s || (s->nact && !d_pairs) || !d_partial) GHS_FAIL(GHS_E_ARG, "solver/pairs/partial is NULL");
+  *d_partial = reinterpret_cast<uint64_t *>(s->cnt + C_RS_WEIGHT);
   if (s->phase != 1 || !s->level_dense || !s->act_ident || s->level_round != 0 || s->hooked)
     GHS_FAIL(GHS_E_STATE, "apply_hooks must follow hook_owner and the all-gather");
   if (s->nact) {
     KT(GHS_K_UNPACK_HOOK, s->nact);
     k_apply_pairs<<<grid_for(s->nact, BLOCK, HOOK_G), BLOCK, 0, s->stream>>>(
         d_pairs, cur_act_count(s), s->ew, s->par, s->best, s->in_mst, (uint32_t)s->e_lo, (uint32_t)s->e_hi,
-        s->cnt + C_WEIGHT);
+        s->cnt + C_RS_WEIGHT);
     GHS_HIP_CHECK(hipGetLastError());
   }
   s->hooked = true;
+  s->rs_fold = true;  // contract folds the (all-reduced) partial totals in first
   return GHS_OK;
 }
 
@@ -4834,6 +4890,7 @@ int ghs_solver_reset(ghs_solver_t *s) {
   t.eu = s->eu; t.ev = s->ev; t.ew = s->ew;
   t.in_mst = s->in_mst; t.stream = s->stream; t.cfg = s->cfg;
   t.debug = s->debug; t.lookahead = s->lookahead; t.seed_runs = s->seed_runs; t.dedup_max = s->dedup_max;
+  t.windowed = s->windowed;
   t.detail = s->detail; t.time_rounds = s->time_rounds;
   t.group_cancel = s->group_cancel;
   { std::lock_guard<std::mutex> lock(g_prof_mutex); t.prof = g_prof_on; }

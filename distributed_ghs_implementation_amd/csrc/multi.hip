@@ -80,6 +80,10 @@ __global__ void k_emu_min_u64(uint64_t *__restrict__ dst, const uint64_t *__rest
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     dst[i] = src[i] < dst[i] ? src[i] : dst[i];
 }
+__global__ void k_emu_sum_u64(uint64_t *__restrict__ dst, const uint64_t *__restrict__ src, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] += src[i];
+}
 __global__ void k_emu_max_i32(int32_t *__restrict__ dst, const int32_t *__restrict__ src, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     dst[i] = src[i] > dst[i] ? src[i] : dst[i];
@@ -218,6 +222,30 @@ int coll_allreduce(ghs_comm *c, T *buf, size_t count, hipStream_t st) {
   return GHS_OK;
 }
 
+// in-place SUM all-reduce over uint64 (the reduce-scatter round's partial totals: 2 words)
+int coll_allreduce_sum_u64(ghs_comm *c, uint64_t *buf, size_t count, hipStream_t st) {
+  if (c->nccl) {
+    COMM_NCCL(ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, c->nccl, st));
+    return GHS_OK;
+  }
+  GHS_HIP_CHECK(hipStreamSynchronize(st));
+  c->emu->ptrs[c->rank] = buf;
+  COMM_BARRIER(c);
+  if (c->rank == 0) {
+    for (int r = 1; r < c->nranks; ++r)
+      k_emu_sum_u64<<<1, 64, 0, st>>>(buf, (const uint64_t *)c->emu->ptrs[r], count);
+    GHS_HIP_CHECK(hipGetLastError());
+    GHS_HIP_CHECK(hipStreamSynchronize(st));
+  }
+  COMM_BARRIER(c);
+  if (c->rank != 0) {
+    GHS_HIP_CHECK(hipMemcpyAsync(buf, c->emu->ptrs[0], count * 8, hipMemcpyDeviceToDevice, st));
+    GHS_HIP_CHECK(hipStreamSynchronize(st));
+  }
+  COMM_BARRIER(c);
+  return GHS_OK;
+}
+
 // Setup agreement, before a rank's first collective: every rank contributes its setup status and
 // learns whether any rank failed (int32 MAX over RCCL; the emulated group's barrier). A rank whose
 // workspace allocation or copy failed thereby fails the call on every rank instead of leaving the
@@ -300,7 +328,9 @@ int run_loop(ghs_solver_t *s, ghs_comm *c) {
       LOOP_CHECK(coll_reducescatter_min_u64(c, hs, per, st));
       LOOP_CHECK(ghs_solver_hook_owner(s, (uint32_t)c->rank, per, c->pairs));
       LOOP_CHECK(coll_allgather_u64(c, c->pairs + (size_t)c->rank * per, c->pairs, per, st));
-      LOOP_CHECK(ghs_solver_apply_hooks(s, c->pairs));
+      uint64_t *partial = nullptr;
+      LOOP_CHECK(ghs_solver_apply_hooks(s, c->pairs, &partial));
+      LOOP_CHECK(coll_allreduce_sum_u64(c, partial, 2, st));
     } else if (multi && count) {
       if (uint64_t *slots = ghs_solver_best_slots_of(s)) {  // a dense level's first round: best in place
         LOOP_CHECK(coll_allreduce<uint64_t>(c, slots, count, st));

@@ -123,8 +123,12 @@ class HipStepper:
         _native.check(self.L.ghs_solver_hook_owner(self.h, int(rank), int(per), _ptr(pairs)))
 
     def apply_hooks(self, pairs):
-        """Every rank's hooks (the all-gathered pairs): par, own-range MSF flags, totals."""
-        _native.check(self.L.ghs_solver_apply_hooks(self.h, _ptr(pairs)))
+        """Every rank's hooks (the all-gathered pairs): par, own-range MSF flags; returns this
+        rank's partial totals (an int64 view of 2 words: weight, MSF edges of its own range) to
+        SUM-all-reduce in place before contract."""
+        p = ctypes.c_void_p(0)
+        _native.check(self.L.ghs_solver_apply_hooks(self.h, _ptr(pairs), ctypes.byref(p)))
+        return _device_u8_view(p.value, 16, self.e.edges.device, self.e.ws).view(torch.int64)
 
     def contract(self):
         d = ctypes.c_int(0)
@@ -164,9 +168,16 @@ class HipStepper:
             pass
 
 
-def run_rounds(stepper, allreduce_min, max_rounds=4096, allreduce_max=None, allgather=None):
+def run_rounds(stepper, allreduce_min, max_rounds=4096, allreduce_max=None, allgather=None, rs=None):
     """The level loop shared by every backend: (level open: OR the fragment flags), min-edge,
     all-reduce MIN, (a level's first round: owner-computes hook, all-reduce MAX), contract.
+
+    `rs` (default: allreduce_min.rs when present) enables the library loop's reduce-scatter
+    protocol for a level's first round (ABI 6; multi.hip run_loop): hook_slots -> reduce-scatter
+    MIN (unsigned) -> hook_owner on this rank's slice -> all-gather of the pairs -> apply_hooks ->
+    SUM all-reduce of the partial totals. It needs `rs.world`, `rs.rank`,
+    `rs.reduce_scatter_min_u64(t)` (each rank's slice reduced in place), `rs.allgather_slices(t,
+    per)` and `rs.allreduce_sum(t)`.
 
     `allreduce_min(tensor)` / `allreduce_max(tensor)` reduce in place across ranks (identity for
     one rank; allreduce_max defaults to allreduce_min's backend with MAX). `allgather(tensor) ->
@@ -176,6 +187,7 @@ def run_rounds(stepper, allreduce_min, max_rounds=4096, allreduce_max=None, allg
     Raises RuntimeError past `max_rounds` (hang guard; Boruvka needs at most ceil(log2 n) + 1
     rounds per level)."""
     rounds = 0
+    rs = rs or getattr(allreduce_min, "rs", None)
     gather = allgather or getattr(allreduce_min, "gather", None)
     use_bits = gather is not None and hasattr(stepper, "flag_bits")
     while True:
@@ -187,7 +199,17 @@ def run_rounds(stepper, allreduce_min, max_rounds=4096, allreduce_max=None, allg
             else:
                 (allreduce_max or allreduce_min.max)(stepper.exchange_buffer())
             count = stepper.minedge()
-        if count:
+        slots = None
+        if count and rs is not None and getattr(stepper, "hook_slots", None) is not None:
+            slots = stepper.hook_slots(rs.world)
+        if slots is not None:  # reduce-scatter CONNECT: S * 8 (N - 1) / N wire bytes per rank
+            per = slots.numel() // rs.world
+            rs.reduce_scatter_min_u64(slots)
+            pairs = torch.empty(slots.numel(), dtype=torch.int64, device=slots.device)
+            stepper.hook_owner(rs.rank, per, pairs)
+            rs.allgather_slices(pairs, per)
+            rs.allreduce_sum(stepper.apply_hooks(pairs))
+        elif count:
             dense = stepper.pack(count)
             allreduce_min(dense)
             stepper.unpack(dense)
@@ -225,10 +247,47 @@ def _torch_allgather(group=None):
     return fn
 
 
-def torch_allreduce_min(group=None):
+class TorchRs:
+    """The reduce-scatter protocol's collectives over a torch.distributed group (see run_rounds).
+    uint64 keys travel as int64 with the sign bit flipped, so a signed MIN orders them unsigned;
+    nccl reduce-scatters and all-gathers the slices in place, gloo (no in-place reduce-scatter)
+    all-reduces the whole buffer and all-gathers through per-rank chunks."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.nccl = dist.get_backend(group) == "nccl"
+
+    def reduce_scatter_min_u64(self, t):
+        sign = torch.tensor(-(1 << 63), dtype=torch.int64, device=t.device)
+        t.bitwise_xor_(sign)
+        if self.nccl:
+            per = t.numel() // self.world
+            dist.reduce_scatter_tensor(t[self.rank * per:(self.rank + 1) * per], t, op=dist.ReduceOp.MIN,
+                                       group=self.group)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        t.bitwise_xor_(sign)
+
+    def allgather_slices(self, t, per):
+        mine = t[self.rank * per:(self.rank + 1) * per]
+        if self.nccl:
+            dist.all_gather_into_tensor(t, mine.clone(), group=self.group)
+        else:
+            parts = [torch.empty_like(mine) for _ in range(self.world)]
+            dist.all_gather(parts, mine.clone(), group=self.group)
+            t.copy_(torch.cat(parts))
+
+    def allreduce_sum(self, t):
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+
+
+def torch_allreduce_min(group=None, rs=True):
     fn = _torch_allreduce(dist.ReduceOp.MIN, group)
     fn.max = _torch_allreduce(dist.ReduceOp.MAX, group)
     fn.gather = _torch_allgather(group)
+    fn.rs = TorchRs(group) if rs and dist.is_initialized() and dist.get_world_size(group) > 1 else None
     return fn
 
 

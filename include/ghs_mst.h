@@ -235,12 +235,16 @@ int ghs_solver_unpack_hook(ghs_solver_t *h, const int32_t *d_dense);
  *                                     fragment of c's minimum edge (UINT64_MAX: no edge); the ends
  *                                     come from the replicated canonical list
  *   <caller: all-gather the S/N-slot slices (in place into pairs, S uint64)>
- *   apply_hooks(h, pairs)             par (a mutual pair keeps its smaller fragment as the root),
- *                                     the MSF flags of the rank's own edge range, the totals
- * then contract as usual. (Replaces 2(N-1)/N x 12 bytes per slot with (N-1)/N x 16.) */
+ *   apply_hooks(h, pairs, &partial)   par for every fragment (a mutual pair stays a 2-cycle that the
+ *                                     jump resolves: its smaller fragment keeps the root), the MSF
+ *                                     flags of the rank's own edge range, and in `partial` (2 uint64,
+ *                                     device) the weight and count of those own-range MSF edges
+ *   <caller: all-reduce SUM (uint64) of partial, in place>
+ * then contract as usual (it adds the summed partial totals to the solve's totals). (Replaces
+ * 2(N-1)/N x 12 bytes per slot with (N-1)/N x 16, + 16 bytes.) */
 int ghs_solver_hook_slots(ghs_solver_t *h, uint32_t nranks, uint64_t **d_slots, uint64_t *padded);
 int ghs_solver_hook_owner(ghs_solver_t *h, uint32_t rank, uint64_t per_rank, uint64_t *d_pairs);
-int ghs_solver_apply_hooks(ghs_solver_t *h, const uint64_t *d_pairs);
+int ghs_solver_apply_hooks(ghs_solver_t *h, const uint64_t *d_pairs, uint64_t **d_partial);
 /* hook + jump + next list; *done = 1 when every level is complete */
 int ghs_solver_contract(ghs_solver_t *h, int *done);
 int ghs_solver_finish(ghs_solver_t *h, ghs_result_t *result, ghs_round_stats_t *stats);

@@ -20,6 +20,13 @@ fragments whose winning edge (best key) is one of ITS level edges and marks that
 on its own copy only; slot i of the int32 exchange carries par[c] ^ c for active fragment c (0
 where another rank owns the winner), a MAX all-reduce gathers every hook, and unpack applies
 them (par, totals) identically on every rank. The MSF is then the OR of the ranks' flags.
+
+Reduce-scatter CONNECT (ghs_solver_hook_slots / hook_owner / apply_hooks, ABI 6; k_hook_owner +
+k_apply_pairs + k_fold_partial in boruvka.hip), same round: the active slots' local minima,
+padded with KEY_NONE to a multiple of the rank count, are MIN-reduce-scattered; rank r resolves
+its slice [r*per, (r+1)*per) to pairs (eid << 32 | other slot); the all-gathered pairs give every
+rank the same parents (mutual pair: the smaller label stays root), each rank flags and sums only
+the winning edges of ITS edge range, and the 2-word partial totals are SUM-all-reduced.
 """
 import numpy as np
 
@@ -52,6 +59,9 @@ class CpuStepper:
         self.level_round = 0
         self.hook_par = None  # par of an owner-computed CONNECT (unpack_hook), else None
         self.hooks_exchanged = 0  # rounds whose CONNECT came through the hook exchange
+        self.rs = True  # offer the reduce-scatter protocol (hook_slots) to the caller
+        self._slots = None
+        self._partial = None
 
     def _open_level(self):
         lo, hi = self.thr[self.level], self.thr[self.level + 1]
@@ -136,9 +146,64 @@ class CpuStepper:
         self.hook_par = par
         self.hooks_exchanged += 1
 
+    def hook_slots(self, nranks):
+        """The reduce-scatter protocol of a level's first round: best[active] padded with KEY_NONE
+        to a multiple of nranks, an int64 tensor of uint64 keys (MIN-reduce-scatter unsigned), or
+        None (the all-reduce protocol applies)."""
+        if not self.rs or self.ranks <= 1 or self.level_round != 0 or self.done or not len(self.active) \
+                or not self.level_open:
+            return None
+        S = -(-len(self.active) // nranks) * nranks
+        vals = np.full(S, KEY_NONE, dtype=np.uint64)
+        vals[: len(self.active)] = self.best[self.active]
+        self._slots = self.torch.from_numpy(vals.view(np.int64))
+        return self._slots
+
+    def hook_owner(self, rank, per, pairs):
+        """Resolve this rank's slice of the reduced slots to (eid << 32 | other slot)."""
+        k = self._slots.numpy().view(np.uint64)[rank * per:(rank + 1) * per].copy()
+        lo = rank * per
+        out = np.full(per, KEY_NONE, dtype=np.uint64)
+        n_real = max(0, min(per, len(self.active) - lo))
+        kk = k[:n_real]
+        has = kk != KEY_NONE
+        eid = (kk[has] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+        c = self.active[lo:lo + n_real][has]
+        la, lb = self.comp[self.u[eid]], self.comp[self.v[eid]]
+        other = np.searchsorted(self.active, np.where(la == c, lb, la))
+        sub = out[:n_real]
+        sub[has] = (eid.astype(np.uint64) << np.uint64(32)) | other.astype(np.uint64)
+        pairs.numpy().view(np.uint64)[lo:lo + per] = out
+
+    def apply_hooks(self, pairs):
+        """Every rank's pairs: parents (mutual pair resolved, smaller slot stays root), own-range
+        MSF flags; returns the partial totals [weight, edges] (int64) to SUM-all-reduce."""
+        act = self.active
+        p = pairs.numpy().view(np.uint64)[: len(act)]
+        has = p != KEY_NONE
+        i = np.flatnonzero(has)
+        o = (p[i] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+        eid = (p[i] >> np.uint64(32)).astype(np.int64)
+        mutual = (p[o] & np.uint64(0xFFFFFFFF)).astype(np.int64) == i
+        hook = ~(mutual & (i < o))
+        par = np.arange(self.n, dtype=np.int64)
+        par[act[i[hook]]] = act[o[hook]]
+        own = hook & (eid >= self.e_lo) & (eid < self.e_hi)
+        self.in_mst[eid[own]] = 1
+        self.best[act] = KEY_NONE
+        self.best[act[i]] = self.key[eid]
+        self.hook_par = par
+        self.hooks_exchanged += 1
+        self._partial = self.torch.tensor([int(self.w[eid[own]].sum()), int(own.sum())], dtype=self.torch.int64)
+        return self._partial
+
     def contract(self):
         if self.done:
             return True
+        if self._partial is not None:  # the SUM-reduced partial totals of apply_hooks
+            self.total += int(self._partial[0])
+            self.count += int(self._partial[1])
+            self._partial = None
         act = self.active
         k = self.best[act]
         has = k != KEY_NONE

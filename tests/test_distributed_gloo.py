@@ -2,7 +2,9 @@
 MIN) on CPU with the gloo backend, world_size 2 and 3, with one and with several weight levels.
 The per-rank compute is the oracle's numpy stepper (oracle/boruvka_steps.py) standing in for the
 HIP stepper, including the owner-computes CONNECT exchange of a level's first round (hook_local,
-int32 MAX all-reduce, unpack_hook: distributed.run_rounds drives it exactly as for HipStepper).
+int32 MAX all-reduce, unpack_hook: distributed.run_rounds drives it exactly as for HipStepper)
+and the reduce-scatter CONNECT of the library loop (hook_slots, reduce-scatter MIN, hook_owner,
+pair all-gather, apply_hooks, SUM of the partial totals; distributed.TorchRs over gloo).
 The totals must equal canonical Kruskal on every rank and the OR of the ranks' MSF flags must
 equal Kruskal's edge set (an owner-computed hook marks its edge on the owning rank only)."""
 import os
@@ -23,17 +25,18 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, u, v, w, thr, out, owner_hooks):
+def _worker(rank, world, port, n, u, v, w, thr, out, owner_hooks, use_rs):
     import torch.distributed as dist
 
     from distributed_ghs_implementation_amd.device import edge_range
-    from distributed_ghs_implementation_amd.distributed import run_rounds
+    from distributed_ghs_implementation_amd.distributed import TorchRs, run_rounds
     from oracle.boruvka_steps import CpuStepper
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     lo, hi = edge_range(len(u), rank, world)
     st = CpuStepper(n, u, v, w, lo, hi, thr, ranks=world if owner_hooks else 1)
+    st.rs = use_rs
 
     def ar(t):
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
@@ -41,24 +44,26 @@ def _worker(rank, world, port, n, u, v, w, thr, out, owner_hooks):
     def ar_max(t):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
 
-    rounds = run_rounds(st, ar, allreduce_max=ar_max)
+    rounds = run_rounds(st, ar, allreduce_max=ar_max, rs=TorchRs() if use_rs else None)
     total, count = st.finish()
     out[rank] = (st.in_mst.tolist(), total, count, rounds, st.hooks_exchanged)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run(world, n, u, v, w, thr, owner_hooks=True):
+def _run(world, n, u, v, w, thr, owner_hooks=True, use_rs=False):
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), n, u, v, w, thr, out, owner_hooks), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), n, u, v, w, thr, out, owner_hooks, use_rs), nprocs=world,
+             join=True)
     return dict(out)
 
 
-@pytest.mark.parametrize("world,name,levels,owner_hooks", [(2, "ties_4.json", 1, True), (2, "cgf_n1000_p001.json", 3, True),
-                                                           (3, "ties_2.json", 2, True), (2, "ties_5.json", 3, True),
-                                                           (2, "ties_5.json", 3, False)])
-def test_gloo_ranks_match_kruskal(world, name, levels, owner_hooks):
+@pytest.mark.parametrize("world,name,levels,owner_hooks,use_rs", [
+    (2, "ties_4.json", 1, True, False), (2, "cgf_n1000_p001.json", 3, True, False),
+    (3, "ties_2.json", 2, True, False), (2, "ties_5.json", 3, True, False), (2, "ties_5.json", 3, False, False),
+    (2, "cgf_n1000_p001.json", 3, True, True), (3, "ties_2.json", 2, True, True), (3, "ties_5.json", 3, True, True)])
+def test_gloo_ranks_match_kruskal(world, name, levels, owner_hooks, use_rs):
     from oracle import oracle
     fx = load_fixture(name)
     n = fx["num_nodes"]
@@ -67,7 +72,7 @@ def test_gloo_ranks_match_kruskal(world, name, levels, owner_hooks):
     ref_in, ref_tw, ref_k = oracle.kruskal_c(n, u, v, w)
     qs = np.quantile(w, np.linspace(0, 1, levels + 1)[1:-1]).astype(np.int64).tolist() if levels > 1 else []
     thr = [0] + sorted(set(int(q) + 1 for q in qs)) + [1 << 32]
-    out = _run(world, n, u, v, w, thr, owner_hooks)
+    out = _run(world, n, u, v, w, thr, owner_hooks, use_rs)
     assert len(out) == world
     flags = np.zeros(len(u), np.uint8)
     for rank in range(world):

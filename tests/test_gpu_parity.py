@@ -209,8 +209,10 @@ def _emulate_ranks(e, world, cfg=None, bitmaps=True, rs=False):
                 for r, st in enumerate(steppers):
                     st.hook_owner(r, per, pairs)
                 assert not bool((pairs == -2).any())  # every slot written by its owner
-                for st in steppers:
-                    st.apply_hooks(pairs)
+                partial = [st.apply_hooks(pairs) for st in steppers]
+                tot = sum(pt.clone() for pt in partial)  # the SUM all-reduce of the partial totals
+                for pt in partial:
+                    pt.copy_(tot)
             elif counts[0]:
                 dense = [s.pack(counts[0]).clone() for s in steppers]
                 red = dense[0]

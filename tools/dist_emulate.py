@@ -123,9 +123,15 @@ def main():
                     _, t = timed(r, lambda: s.hook_owner(r, per, pairs))
                     ms[r] += t
                 coll.append(("allgather_pairs", per * 8))
+                partial = []
                 for r, s in enumerate(steppers):
-                    _, t = timed(r, lambda: s.apply_hooks(pairs))
+                    pt, t = timed(r, lambda: s.apply_hooks(pairs))
+                    partial.append(pt)
                     ms[r] += t
+                tot = sum(pt.clone() for pt in partial)
+                for pt in partial:
+                    pt.copy_(tot)
+                coll.append(("allreduce_sum_u64", 16))
             elif counts[0]:
                 slots = [None] if args.no_inplace else [s.best_slots() for s in steppers]
                 if slots[0] is not None:  # the library loop's in-place uint64 MIN (not timed)
