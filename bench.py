@@ -329,6 +329,31 @@ def make_workload(args, world):
     return edges, tag, cfg
 
 
+def dist_engine(edges, rank, world, dist, backend):
+    """N > 1: DistributedMST with the library's round loop over its own RCCL communicator; if that
+    fails on any rank (setup or the first solve; the ranks agree on it), every rank falls back to
+    the torch.distributed loop (run_rounds) and the line names the loop that ran."""
+    import torch
+    from distributed_ghs_implementation_amd.distributed import DistributedMST
+    eng, err = None, None
+    try:
+        eng = DistributedMST(edges, rank, world)
+        eng.run()
+    except Exception as ex:  # noqa: BLE001 (reported in the line, then the fallback)
+        err = ex
+    flag = torch.tensor([1 if err is not None else 0], dtype=torch.int32,
+                        device="cuda" if backend == "nccl" else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    if not int(flag.item()):
+        return eng, "library (ghs_solver_run over its own RCCL communicator)" if eng.native else "run_rounds"
+    print(f"rank {rank}: library loop failed ({err or 'on another rank'}); torch.distributed loop instead",
+          file=sys.stderr)
+    if eng is not None:
+        eng.close()
+    eng = DistributedMST(edges, rank, world, native=False)
+    return eng, f"run_rounds over torch.distributed (the library loop failed: {err or 'on another rank'})"
+
+
 def time_steps(step, steps, warmup, world, dist):
     import torch
     for _ in range(warmup):
@@ -389,8 +414,9 @@ def main():
     n, m = edges.n, edges.m
     cfg.update({"n": n, "m": m, "partition": f"canonical edge ranges x{world}", "parallelism": f"edges{world}"})
 
+    loop = None
     if world > 1:
-        eng = DistributedMST(edges, rank, world)
+        eng, loop = dist_engine(edges, rank, world, dist, args.backend)
     else:
         from distributed_ghs_implementation_amd import _native
         custom = args.options or args.dedup_max is not None
@@ -425,6 +451,25 @@ def main():
         if rank == 0:
             print(f"ranks agree: weight {results[-1].total_weight} edges {results[-1].num_mst_edges} eid checksum {chk}",
                   file=sys.stderr)
+
+    parity = None
+    if world > 1:
+        # outside the timed steps: the N-rank MSF (gathered to rank 0) against a one-GPU solve of
+        # the same resident graph on rank 0 — edge for edge
+        eids = eng.collect_mst(0)
+        if rank == 0:
+            ref = DeviceMST(edges)
+            rres, _ = ref.run()
+            ref_eids = torch.nonzero(ref.in_mst[:m]).flatten().to(torch.int64).cpu()
+            got = results[-1]
+            parity = {"against": "one-GPU solve of the same graph (DeviceMST), edge for edge",
+                      "total_weight": got.total_weight, "edges": got.num_mst_edges,
+                      "match": bool(rres.total_weight == got.total_weight and rres.num_mst_edges == got.num_mst_edges
+                                    and torch.equal(ref_eids, eids.cpu()))}
+            if not parity["match"]:
+                print(f"N={world} MSF differs from the one-GPU solve: {parity}", file=sys.stderr)
+            del ref, ref_eids
+            torch.cuda.empty_cache()
 
     ktab, s1, _ = profile_step(eng.run, n)
     # the canonical passes are also timed inside the timed steps (two events per pass, no idle
@@ -474,6 +519,8 @@ def main():
                 "cpu_baseline_networkx": cpu_nx, "end_to_end": e2e, "kernels": kernels,
                 "mst": {"total_weight": res0.total_weight, "edges": res0.num_mst_edges}, "breakdown": breakdown}
         if world > 1:
+            line["loop"] = loop
+            line["parity"] = parity
             line["ms_per_step_solve"] = round(dt_solve * 1e3 / args.steps, 4)
             line["step"] = "solve + gather of the MSF edge ids to rank 0 (collect_results)"
     del eng

@@ -2446,7 +2446,7 @@ __global__ __launch_bounds__(BM_T) void k_bmin(const uint4 *__restrict__ rec, co
   const bool noop = guard_nact && *guard_nact <= 1;
   const uint64_t T = noop ? 0 : in.prefix[in.nseg];
   const uint64_t R2 = 2 * bk_quota(T);  // record region stride
-  const uint32_t t = blockIdx.x, tb = t << BS;
+  const uint32_t t = blockIdx.x;
   uint32_t cnt = 0, st = 0;
   if (threadIdx.x < BK_G && !noop) {
     st = O[(uint64_t)t * BK_G + threadIdx.x];

@@ -56,3 +56,21 @@ def test_setup_failure_fails_every_rank(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     v = json.loads(out.read_text())
     assert v == {"world": 3, "codes": [_native.GHS_E_STATE, _native.GHS_E_NOMEM, _native.GHS_E_STATE]}
+
+
+def test_bench_two_ranks_sharing_the_gpu(tmp_path):
+    """bench.py's N > 1 leg (gloo, both ranks on the one GPU, R-MAT s16): the line names the loop
+    that ran and its MSF matches a one-GPU solve of the same graph edge for edge."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo", "--scale", "16",
+           "--steps", "2", "--warmup", "1"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["loop"] == "run_rounds"
+    assert line["parity"]["match"] is True, line["parity"]
