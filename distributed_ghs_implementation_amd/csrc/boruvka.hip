@@ -2359,10 +2359,12 @@ constexpr int BM_ILP = GHS_BM_ILP;
 // The LDS core of a bucketed round (k_bmin over records, k_wmin over a window of the level's edge
 // list): `sweep(f)` calls f(a, b, key) for every candidate edge of bucket t (block-wide: every
 // thread calls it, each thread gets its share); s_min holds KEY_NONE in every slot.
-template <uint32_t BS, class Sweep>
+// FULL (level 0's windowed round 0): best and par of EVERY vertex of the bucket below n are written
+// (KEY_NONE / itself where nothing hooks), so the solve starts without initialising them.
+template <uint32_t BS, bool FULL, class Sweep>
 __device__ __forceinline__ void bucket_round(uint32_t t, unsigned long long *s_min, Sweep sweep,
                                              uint32_t *__restrict__ par, uint64_t *__restrict__ best,
-                                             uint8_t *__restrict__ in_mst) {
+                                             uint8_t *__restrict__ in_mst, uint32_t n) {
   constexpr uint32_t SPAN = 1u << BS;
   const uint32_t tb = t << BS;
   // sweep 1: every target's minimum. A hot end (HOT_MARK) is never this bucket's target. A plain
@@ -2383,6 +2385,8 @@ __device__ __forceinline__ void bucket_round(uint32_t t, unsigned long long *s_m
     if (v != KEY_NONE) {
       best[tb + i] = v;
       in_mst[(uint32_t)v] = 1;
+    } else if (FULL && tb + i < n) {
+      best[tb + i] = KEY_NONE;
     }
   }
   __syncthreads();
@@ -2428,15 +2432,28 @@ __device__ __forceinline__ void bucket_round(uint32_t t, unsigned long long *s_m
   for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) {
     const uint64_t v = s_min[i];
     if ((uint32_t)v == (uint32_t)TAG) par[tb + i] = (uint32_t)(v >> 32);
+    else if (FULL && tb + i < n) par[tb + i] = tb + i;
   }
 }
 
+// FULL: a bucket without candidates still initialises its vertices (see bucket_round)
 template <uint32_t BS>
+__device__ __forceinline__ void bucket_ident(uint32_t t, uint32_t *__restrict__ par, uint64_t *__restrict__ best,
+                                             uint32_t n) {
+  const uint32_t tb = t << BS;
+  for (uint32_t i = threadIdx.x; i < (1u << BS); i += BM_T) {
+    if (tb + i >= n) break;
+    best[tb + i] = KEY_NONE;
+    par[tb + i] = tb + i;
+  }
+}
+
+template <uint32_t BS, bool FULL = false>
 __global__ __launch_bounds__(BM_T) void k_bmin(const uint4 *__restrict__ rec, const uint32_t *__restrict__ O,
                                                SegView in, uint32_t *__restrict__ par, uint64_t *__restrict__ best,
                                                uint8_t *__restrict__ in_mst,
                                                const unsigned long long *__restrict__ guard_nact,
-                                               const unsigned long long *__restrict__ only_if) {
+                                               const unsigned long long *__restrict__ only_if, uint32_t n = 0) {
   constexpr uint32_t SPAN = 1u << BS;
   __shared__ unsigned long long s_min[SPAN];
   __shared__ uint64_t s_pos[BK_G];  // non-empty run i: its first record's position
@@ -2455,7 +2472,10 @@ __global__ __launch_bounds__(BM_T) void k_bmin(const uint4 *__restrict__ rec, co
   // records before each run (scan of the counts), then the non-empty runs' slots (scan of their flags)
   uint32_t R, NZ;
   const uint32_t before = block_excl_scan<BM_T>(cnt, s_wsum, &R);
-  if (R == 0) return;  // block-uniform: no record of this bucket
+  if (R == 0) {  // block-uniform: no record of this bucket
+    if (FULL) bucket_ident<BS>(t, par, best, n);
+    return;
+  }
   const uint32_t zi = block_excl_scan<BM_T>(cnt ? 1u : 0u, s_wsum, &NZ);
   if (cnt) {
     s_pos[zi] = R2 * threadIdx.x + st;
@@ -2489,7 +2509,7 @@ __global__ __launch_bounds__(BM_T) void k_bmin(const uint4 *__restrict__ rec, co
       for (int j = 0; j < BM_ILP; ++j) f(a[j], b[j], k[j]);
     }
   };
-  bucket_round<BS>(t, s_min, sweep, par, best, in_mst);
+  bucket_round<BS, FULL>(t, s_min, sweep, par, best, in_mst, n);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2577,7 +2597,7 @@ __global__ __launch_bounds__(BM_T) void k_wmin(const uint32_t *__restrict__ src,
                                                const uint64_t *__restrict__ key, SegView in, uint32_t nb,
                                                const uint64_t *__restrict__ start, uint32_t *__restrict__ par,
                                                uint64_t *__restrict__ best, uint8_t *__restrict__ in_mst,
-                                               const unsigned long long *__restrict__ long_flag) {
+                                               const unsigned long long *__restrict__ long_flag, uint32_t n) {
   constexpr uint32_t SPAN = 1u << BS;
   __shared__ unsigned long long s_min[SPAN];
   __shared__ uint32_t s_seg[2];
@@ -2588,7 +2608,10 @@ __global__ __launch_bounds__(BM_T) void k_wmin(const uint32_t *__restrict__ src,
   const uint32_t t = ((j / WM_CHUNK) * 8 + blockIdx.x % 8) * WM_CHUNK + j % WM_CHUNK;
   if (t >= nb || *long_flag) return;
   const uint64_t wlo = start[t ? t - 1 : 0], whi = start[t + 1 < nb ? t + 1 : nb];
-  if (whi <= wlo) return;  // block-uniform: no edge with an end in this bucket
+  if (whi <= wlo) {  // block-uniform: no edge with an end in this bucket
+    bucket_ident<BS>(t, par, best, n);
+    return;
+  }
   if (threadIdx.x == 0) {
     s_seg[0] = seg_find(in.prefix, 0, in.nseg - 1, wlo);
     s_seg[1] = seg_find(in.prefix, 0, in.nseg - 1, whi - 1);
@@ -2619,7 +2642,7 @@ __global__ __launch_bounds__(BM_T) void k_wmin(const uint32_t *__restrict__ src,
       }
     }
   };
-  bucket_round<BS>(t, s_min, sweep, par, best, in_mst);
+  bucket_round<BS, true>(t, s_min, sweep, par, best, in_mst, n);
 }
 
 // The hot fragments' CONNECT in a bucketed level-first round (one thread each): a fragment's
@@ -3298,6 +3321,7 @@ struct ghs_solver {
   uint4 *rec = nullptr;         // records (a, b, key): 16 B each
   uint64_t *wstart = nullptr;   // windowed round 0: each bucket's first edge (nb + 1)
   bool windowed = true;         // level 0 round 0 of a lattice-like solve windowed (k_wmin)
+  bool state_init_pending = false;  // one rank: best / par initialised by level 0's first round
   uint32_t *bk_off = nullptr;
   uint32_t bk_bs = 13, bk_nb = 0;
   bool bucketed = false;        // this solve runs bucketed rounds (decided once the plan landed)
@@ -3998,7 +4022,7 @@ constexpr bool BK_RANDOM_L0 = GHS_BK_RANDOM_L0;
 // bucket's targets
 static void enqueue_bmin(ghs_solver *s, const uint32_t *a, const uint32_t *b, const uint64_t *k, SegView in,
                          const unsigned long long *guard, uint64_t items, const uint32_t *hot,
-                         const unsigned long long *only_if = nullptr) {
+                         const unsigned long long *only_if = nullptr, bool full = false) {
   {
     KT(GHS_K_BUCKET, items);
     k_bucket<<<BK_G, BK_T, 0, s->stream>>>(a, b, k, in, s->bk_bs, s->bk_nb, s->rec, s->bk_off, guard, hot, s->best,
@@ -4006,16 +4030,26 @@ static void enqueue_bmin(ghs_solver *s, const uint32_t *a, const uint32_t *b, co
   }
   {
     KT(GHS_K_BMIN, items);
-    if (s->bk_bs == 13)
+    if (full) {  // level 0's windowed round falling back: every vertex's best / par written
+      if (s->bk_bs == 13)
+        k_bmin<13, true><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard,
+                                                           only_if, s->n);
+      else
+        k_bmin<14, true><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard,
+                                                           only_if, s->n);
+    } else if (s->bk_bs == 13) {
       k_bmin<13><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard, only_if);
-    else
+    } else {
       k_bmin<14><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard, only_if);
+    }
   }
   if (hot) {
     KT(GHS_K_HOT_HOOK, 0);
     k_hot_hook<<<1, HOT_K, 0, s->stream>>>(hot, s->best, s->eu, s->ev, s->lab, s->par, s->in_mst, s->cnt + C_ERR);
   }
 }
+
+static int enqueue_state_init(ghs_solver *s);
 
 static int enqueue_minedge(ghs_solver *s) {
   const bool timed = s->detail || (s->time_rounds && s->level_round >= 1);
@@ -4028,11 +4062,18 @@ static int enqueue_minedge(ghs_solver *s) {
                                       : ((s->level == 0 && s->nact >= BUCKET_MIN_ACTIVE) ||
                                          (BK_LEVEL_FIRST && s->level > 0 && s->level_round == 0) ||
                                          (s->cfg.options & GHS_OPT_BUCKETED)));
+  const bool windowed0 = s->level_round == 0 && (s->cur_arcs || !s->arcs_known) && s->round_bucketed &&
+                         s->level == 0 && s->lattice && s->windowed;
+  if (s->state_init_pending) {
+    s->state_init_pending = false;
+    if (!windowed0)
+      if (int rc = enqueue_state_init(s)) return rc;
+  }
   if (s->level_round == 0) {
     if (s->cur_arcs || !s->arcs_known) {
       const unsigned g = s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->ident_g) : s->ident_g;
       const uint64_t items = s->arcs_known ? s->cur_arcs : 0;
-      if (s->round_bucketed && s->level == 0 && s->lattice && s->windowed) {
+      if (windowed0) {
         // windowed round 0 (k_wmin over the edge list); k_bucket / k_bmin run instead only if a
         // level-0 edge spans more than one bucket (k_select's flag)
         const unsigned long long *far = s->cnt + C_LONG;
@@ -4047,12 +4088,12 @@ static int enqueue_minedge(ghs_solver *s) {
           const unsigned wg = 8 * WM_CHUNK * ((s->bk_nb + 8 * WM_CHUNK - 1) / (8 * WM_CHUNK));
           if (s->bk_bs == 13)
             k_wmin<13><<<wg, BM_T, 0, s->stream>>>(I.src, I.dst, I.key, in, s->bk_nb, s->wstart, s->par, s->best,
-                                                  s->in_mst, far);
+                                                  s->in_mst, far, s->n);
           else
             k_wmin<14><<<wg, BM_T, 0, s->stream>>>(I.src, I.dst, I.key, in, s->bk_nb, s->wstart, s->par, s->best,
-                                                  s->in_mst, far);
+                                                  s->in_mst, far, s->n);
         }
-        enqueue_bmin(s, I.src, I.dst, I.key, in, nullptr, items, nullptr, far);
+        enqueue_bmin(s, I.src, I.dst, I.key, in, nullptr, items, nullptr, far, true);
       } else if (s->round_bucketed) {
         // the level's edges carry roots (past level 0: resolved, and the giant is one of them)
         enqueue_bmin(s, I.src, I.dst, I.key, in, nullptr, items, s->level > 0 ? s->giant + GIANT_HOT : nullptr);
@@ -4393,6 +4434,16 @@ size_t ghs_workspace_bytes(uint32_t n, uint64_t m, uint64_t local_edges) {
   return workspace_layout(n, m, local_edges, nullptr, nullptr);
 }
 
+// Every vertex a root without a candidate: best = KEY_NONE, par = itself.
+static int enqueue_state_init(ghs_solver *s) {
+  KT(GHS_K_INIT, s->n);
+  hipError_t e;
+  if ((e = hipMemsetAsync(s->best, 0xff, (size_t)s->n * 8, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset best: ") + hipGetErrorString(e));
+  k_iota<<<grid_for(s->n, 256, 8192), 256, 0, s->stream>>>(s->par, s->n);  // every root: par[r] == r
+  GHS_HIP_CHECK(hipGetLastError());
+  return GHS_OK;
+}
+
 // The per-solve start of a solver: plan, state arrays, counters (create, and reset between solves).
 static int solver_begin(ghs_solver *s) {
   hipError_t e;
@@ -4409,9 +4460,14 @@ static int solver_begin(ghs_solver *s) {
     // several ranks with dense levels: every level runs on the dense arrays (k_dense_open sets
     // them up), so the vertex-sized best / par are never read — only lab is (s26: 805 MB of
     // writes per rank saved)
+    // one rank: best / par are initialised in front of level 0's first round, or not at all when
+    // that round is the windowed one (its kernels write every vertex's slots: grid 3 GB of writes)
     if (!s->dense_mode) {
-      if ((e = hipMemsetAsync(s->best, 0xff, (size_t)n * 8, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset best: ") + hipGetErrorString(e));
-      k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->par, n);  // every root: par[r] == r
+      if (s->cfg.num_ranks <= 1) {
+        s->state_init_pending = true;
+      } else if (int rc = enqueue_state_init(s)) {
+        return rc;
+      }
     }
     k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->lab, n);
   }
