@@ -3633,12 +3633,14 @@ static void default_config(ghs_config_t *c) {
 // level1_edges_per_vertex <= 0 picks the first level's size from the density. The first level
 // should just reach the point where a giant fragment forms (the filter of the later levels drops
 // the edges inside it) without paying for an extra level of n-sized passes: 0.5n edges for dense
-// random-like graphs (R-MAT s24: 6.18 ms vs 6.98 at 1.0n), n edges for sparse lattice-like ones
-// (bond percolation of the square lattice at half the edges; 16384^2 grid: 56 ms vs 72 at 0.5n;
-// profiles/r01/sweep_levels_*.jsonl).
+// random-like graphs (R-MAT s24: 6.18 ms vs 6.98 at 1.0n), 1.2n for sparse lattice-like ones
+// (just past bond percolation of the square lattice at half the edges; 16384^2 grid: 56 ms vs 72
+// at 0.5n, profiles/r01/sweep_levels_*.jsonl; r03 with the bucketed level-0 rounds, two sweeps:
+// grid 39.1 / 40.1 ms at 1.0n -> 38.8 / 39.4 at 1.2n, gradient grid 15.9 / 16.0 -> 15.7 / 15.3,
+// profiles/r03/sweeps/; R-MAT 0.35-0.5n within the noise).
 static double level1_auto(const ghs_config_t &c, uint32_t n, uint64_t m) {
   if (c.level1_edges_per_vertex > 0) return c.level1_edges_per_vertex;
-  return (m >= 4ull * n) ? 0.5 : 1.0;
+  return (m >= 4ull * n) ? 0.5 : 1.2;
 }
 
 // ---- level planning: thresholds from a sample of the GLOBAL canonical weights ----------------

@@ -83,7 +83,7 @@ typedef struct ghs_result {
  * level1_edges_per_vertex * n lightest edges, each further level level_growth times more, the
  * last level the rest; max_levels = 1 runs plain Boruvka over every edge at once. Thresholds
  * are weight quantiles of a fixed sample of the canonical list, so every rank plans the same
- * levels. level1_edges_per_vertex <= 0 (the default) = auto: 0.5 when m >= 4n, else 1.0.
+ * levels. level1_edges_per_vertex <= 0 (the default) = auto: 0.5 when m >= 4n, else 1.2.
  * Results do not depend on the plan (only speed does).
  * ABI 5: every path option lives here (the library reads no environment variable that changes the
  * algorithm or a launch shape); options = 0 and dedup_max = 0 select the default path. */

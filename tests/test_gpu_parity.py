@@ -596,7 +596,7 @@ def _host_plan(w, n, m, max_levels=8, l1=0.0, growth=8.0, nsample=16384):
     """The level plan's formula (boruvka.hip k_plan, level1_auto) restated: order statistics of
     an evenly spaced weight sample."""
     if l1 <= 0:
-        l1 = 0.5 if m >= 4 * n else 1.0
+        l1 = 0.5 if m >= 4 * n else 1.2
     L = max(1, min(max_levels, 32))
     thr = [0]
     if L > 1 and m > 0:
