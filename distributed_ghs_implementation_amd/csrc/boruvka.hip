@@ -4239,24 +4239,31 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
 // is queried only after SLOT_QUIET_MS of waiting: hipStreamQuery enqueues a marker behind the
 // last launch, and its system-scope release idled the GPU ~5.6 us before every round >= 2.
 constexpr int SLOT_QUIET_MS = 20;
+constexpr int SLOT_QUERY_MS = 5;
 static int wait_slot(ghs_solver *s, const RoundSlot *hs, unsigned long long seq) {
   if (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) == seq) return GHS_OK;
   const auto t0 = std::chrono::steady_clock::now();
   unsigned spins = 0;
   bool quiet = true;
+  auto last_query = t0;
   while (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) != seq) {
     if ((spins & 255) == 0 && solver_cancelled(s)) GHS_FAIL(GHS_E_STATE, "cancelled: another rank of the solve failed");
     if ((++spins & 255) == 0 && quiet)
       quiet = std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(SLOT_QUIET_MS);
     if (!quiet) {
-      // a long wait (a multi-rank solve's peers share the device, or the stream failed): check the
-      // stream now and then, sleeping between checks (a runtime call per spin from several rank
-      // threads starved the other ranks' launches: one emulated s26 x8 solve took 5.7 s)
+      // a long wait (a multi-rank solve's peers share the device, or the stream failed): sleep
+      // between polls and query the stream only every SLOT_QUERY_MS — each query enqueues a marker
+      // whose system-scope release idles the GPU, and 8 emulated rank threads querying every 50 us
+      // fed back into ever longer waits (emulated s26 x8 solves of 3-6 s instead of ~80 ms)
       std::this_thread::sleep_for(std::chrono::microseconds(50));
-      const hipError_t q = hipStreamQuery(s->stream);
-      if (q != hipSuccess && q != hipErrorNotReady) GHS_HIP_CHECK(q);
-      if (q == hipSuccess && __atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) != seq)
-        GHS_FAIL(GHS_E_STATE, "round report missing after the stream drained");
+      const auto now = std::chrono::steady_clock::now();
+      if (now - last_query >= std::chrono::milliseconds(SLOT_QUERY_MS)) {
+        last_query = now;
+        const hipError_t q = hipStreamQuery(s->stream);
+        if (q != hipSuccess && q != hipErrorNotReady) GHS_HIP_CHECK(q);
+        if (q == hipSuccess && __atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) != seq)
+          GHS_FAIL(GHS_E_STATE, "round report missing after the stream drained");
+      }
     }
   }
   return GHS_OK;
