@@ -116,6 +116,10 @@ def launch_bytes(rec, stats, res, n):
         return 40.0 * bucketed_edges  # pass A a, b (8 B) + pass B edge in (16 B) + record out (16 B)
     if k == "k_bmin":
         return 32.0 * bucketed_edges  # two sweeps over the records
+    if k == "k_wmin":
+        # level 0's windowed round: every edge read by the windows of its two buckets (a, b, key
+        # twice), best + par of every vertex written
+        return 32.0 * live + 12.0 * n
     # rounds >= 1 of one rank with >= 1M active fragments launch both CONNECT forms and the
     # device runs one (boruvka.hip k_win / k_hook guards: edge form while the survivors are
     # fewer than 4x the active fragments)
@@ -133,7 +137,7 @@ def launch_bytes(rec, stats, res, n):
     return 0.0
 
 
-STAGE1 = ("k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>", "k_bucket", "k_bmin")
+STAGE1 = ("k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>", "k_bucket", "k_bmin", "k_wstarts", "k_wmin")
 
 
 def kernel_table(records, stats, res, n):
@@ -167,7 +171,7 @@ def stage1_roofline(records, stats):
 # profile name -> the PMC file's kernel-name prefix (rocprofv3 prints every template argument:
 # k_minedge<false, true, false>; any later template parameter still matches the prefix)
 PMC_NAMES = {"k_minedge<IDENT>": "k_minedge<true, false", "k_minedge<COMPACT>": "k_minedge<false, true",
-             "k_bmin": "k_bmin<"}
+             "k_bmin": "k_bmin<", "k_wmin": "k_wmin<"}
 
 
 def _pmc_match(name, key):
