@@ -13,7 +13,7 @@ python3 tools/prof_summary.py "$OUT/prof/run_results.db" > "$OUT/kernels.md" && 
 f=$(find "$OUT/prof" -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && cp "$f" "$OUT/kernel_stats.csv"
 rm -rf "$OUT/prof"
 fi
-KRE="k_filter|k_select|k_minedge|k_level_pass|k_win|k_bucket|k_bmin|k_jump_ident|k_jump|k_hook"
+KRE="k_filter|k_select|k_minedge|k_level_pass|k_win|k_wmin|k_bucket|k_bmin|k_jump_ident|k_jump|k_hook"
 for spec in ${PMC_SPECS:-rmat:rmat-s24-ef16 grid:grid-16384x16384 grid-gradient:grid-gradient-16384x16384}; do
   wl=${spec%%:*}; tag=${spec#*:}
   TAG=${TAG:-ev3}/pmc_$wl KRE="$KRE" WL=$tag BENCH_ARGS="--workload $wl --no-scaling-base" bash tools/gpu/pmc_traffic.sh || { echo "pmc $wl failed"; exit 1; }
