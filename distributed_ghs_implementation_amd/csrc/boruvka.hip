@@ -2361,10 +2361,15 @@ constexpr int BM_ILP = GHS_BM_ILP;
 // thread calls it, each thread gets its share); s_min holds KEY_NONE in every slot.
 // FULL (level 0's windowed round 0): best and par of EVERY vertex of the bucket below n are written
 // (KEY_NONE / itself where nothing hooks), so the solve starts without initialising them.
+// eu != nullptr (level 0: the labels are the vertices): a target's winner comes from its minimum's
+// canonical ends (two gathers per target) instead of a second sweep over the candidates (k_wmin:
+// its window is four times the bucket's edges and does not stay in L2 — PMC: every edge read 4x)
 template <uint32_t BS, bool FULL, class Sweep>
 __device__ __forceinline__ void bucket_round(uint32_t t, unsigned long long *s_min, Sweep sweep,
                                              uint32_t *__restrict__ par, uint64_t *__restrict__ best,
-                                             uint8_t *__restrict__ in_mst, uint32_t n) {
+                                             uint8_t *__restrict__ in_mst, uint32_t n,
+                                             const uint32_t *__restrict__ eu = nullptr,
+                                             const uint32_t *__restrict__ ev = nullptr) {
   constexpr uint32_t SPAN = 1u << BS;
   const uint32_t tb = t << BS;
   // sweep 1: every target's minimum. A hot end (HOT_MARK) is never this bucket's target. A plain
@@ -2394,10 +2399,19 @@ __device__ __forceinline__ void bucket_round(uint32_t t, unsigned long long *s_m
   // slot by a tag carrying the other end (bit 31 set: a key's eid is < 2^31, so a tag never equals
   // a key, and KEY_NONE's low word is not the tag's)
   constexpr uint64_t TAG = 0x80000000ull;
-  sweep([&](uint32_t a, uint32_t b, unsigned long long k) {
-    if ((a >> BS) == t && s_min[a - tb] == k) s_min[a - tb] = ((uint64_t)(b & ~HOT_MARK) << 32) | TAG;
-    if ((b >> BS) == t && s_min[b - tb] == k) s_min[b - tb] = ((uint64_t)(a & ~HOT_MARK) << 32) | TAG;
-  });
+  if (eu) {
+    for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) {
+      const uint64_t v = s_min[i];
+      if (v == KEY_NONE) continue;
+      const uint32_t eid = (uint32_t)v, a = eu[eid], b = ev[eid];
+      s_min[i] = ((uint64_t)(a == tb + i ? b : a) << 32) | TAG;
+    }
+  } else {
+    sweep([&](uint32_t a, uint32_t b, unsigned long long k) {
+      if ((a >> BS) == t && s_min[a - tb] == k) s_min[a - tb] = ((uint64_t)(b & ~HOT_MARK) << 32) | TAG;
+      if ((b >> BS) == t && s_min[b - tb] == k) s_min[b - tb] = ((uint64_t)(a & ~HOT_MARK) << 32) | TAG;
+    });
+  }
   __syncthreads();
   // Hook chains inside the bucket, compressed here so the jump walks fewer random steps (a
   // lattice's horizontal hooks stay in their row's bucket). First a mutual pair inside the bucket
@@ -2592,12 +2606,17 @@ __global__ __launch_bounds__(256) void k_wstarts(SegView in, const uint32_t *__r
 }
 
 constexpr uint32_t WM_CHUNK = 32;
+#ifndef GHS_WM_GATHER
+#define GHS_WM_GATHER 1
+#endif
+constexpr bool WM_GATHER = GHS_WM_GATHER;  // k_wmin: winners from the canonical ends (bucket_round)
 template <uint32_t BS>
 __global__ __launch_bounds__(BM_T) void k_wmin(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
                                                const uint64_t *__restrict__ key, SegView in, uint32_t nb,
                                                const uint64_t *__restrict__ start, uint32_t *__restrict__ par,
                                                uint64_t *__restrict__ best, uint8_t *__restrict__ in_mst,
-                                               const unsigned long long *__restrict__ long_flag, uint32_t n) {
+                                               const unsigned long long *__restrict__ long_flag, uint32_t n,
+                                               const uint32_t *__restrict__ eu, const uint32_t *__restrict__ ev) {
   constexpr uint32_t SPAN = 1u << BS;
   __shared__ unsigned long long s_min[SPAN];
   __shared__ uint32_t s_seg[2];
@@ -2642,7 +2661,7 @@ __global__ __launch_bounds__(BM_T) void k_wmin(const uint32_t *__restrict__ src,
       }
     }
   };
-  bucket_round<BS, true>(t, s_min, sweep, par, best, in_mst, n);
+  bucket_round<BS, true>(t, s_min, sweep, par, best, in_mst, n, eu, ev);
 }
 
 // The hot fragments' CONNECT in a bucketed level-first round (one thread each): a fragment's
@@ -4090,10 +4109,10 @@ static int enqueue_minedge(ghs_solver *s) {
           const unsigned wg = 8 * WM_CHUNK * ((s->bk_nb + 8 * WM_CHUNK - 1) / (8 * WM_CHUNK));
           if (s->bk_bs == 13)
             k_wmin<13><<<wg, BM_T, 0, s->stream>>>(I.src, I.dst, I.key, in, s->bk_nb, s->wstart, s->par, s->best,
-                                                  s->in_mst, far, s->n);
+                                                  s->in_mst, far, s->n, WM_GATHER ? s->eu : nullptr, s->ev);
           else
             k_wmin<14><<<wg, BM_T, 0, s->stream>>>(I.src, I.dst, I.key, in, s->bk_nb, s->wstart, s->par, s->best,
-                                                  s->in_mst, far, s->n);
+                                                  s->in_mst, far, s->n, WM_GATHER ? s->eu : nullptr, s->ev);
         }
         enqueue_bmin(s, I.src, I.dst, I.key, in, nullptr, items, nullptr, far, true);
       } else if (s->round_bucketed) {
