@@ -86,7 +86,9 @@ def _first_round(stats, r):
     return r == 0 or stats[r - 1]["level"] != stats[r]["level"]
 
 
-def launch_bytes(rec, stats, res, n):
+def launch_bytes(rec, stats, res, n, windowed=frozenset()):
+    """`windowed`: the rounds whose windowed kernel (k_wmin) did the work — their k_bucket / k_bmin
+    launches are the device-side fallback that exited at once (k_select's span flag unset)."""
     k = rec["kernel"]
     if k == "k_select":
         return 12.0 * res.canon_edges + 16.0 * res.select_out  # u, v, w in; level-0 edges out
@@ -111,6 +113,10 @@ def launch_bytes(rec, stats, res, n):
         return 24.0 * live + 16.0 * _next_live(stats, r)  # + lab[a], lab[b]; survivors out
     # bucketed rounds: a level's first round buckets its edges, later rounds their compacted
     # survivors; an edge is at least one record (a, b, key: 16 B)
+    if k in ("k_bucket", "k_bmin") and r in windowed:
+        return 0.0
+    if k == "k_wmin" and r not in windowed:
+        return 0.0  # exited at once: the fallback bucketed the round
     bucketed_edges = live if _first_round(stats, r) else _next_live(stats, r)
     if k == "k_bucket":
         return 40.0 * bucketed_edges  # pass A a, b (8 B) + pass B edge in (16 B) + record out (16 B)
@@ -143,11 +149,18 @@ STAGE1 = ("k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>", "k_bucket", "
 def kernel_table(records, stats, res, n):
     """Per kernel: launches, ms per step, algorithmic bytes, achieved GB/s (one profiled step)."""
     tab = {}
+    # a round with k_wmin ran windowed unless its fallback k_bmin took longer (the span flag)
+    per_round = {}
+    for rec in records:
+        if rec["kernel"] in ("k_wmin", "k_bmin"):
+            per_round.setdefault(rec["round"], {}).setdefault(rec["kernel"], 0.0)
+            per_round[rec["round"]][rec["kernel"]] += max(rec["ms"], 0.0)
+    windowed = frozenset(r for r, d in per_round.items() if "k_wmin" in d and d["k_wmin"] >= d.get("k_bmin", 0.0))
     for rec in records:
         t = tab.setdefault(rec["kernel"], {"launches": 0, "ms": 0.0, "bytes": 0.0})
         t["launches"] += 1
         t["ms"] += max(rec["ms"], 0.0)
-        t["bytes"] += launch_bytes(rec, stats, res, n)
+        t["bytes"] += launch_bytes(rec, stats, res, n, windowed)
     for t in tab.values():
         t["achieved_gbs"] = t["bytes"] / (t["ms"] * 1e-3) / 1e9 if t["ms"] > 0 and t["bytes"] > 0 else None
         t["ms"] = round(t["ms"], 4)
