@@ -1241,6 +1241,12 @@ __device__ __forceinline__ void add_totals(unsigned long long wsum, unsigned lon
   }
 }
 
+// Path splitting starts after SPLIT_AFTER steps of a walk: a short walk (most of them) then reads
+// only, instead of a random 4-B store per step that no later walk may need.
+#ifndef GHS_SPLIT_AFTER
+#define GHS_SPLIT_AFTER 0
+#endif
+constexpr uint32_t SPLIT_AFTER = GHS_SPLIT_AFTER;
 __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
                                                 uint32_t *par, uint32_t *__restrict__ lab, uint64_t *__restrict__ best,
                                                 uint8_t *__restrict__ flags, unsigned long long *__restrict__ err,
@@ -1263,7 +1269,7 @@ __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act
         x = x < px ? x : px;
         break;
       }
-      if (ppx != px) par[x] = ppx;
+      if (ppx != px && steps >= SPLIT_AFTER) par[x] = ppx;
       x = px;
       px = ppx;
       if (++steps > JUMP_MAX_STEPS) {
@@ -1347,7 +1353,7 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
           walking &= ~(1u << k);
           continue;
         }
-        if (ppx[k] != px[k]) par[x[k]] = ppx[k];
+        if (ppx[k] != px[k] && steps >= SPLIT_AFTER) par[x[k]] = ppx[k];
         x[k] = px[k];
         px[k] = ppx[k];
         if (px[k] == x[k]) walking &= ~(1u << k);
