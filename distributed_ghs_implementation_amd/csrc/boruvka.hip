@@ -1241,10 +1241,13 @@ __device__ __forceinline__ void add_totals(unsigned long long wsum, unsigned lon
   }
 }
 
-// Path splitting starts after SPLIT_AFTER steps of a walk: a short walk (most of them) then reads
-// only, instead of a random 4-B store per step that no later walk may need.
+// k_jump's path splitting starts after SPLIT_AFTER steps of a walk: a short walk (most of them)
+// then only reads, instead of a random 4-B store per step that no later walk may need. 16384^2
+// grid, level 0 rounds 1-3: 2.29 / 1.29 / 0.48 -> 1.85 / 1.17 / 0.43 ms (2 steps; 4 the same).
+// k_jump_ident keeps splitting from the first step: the gradient grid's long hook chains need it
+// (its level-0 jump 1.54 -> 1.83 ms with 2 steps, profiles/r03/ab_split/).
 #ifndef GHS_SPLIT_AFTER
-#define GHS_SPLIT_AFTER 0
+#define GHS_SPLIT_AFTER 2
 #endif
 constexpr uint32_t SPLIT_AFTER = GHS_SPLIT_AFTER;
 __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
@@ -1353,7 +1356,7 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
           walking &= ~(1u << k);
           continue;
         }
-        if (ppx[k] != px[k] && steps >= SPLIT_AFTER) par[x[k]] = ppx[k];
+        if (ppx[k] != px[k]) par[x[k]] = ppx[k];
         x[k] = px[k];
         px[k] = ppx[k];
         if (px[k] == x[k]) walking &= ~(1u << k);
