@@ -250,8 +250,8 @@ def _torch_allgather(group=None):
 class TorchRs:
     """The reduce-scatter protocol's collectives over a torch.distributed group (see run_rounds).
     uint64 keys travel as int64 with the sign bit flipped, so a signed MIN orders them unsigned;
-    nccl reduce-scatters and all-gathers the slices in place, gloo (no in-place reduce-scatter)
-    all-reduces the whole buffer and all-gathers through per-rank chunks."""
+    nccl reduce-scatters into this rank's slice and all-gathers the slices, gloo (no
+    reduce-scatter) all-reduces the whole buffer and all-gathers through per-rank chunks."""
 
     def __init__(self, group=None):
         self.group = group
@@ -262,10 +262,11 @@ class TorchRs:
     def reduce_scatter_min_u64(self, t):
         sign = torch.tensor(-(1 << 63), dtype=torch.int64, device=t.device)
         t.bitwise_xor_(sign)
-        if self.nccl:
+        if self.nccl:  # (a separate output: no aliasing between the collective's buffers)
             per = t.numel() // self.world
-            dist.reduce_scatter_tensor(t[self.rank * per:(self.rank + 1) * per], t, op=dist.ReduceOp.MIN,
-                                       group=self.group)
+            out = torch.empty(per, dtype=t.dtype, device=t.device)
+            dist.reduce_scatter_tensor(out, t, op=dist.ReduceOp.MIN, group=self.group)
+            t[self.rank * per:(self.rank + 1) * per].copy_(out)
         else:
             dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
         t.bitwise_xor_(sign)
