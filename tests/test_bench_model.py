@@ -1,0 +1,48 @@
+"""bench.py's per-kernel byte model and stage-1 roofline on synthetic launch records (no GPU):
+the windowed level-0 round (k_wmin) against its device-side fallback (k_bucket / k_bmin), and the
+PMC kernel-name match of the templated kernels."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+N = 1 << 20
+STATS = [{"level": 0, "live_arcs": 2 * N, "active_components": N, "level_arcs": 2 * N, "hooks": N // 2},
+         {"level": 0, "live_arcs": N, "active_components": N // 4, "level_arcs": 0, "hooks": N // 8}]
+
+
+def _rec(kernel, ms, rnd=0):
+    return {"kernel": kernel, "ms": ms, "round": rnd, "level": 0, "items": 0}
+
+
+def test_windowed_round_charges_k_wmin_only():
+    recs = [_rec("k_wstarts", 0.01), _rec("k_wmin", 1.0), _rec("k_bucket", 0.005), _rec("k_bmin", 0.004)]
+    tab = bench.kernel_table(recs, STATS, None, N)
+    assert tab["k_wmin"]["bytes"] == 32.0 * 2 * N + 12.0 * N
+    assert tab["k_bucket"]["bytes"] == 0.0 and tab["k_bmin"]["bytes"] == 0.0
+
+
+def test_fallback_round_charges_the_bucketed_kernels():
+    recs = [_rec("k_wstarts", 0.01), _rec("k_wmin", 0.003), _rec("k_bucket", 0.8), _rec("k_bmin", 0.9)]
+    tab = bench.kernel_table(recs, STATS, None, N)
+    assert tab["k_wmin"]["bytes"] == 0.0
+    assert tab["k_bucket"]["bytes"] > 0 and tab["k_bmin"]["bytes"] > 0
+
+
+def test_stage1_counts_the_windowed_kernels():
+    recs = [_rec("k_wstarts", 0.01), _rec("k_wmin", 1.0), _rec("k_minedge<COMPACT>", 0.5, 1)]
+    s1 = bench.stage1_roofline(recs, STATS)
+    assert abs(s1["ms"] - 1.51) < 1e-9
+    assert s1["live_edges"] == 3 * N
+    assert "k_wmin" in s1["kernels"]
+
+
+def test_pmc_names_match_templated_kernels():
+    assert bench._pmc_match("k_wmin", "k_wmin<14u>")
+    assert bench._pmc_match("k_bmin", "k_bmin<13u, false>")
+    assert bench._pmc_match("k_minedge<COMPACT>", "k_minedge<false, true, false, true>")
+    assert not bench._pmc_match("k_minedge<IDENT>", "k_minedge<false, true, false, true>")
