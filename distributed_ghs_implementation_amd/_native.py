@@ -44,6 +44,7 @@ EXPORTED_SYMBOLS = (
     "ghs_rmat_temp_bytes", "ghs_rmat_generate", "ghs_rmat_tuples", "ghs_grid_generate",
     "ghs_profile_enable", "ghs_profile_read", "ghs_kernel_name",
     "ghs_comm_unique_id", "ghs_comm_init", "ghs_comm_destroy", "ghs_solver_run", "ghs_mst_emulated",
+    "ghs_release_cache",
 )
 
 
@@ -96,7 +97,7 @@ class RoundStatsList(collections.abc.Sequence):
         return repr(list(self))
 
 
-ABI_VERSION = 6  # include/ghs_mst.h GHS_MST_ABI_VERSION
+ABI_VERSION = 7  # include/ghs_mst.h GHS_MST_ABI_VERSION
 
 
 class Result(ctypes.Structure):
@@ -113,6 +114,12 @@ class Result(ctypes.Structure):
         ("canon_edges", ctypes.c_uint64),
         ("select_out", ctypes.c_uint64),
         ("filter_out", ctypes.c_uint64),
+        # ABI 7: the multi-rank drivers' host phases (max over ranks) and cache reuse
+        ("ms_setup", ctypes.c_double),
+        ("ms_solve", ctypes.c_double),
+        ("ms_gather", ctypes.c_double),
+        ("reused", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
     ]
 
 
@@ -159,6 +166,13 @@ OPT_TIME_ROUNDS = 0x20
 OPT_DETAIL = 0x40
 OPT_BUCKETED_FIRST = 0x80
 OPT_NO_WINDOW = 0x100
+OPT_NO_TAIL = 0x200
+
+# ghs_result_t.pass_flags bits
+PASS_BUCKETED = 0x1
+PASS_LATTICE = 0x2
+PASS_WINDOWED = 0x4
+PASS_TAIL = 0x8
 
 
 class Config(ctypes.Structure):
@@ -172,12 +186,12 @@ class Config(ctypes.Structure):
         ("options", ctypes.c_uint32),
         ("dedup_max", ctypes.c_uint32),
         ("fault_rank", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("fault_round", ctypes.c_uint32),
     ]
 
 
 def make_config(max_levels=None, level1_edges_per_vertex=None, level_growth=None, num_ranks=None, options=None,
-                dedup_max=None, fault_rank=None):
+                dedup_max=None, fault_rank=None, fault_round=None):
     c = Config()
     load().ghs_default_config(ctypes.byref(c))
     if options is not None:
@@ -186,6 +200,8 @@ def make_config(max_levels=None, level1_edges_per_vertex=None, level_growth=None
         c.dedup_max = int(dedup_max)
     if fault_rank is not None:
         c.fault_rank = int(fault_rank)
+    if fault_round is not None:
+        c.fault_round = int(fault_round)
     if num_ranks is not None:
         c.num_ranks = int(num_ranks)
     if max_levels is not None:
@@ -261,6 +277,7 @@ def load():
             "ghs_comm_destroy": (i32, [vp]),
             "ghs_solver_run": (i32, [vp, vp]),
             "ghs_mst_emulated": (i32, [u32, u64, vp, vp, vp, i32, P(Config), vp, P(Result), P(RoundStats)]),
+            "ghs_release_cache": (i32, []),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(L, name)
@@ -312,6 +329,11 @@ class Comm:
             self.close()
         except Exception:
             pass
+
+
+def release_cache():
+    """Free the multi-rank drivers' cached per-rank state (ghs_release_cache)."""
+    check(load().ghs_release_cache())
 
 
 def device_count():

@@ -3344,6 +3344,7 @@ struct ghs_solver {
   bool level_dense = false;     // the open level runs in dense labels
   bool rs_fold = false;         // apply_hooks left partial totals for contract to fold in
   uint64_t dense_n = 0;
+  uint64_t hook_S = 0;          // the padded slot count of the last hook_slots (hook_owner's bound)
   // bucketed rounds (single rank, lattice-like graphs; k_bucket / k_bmin): the record buffers,
   // the offsets table, the bucket geometry, and the per-solve / per-round decisions
   uint4 *rec = nullptr;         // records (a, b, key): 16 B each
@@ -3395,6 +3396,8 @@ uint32_t ghs_solver_ranks_of(const ghs_solver *s) { return s->cfg.num_ranks; }
 // fragments' minima contiguous in best[0, nact) — an unsigned MIN all-reduce over best itself
 // replaces pack_best / all-reduce / unpack_best (nullptr: use those)
 void ghs_solver_set_group_cancel(ghs_solver *s, const int *flag) { s->group_cancel = flag; }
+const ghs_config_t *ghs_solver_cfg_of(const ghs_solver *s) { return &s->cfg; }
+uint32_t ghs_solver_round_of(const ghs_solver *s) { return s->round; }
 uint64_t *ghs_solver_best_slots_of(ghs_solver *s) {
   return (s->phase == 1 && s->nact && s->act_ident && s->level_dense) ? s->best : nullptr;
 }
@@ -3407,7 +3410,8 @@ static uint32_t g_prof_next_id = 0;
 static const char *const KERNEL_NAMES[GHS_K_COUNT] = {
     "k_select", "k_filter", "k_level_pass", "k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>",
     "k_win", "k_hook", "k_jump_ident", "k_jump", "k_select_lb", "k_resolve", "k_giant", "k_scan_counts",
-    "k_plan", "k_init", "k_pack_best", "k_unpack_best", "k_round_report", "k_pack_hook", "k_unpack_hook", "k_dense", "k_flag_bits", "k_bucket", "k_bmin", "k_wstarts", "k_wmin", "k_hot_hook"};
+    "k_plan", "k_init", "k_pack_best", "k_unpack_best", "k_round_report", "k_pack_hook", "k_unpack_hook", "k_dense", "k_flag_bits", "k_bucket", "k_bmin", "k_wstarts", "k_wmin", "k_hot_hook",
+    "k_tail_open", "k_tail_round", "k_tail_hook", "k_bcount"};
 
 struct KtScope {
   ghs_solver *s;
@@ -3655,7 +3659,7 @@ static void default_config(ghs_config_t *c) {
   c->options = 0;
   c->dedup_max = 0;
   c->fault_rank = 0;
-  c->reserved = 0;
+  c->fault_round = 0;
 }
 
 // level1_edges_per_vertex <= 0 picks the first level's size from the density. The first level
@@ -4529,6 +4533,7 @@ static int solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint
   *out = nullptr;
   if (m >= (1ull << 31)) GHS_FAIL(GHS_E_ARG, "m must be < 2^31");
   if (e_lo > e_hi || e_hi > m) GHS_FAIL(GHS_E_ARG, "bad edge range");
+  if (cfg && (cfg->num_ranks < 1 || cfg->num_ranks > GHS_MAX_RANKS)) GHS_FAIL(GHS_E_ARG, "num_ranks must be in [1, GHS_MAX_RANKS]");
   if (m && (!d_u || !d_v || !d_w || !d_in_mst)) GHS_FAIL(GHS_E_ARG, "d_u/d_v/d_w/d_in_mst is NULL");
   if ((((uintptr_t)d_u) | ((uintptr_t)d_v) | ((uintptr_t)d_w)) & 15)
     GHS_FAIL(GHS_E_ARG, "d_u/d_v/d_w must be 16-byte aligned");
@@ -4603,6 +4608,36 @@ int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_
   return solver_create(n, m, d_u, d_v, d_w, e_lo, e_hi, cfg, d_workspace, workspace_bytes, d_in_mst, stream, nullptr,
                        out);
 }
+
+}  // extern "C"
+
+int ghs_solver_create_pooled(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
+                             uint64_t e_lo, uint64_t e_hi, const ghs_config_t *cfg, void *d_workspace,
+                             size_t workspace_bytes, uint8_t *d_in_mst, void *stream, void *hostres,
+                             ghs_solver_t **out) {
+  if (!hostres) GHS_FAIL(GHS_E_ARG, "host resources are NULL");
+  return solver_create(n, m, d_u, d_v, d_w, e_lo, e_hi, cfg, d_workspace, workspace_bytes, d_in_mst, stream,
+                       static_cast<HostRes *>(hostres), out);
+}
+
+void *ghs_hostres_new(int *rc) {
+  HostRes *r = new HostRes();
+  if ((*rc = hostres_init(r)) != GHS_OK) {
+    hostres_free(r);
+    delete r;
+    return nullptr;
+  }
+  return r;
+}
+
+void ghs_hostres_delete(void *res) {
+  if (!res) return;
+  HostRes *r = static_cast<HostRes *>(res);
+  hostres_free(r);
+  delete r;
+}
+
+extern "C" {
 
 // stepwise API: one round per minedge/contract pair, exact counts after every contract
 int ghs_solver_minedge(ghs_solver_t *s, uint64_t *num_active) {
@@ -4767,6 +4802,10 @@ int ghs_solver_hook_slots(ghs_solver_t *s, uint32_t nranks, uint64_t **d_slots, 
   *d_slots = nullptr;
   *padded = 0;
   if (s->phase != 1) GHS_FAIL(GHS_E_STATE, "hook_slots must follow minedge");
+  // the padding (< nranks slots past nact) lives in dbest's and the communicator's 64 spare slots
+  if (nranks != s->cfg.num_ranks) GHS_FAIL(GHS_E_ARG, "hook_slots: nranks differs from the solver's num_ranks");
+  if (nranks > GHS_MAX_RANKS) GHS_FAIL(GHS_E_ARG, "hook_slots: more than GHS_MAX_RANKS ranks");
+  s->hook_S = 0;
   // a dense level's opening round (its slots are best itself, in dense-label order)
   if (s->cfg.num_ranks <= 1 || s->level_round != 0 || !s->nact || s->hooked || !s->act_ident || !s->level_dense)
     return GHS_OK;
@@ -4777,6 +4816,7 @@ int ghs_solver_hook_slots(ghs_solver_t *s, uint32_t nranks, uint64_t **d_slots, 
   }
   *d_slots = s->best;
   *padded = S;
+  s->hook_S = S;
   return GHS_OK;
 }
 
@@ -4784,6 +4824,8 @@ int ghs_solver_hook_owner(ghs_solver_t *s, uint32_t rank, uint64_t per, uint64_t
   if (!s || !d_pairs) GHS_FAIL(GHS_E_ARG, "solver/pairs is NULL");
   if (s->phase != 1 || !s->level_dense || !s->act_ident || s->level_round != 0 || s->hooked)
     GHS_FAIL(GHS_E_STATE, "hook_owner must follow hook_slots and the reduce-scatter");
+  if (rank >= s->cfg.num_ranks || (uint64_t)(rank + 1) * per > s->hook_S || per * s->cfg.num_ranks != s->hook_S)
+    GHS_FAIL(GHS_E_ARG, "hook_owner: rank / slice outside the padded slots of hook_slots");
   const uint64_t lo = (uint64_t)rank * per, hi = lo + per;
   if (per) {
     KT(GHS_K_PACK_HOOK, per);

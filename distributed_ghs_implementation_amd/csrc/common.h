@@ -69,6 +69,16 @@ void ghs_solver_set_group_cancel(ghs_solver *s, const int *flag);
 bool ghs_solver_cancelled_of(const ghs_solver *s);
 // the multi-rank round loop's contract: rounds >= 2 of a level pipelined (no host sync)
 int ghs_solver_contract_async(ghs_solver *s, int *done);
+const ghs_config_t *ghs_solver_cfg_of(const ghs_solver *s);
+uint32_t ghs_solver_round_of(const ghs_solver *s);
+// pinned host resources of a solver (report ring, counters mirror, events), kept across solves by
+// the multi-rank drivers' cache: solver creation over them allocates nothing on the host
+void *ghs_hostres_new(int *rc);
+void ghs_hostres_delete(void *res);
+int ghs_solver_create_pooled(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
+                             uint64_t e_lo, uint64_t e_hi, const ghs_config_t *cfg, void *d_workspace,
+                             size_t workspace_bytes, uint8_t *d_in_mst, void *stream, void *hostres,
+                             ghs_solver_t **out);
 
 #define GHS_HIP_CHECK(expr)                                                                     \
   do {                                                                                          \

@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
@@ -303,10 +305,17 @@ int run_loop(ghs_solver_t *s, ghs_comm *c) {
     }
     LOOP_CHECK(comm_scratch(c, ghs_solver_n_of(s)));
   }
+  const ghs_config_t *cf = ghs_solver_cfg_of(s);
   for (uint32_t guard = 0;; ++guard) {
     if (guard > 16 * GHS_MAX_ROUND_STATS) {
       ghs::set_error("round cap exceeded");
       return loop_fail(c, GHS_E_ROUNDCAP);
+    }
+    // test hook (ghs_config_t.fault_round): this rank fails between rounds while its peers go on
+    // into the next collective — their waits must end through the group's cancel path
+    if (multi && cf->fault_round && cf->fault_rank == (uint32_t)c->rank + 1 && ghs_solver_round_of(s) >= cf->fault_round) {
+      ghs::set_error("injected mid-solve failure (fault_round)");
+      return loop_fail(c, GHS_E_STATE);
     }
     uint64_t count = 0;
     int rc = ghs_solver_minedge(s, &count);
@@ -369,20 +378,99 @@ void edge_range(uint64_t m, int r, int N, uint64_t *lo, uint64_t *hi) {
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// one rank of a driver below: its stream, canonical copy (ghs_mst_multi), workspace, solver
-struct Rank {
+// The drivers' per-rank state, kept across calls (ghs_release_cache): a rank's stream, workspace,
+// replicated canonical copy and flags (ghs_mst_multi), and pinned report ring — a call of the same
+// shape then allocates nothing. Per-call allocation of ~N workspaces (s26 x 8 emulated: 8 x ~11 GB)
+// was the suspected cause of the multi-second emulated calls of round 3.
+struct RankState {
   int dev = 0;
   hipStream_t stream = nullptr;
-  void *canon = nullptr;       // u, v, w (ghs_mst_multi: replicated per device)
+  void *canon = nullptr;       // ghs_mst_multi: u, v, w replicated per device
   void *ws = nullptr;
+  size_t ws_bytes = 0;
   uint8_t *in_mst = nullptr;   // ghs_mst_multi: m flags per device (own range written)
+  void *hostres = nullptr;     // pinned counters / report ring / events of the rank's solver
+};
+
+// one rank of a driver call: its cached state, this call's solver and outcome
+struct Rank {
+  RankState *st = nullptr;
   ghs_solver_t *solver = nullptr;
   ghs_comm *comm = nullptr;
   int rc = GHS_OK;
   std::string err;
   ghs_result_t result{};
   std::vector<ghs_round_stats_t> stats;
+  double ms_setup = 0, ms_solve = 0, ms_gather = 0;
 };
+
+struct DriverCache {
+  int kind = 0;  // 1 = ghs_mst_multi, 2 = ghs_mst_emulated
+  std::vector<int> devs;
+  uint32_t n = 0;
+  uint64_t m = 0;
+  std::vector<RankState> ranks;
+  std::vector<ghs_comm> comms;  // ghs_mst_multi's clique (nccl) and both drivers' collective scratch
+};
+std::mutex g_drv_mu;           // one driver call at a time per process (they share the cache)
+DriverCache *g_drv = nullptr;
+
+void cache_free(DriverCache *c) {
+  if (!c) return;
+  for (RankState &x : c->ranks) {
+    if (hipSetDevice(x.dev) != hipSuccess) continue;
+    if (x.stream) (void)hipStreamSynchronize(x.stream);
+    for (void *p : {x.canon, x.ws, (void *)x.in_mst})
+      if (p) (void)hipFree(p);
+    if (x.stream) (void)hipStreamDestroy(x.stream);
+    ghs_hostres_delete(x.hostres);
+  }
+  for (ghs_comm &k : c->comms) {
+    if (hipSetDevice(k.dev) != hipSuccess) continue;
+    if (k.nccl) ncclCommDestroy(k.nccl);  // (one aborted by loop_fail was nulled there)
+    k.nccl = nullptr;
+    for (void *p : {(void *)k.dense, (void *)k.hook, (void *)k.gathered, (void *)k.agree, (void *)k.pairs})
+      if (p) (void)hipFree(p);
+  }
+  delete c;
+}
+
+// the cache of this call's shape (g_drv_mu held): the one kept from an earlier call of the same
+// shape, or a fresh one (another shape's is freed first: one shape's state at a time)
+DriverCache *cache_acquire(int kind, const std::vector<int> &devs, uint32_t n, uint64_t m, bool *reused) {
+  if (g_drv && g_drv->kind == kind && g_drv->devs == devs && g_drv->n == n && g_drv->m == m) {
+    *reused = true;
+    return g_drv;
+  }
+  cache_free(g_drv);
+  g_drv = new DriverCache;
+  g_drv->kind = kind;
+  g_drv->devs = devs;
+  g_drv->n = n;
+  g_drv->m = m;
+  const int N = (int)devs.size();
+  g_drv->ranks.resize(N);
+  g_drv->comms.resize(N);
+  for (int i = 0; i < N; ++i) {
+    g_drv->ranks[i].dev = devs[i];
+    g_drv->comms[i].nranks = N;
+    g_drv->comms[i].rank = i;
+    g_drv->comms[i].dev = devs[i];
+  }
+  *reused = false;
+  return g_drv;
+}
+
+// after a call: a failed call leaves no state behind (aborted communicators, cancelled solvers)
+void cache_release_on(int rc) {
+  if (rc == GHS_OK || !g_drv) return;
+  cache_free(g_drv);
+  g_drv = nullptr;
+}
+
+inline double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
 
 int rank_fail(Rank &d, int rc) {
   d.rc = rc;
@@ -392,11 +480,14 @@ int rank_fail(Rank &d, int rc) {
   return rc;
 }
 
-// create the rank's solver over device-resident u/v/w, agree with the other ranks that every setup
-// succeeded, and run it to completion. setup_rc: the driver's own setup of this rank (stream,
-// copies) — a failed rank still joins the agreement, so its peers leave too.
+// create the rank's solver over device-resident u/v/w (workspace and pinned resources from the
+// cache, allocated on first use), agree with the other ranks that every setup succeeded, and run it
+// to completion. setup_rc: the driver's own setup of this rank (stream, copies) — a failed rank
+// still joins the agreement, so its peers leave too. t0: the rank's start (phase times).
 int rank_solve(Rank &d, int r, int N, uint32_t n, uint64_t m, const uint32_t *du, const uint32_t *dv,
-               const uint32_t *dw, uint8_t *d_in_mst, const ghs_config_t *cfg, int setup_rc) {
+               const uint32_t *dw, uint8_t *d_in_mst, const ghs_config_t *cfg, int setup_rc,
+               std::chrono::steady_clock::time_point t0) {
+  RankState &x = *d.st;
   int rc = setup_rc;
   uint64_t lo, hi;
   edge_range(m, r, N, &lo, &hi);
@@ -404,42 +495,53 @@ int rank_solve(Rank &d, int r, int N, uint32_t n, uint64_t m, const uint32_t *du
   ghs_config_t c2;
   if (cfg) c2 = *cfg; else ghs_default_config(&c2);
   c2.num_ranks = (uint32_t)N;
-  if (!rc && hipSetDevice(d.dev) != hipSuccess) {
+  if (!rc && hipSetDevice(x.dev) != hipSuccess) {
     ghs::set_error("hipSetDevice failed");
     rc = GHS_E_HIP;
   }
-  if (!rc && c2.fault_rank == (uint32_t)r + 1) {  // test hook (ghs_config_t.fault_rank)
+  if (!rc && c2.fault_rank == (uint32_t)r + 1 && c2.fault_round == 0) {  // test hook (ghs_config_t.fault_rank)
     ghs::set_error("injected setup failure (fault_rank)");
     rc = GHS_E_NOMEM;
   }
-  if (!rc && hipMalloc(&d.ws, wsb) != hipSuccess) {
-    ghs::set_error("hipMalloc of a rank workspace failed");
-    rc = GHS_E_NOMEM;
+  if (!rc && x.ws_bytes < wsb) {
+    if (x.ws) (void)hipFree(x.ws);
+    x.ws = nullptr;
+    x.ws_bytes = 0;
+    if (hipMalloc(&x.ws, wsb) != hipSuccess) {
+      ghs::set_error("hipMalloc of a rank workspace failed");
+      rc = GHS_E_NOMEM;
+    } else {
+      x.ws_bytes = wsb;
+    }
   }
-  if (!rc) rc = ghs_solver_create(n, m, du, dv, dw, lo, hi, &c2, d.ws, wsb, d_in_mst, d.stream, &d.solver);
+  if (!rc && !x.hostres) x.hostres = ghs_hostres_new(&rc);
+  if (!rc) rc = ghs_solver_create_pooled(n, m, du, dv, dw, lo, hi, &c2, x.ws, x.ws_bytes, d_in_mst, x.stream, x.hostres,
+                                         &d.solver);
   if (rc < 0) d.err = ghs_last_error();
-  const int agreed = comm_agree(d.comm, rc < 0 ? rc : GHS_OK, d.stream);
+  const int agreed = comm_agree(d.comm, rc < 0 ? rc : GHS_OK, x.stream);
+  d.ms_setup = ms_since(t0);
   if (agreed < 0) {
     if (!rc) d.err = ghs_last_error();
     d.rc = agreed;
     if (d.comm && d.comm->group_cancel) __atomic_store_n(d.comm->group_cancel, 1, __ATOMIC_RELEASE);
     return agreed;
   }
+  const auto t1 = std::chrono::steady_clock::now();
   rc = ghs_solver_run(d.solver, d.comm);
   if (rc < 0) return rank_fail(d, rc);
   d.stats.assign(GHS_MAX_ROUND_STATS, ghs_round_stats_t{});
   rc = ghs_solver_finish(d.solver, &d.result, d.stats.data());
+  d.ms_solve = ms_since(t1);
   if (rc < 0) return rank_fail(d, rc);
   return GHS_OK;
 }
 
-void rank_release(Rank &d) {
-  if (hipSetDevice(d.dev) != hipSuccess) return;
+// the call's solver goes; the rank's cached state stays (its stream drained)
+void rank_detach(Rank &d) {
+  if (!d.st || hipSetDevice(d.st->dev) != hipSuccess) return;
   if (d.solver) ghs_solver_destroy(d.solver);
-  if (d.stream) (void)hipStreamSynchronize(d.stream);
-  for (void *p : {d.canon, d.ws, (void *)d.in_mst})
-    if (p) (void)hipFree(p);
-  if (d.stream) (void)hipStreamDestroy(d.stream);
+  d.solver = nullptr;
+  if (d.st->stream) (void)hipStreamSynchronize(d.st->stream);
 }
 
 // a rank's error that only reports another rank's failure (a cancelled wait, a failed agreement)
@@ -448,8 +550,8 @@ bool peer_error(const Rank &x) {
 }
 
 // the first failing rank's own error (over those that only saw a peer fail), then the totals agree
-// on every rank
-int collect(std::vector<Rank> &d, ghs_result_t *result, ghs_round_stats_t *stats, std::string *err) {
+// on every rank; the host phase times are the maxima over the ranks
+int collect(std::vector<Rank> &d, bool reused, ghs_result_t *result, ghs_round_stats_t *stats, std::string *err) {
   for (auto &x : d)
     if (x.rc && !peer_error(x)) {
       *err = x.err;
@@ -465,7 +567,16 @@ int collect(std::vector<Rank> &d, ghs_result_t *result, ghs_round_stats_t *stats
       *err = "ranks disagree on the MSF totals";
       return GHS_E_STATE;
     }
-  if (result) *result = d[0].result;
+  if (result) {
+    *result = d[0].result;
+    result->ms_setup = result->ms_solve = result->ms_gather = 0;
+    for (auto &x : d) {
+      result->ms_setup = std::max(result->ms_setup, x.ms_setup);
+      result->ms_solve = std::max(result->ms_solve, x.ms_solve);
+      result->ms_gather = std::max(result->ms_gather, x.ms_gather);
+    }
+    result->reused = reused ? 1u : 0u;
+  }
   if (stats)
     for (uint32_t i = 0; i < d[0].result.num_stats; ++i) stats[i] = d[0].stats[i];
   return GHS_OK;
@@ -483,7 +594,8 @@ extern "C" int ghs_comm_unique_id(uint8_t *id) {
 }
 
 extern "C" int ghs_comm_init(int nranks, int rank, const uint8_t *id, ghs_comm_t **out) {
-  if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks) GHS_FAIL(GHS_E_ARG, "bad communicator arguments");
+  if (!out || !id || nranks < 1 || nranks > GHS_MAX_RANKS || rank < 0 || rank >= nranks)
+    GHS_FAIL(GHS_E_ARG, "bad communicator arguments");
   *out = nullptr;
   ghs_comm *c = new ghs_comm;
   c->nranks = nranks;
@@ -531,7 +643,7 @@ extern "C" int ghs_solver_run(ghs_solver_t *s, ghs_comm_t *comm) {
 extern "C" int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t *v, const uint32_t *w,
                              int num_gpus, const int *devices, const ghs_config_t *cfg, uint8_t *in_mst,
                              ghs_result_t *result, ghs_round_stats_t *stats) {
-  if (num_gpus < 1) GHS_FAIL(GHS_E_ARG, "num_gpus must be >= 1");
+  if (num_gpus < 1 || num_gpus > GHS_MAX_RANKS) GHS_FAIL(GHS_E_ARG, "num_gpus must be in [1, GHS_MAX_RANKS]");
   if (m && (!u || !v || !w || !in_mst)) GHS_FAIL(GHS_E_ARG, "NULL host pointer");
   if (m >= (1ull << 31)) GHS_FAIL(GHS_E_ARG, "m must be < 2^31");
   int ndev = 0;
@@ -543,31 +655,33 @@ extern "C" int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const ui
     for (int j = 0; j < i; ++j)
       if (devs[j] == devs[i]) GHS_FAIL(GHS_E_ARG, "devices must be distinct (one rank per GPU)");
   }
+  std::lock_guard<std::mutex> lock(g_drv_mu);
+  const auto t0 = std::chrono::steady_clock::now();
   int prev = 0;
   (void)hipGetDevice(&prev);
+  bool reused = false;
+  DriverCache *C = cache_acquire(1, devs, n, m, &reused);
   std::vector<Rank> d(num_gpus);
-  std::vector<ghs_comm> comms(num_gpus);
-  std::vector<ncclComm_t> nc(num_gpus);
   int rc = GHS_OK;
   std::string err;
-  {
+  if (!C->comms[0].nccl) {  // a fresh cache: the clique (kept with the cache)
+    std::vector<ncclComm_t> nc(num_gpus, nullptr);
     const ncclResult_t nr = ncclCommInitAll(nc.data(), num_gpus, devs.data());
     if (nr != ncclSuccess) {
       rc = GHS_E_HIP;
       err = std::string("ncclCommInitAll: ") + ncclGetErrorString(nr);
+    } else {
+      for (int i = 0; i < num_gpus; ++i) C->comms[i].nccl = nc[i];
     }
   }
   int group_failed = 0;  // set by the first failing rank: the others' waits end (solver_sync)
   for (int i = 0; i < num_gpus; ++i) {
-    d[i].dev = devs[i];
-    comms[i].nranks = num_gpus;
-    comms[i].rank = i;
-    comms[i].dev = devs[i];
-    comms[i].nccl = rc == GHS_OK ? nc[i] : nullptr;
-    comms[i].own_nccl = false;
-    comms[i].group_cancel = &group_failed;
-    d[i].comm = &comms[i];
-    if (rc == GHS_OK && (hipSetDevice(devs[i]) != hipSuccess || hipMalloc((void **)&comms[i].agree, 4) != hipSuccess)) {
+    ghs_comm &k = C->comms[i];
+    k.own_nccl = false;
+    k.group_cancel = &group_failed;
+    d[i].st = &C->ranks[i];
+    d[i].comm = &k;
+    if (rc == GHS_OK && !k.agree && (hipSetDevice(devs[i]) != hipSuccess || hipMalloc((void **)&k.agree, 4) != hipSuccess)) {
       rc = GHS_E_NOMEM;
       err = "hipMalloc of the setup-agreement word failed";
     }
@@ -579,51 +693,47 @@ extern "C" int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const ui
     for (int i = 0; i < num_gpus; ++i)
       th.emplace_back([&, i] {
         Rank &x = d[i];
+        RankState &st = *x.st;
         // setup errors are carried into rank_solve, whose agreement fails every rank together
         int setup = GHS_OK;
         const size_t cb = al256(m * 4);
-        char *c = nullptr;
-        if (hipSetDevice(x.dev) != hipSuccess || hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking) != hipSuccess) {
+        if (hipSetDevice(st.dev) != hipSuccess ||
+            (!st.stream && hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking) != hipSuccess)) {
           ghs::set_error("device setup failed");
           setup = GHS_E_HIP;
-        } else if (hipMalloc(&x.canon, 3 * cb + 256) != hipSuccess || hipMalloc((void **)&x.in_mst, m ? m : 1) != hipSuccess) {
+        } else if ((!st.canon && hipMalloc(&st.canon, 3 * cb + 256) != hipSuccess) ||
+                   (!st.in_mst && hipMalloc((void **)&st.in_mst, m ? m : 1) != hipSuccess)) {
           ghs::set_error("hipMalloc of the device's canonical copy failed");
           setup = GHS_E_NOMEM;
         } else {
-          c = (char *)x.canon;
-          if (m && (hipMemcpyAsync(c, u, m * 4, hipMemcpyHostToDevice, x.stream) != hipSuccess ||
-                    hipMemcpyAsync(c + cb, v, m * 4, hipMemcpyHostToDevice, x.stream) != hipSuccess ||
-                    hipMemcpyAsync(c + 2 * cb, w, m * 4, hipMemcpyHostToDevice, x.stream) != hipSuccess)) {
+          const char *c = (const char *)st.canon;
+          if (m && (hipMemcpyAsync((void *)c, u, m * 4, hipMemcpyHostToDevice, st.stream) != hipSuccess ||
+                    hipMemcpyAsync((void *)(c + cb), v, m * 4, hipMemcpyHostToDevice, st.stream) != hipSuccess ||
+                    hipMemcpyAsync((void *)(c + 2 * cb), w, m * 4, hipMemcpyHostToDevice, st.stream) != hipSuccess)) {
             ghs::set_error("H2D copy of the canonical list failed");
             setup = GHS_E_HIP;
           }
         }
+        const char *c = (const char *)st.canon;
         if (rank_solve(x, i, num_gpus, n, m, (const uint32_t *)c, (const uint32_t *)(c ? c + cb : nullptr),
-                       (const uint32_t *)(c ? c + 2 * cb : nullptr), x.in_mst, cfg, setup))
+                       (const uint32_t *)(c ? c + 2 * cb : nullptr), st.in_mst, cfg, setup, t0))
           return;
+        const auto t2 = std::chrono::steady_clock::now();
         uint64_t lo, hi;
         edge_range(m, i, num_gpus, &lo, &hi);
-        if (hi > lo && (hipMemcpyAsync(in_mst + lo, x.in_mst + lo, hi - lo, hipMemcpyDeviceToHost, x.stream) != hipSuccess ||
-                        hipStreamSynchronize(x.stream) != hipSuccess)) {
+        if (hi > lo && (hipMemcpyAsync(in_mst + lo, st.in_mst + lo, hi - lo, hipMemcpyDeviceToHost, st.stream) != hipSuccess ||
+                        hipStreamSynchronize(st.stream) != hipSuccess)) {
           ghs::set_error("D2H copy of the flags failed");
           rank_fail(x, GHS_E_HIP);
         }
+        x.ms_gather = ms_since(t2);
       });
     for (auto &t : th) t.join();
-    rc = collect(d, result, stats, &err);
+    rc = collect(d, reused, result, stats, &err);
   }
-  for (auto &x : d) rank_release(x);
-  for (int i = 0; i < num_gpus; ++i) {
-    if (comms[i].nccl) {
-      (void)hipSetDevice(devs[i]);
-      ncclCommDestroy(comms[i].nccl);
-      comms[i].nccl = nullptr;
-    }
-    (void)hipSetDevice(devs[i]);
-    for (void *p : {(void *)comms[i].dense, (void *)comms[i].hook, (void *)comms[i].gathered, (void *)comms[i].agree,
-                    (void *)comms[i].pairs})
-      if (p) (void)hipFree(p);
-  }
+  for (auto &x : d) rank_detach(x);
+  for (ghs_comm &k : C->comms) k.group_cancel = nullptr;
+  cache_release_on(rc);
   (void)hipSetDevice(prev);
   if (rc) GHS_FAIL(rc, err);
   return GHS_OK;
@@ -632,47 +742,63 @@ extern "C" int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const ui
 extern "C" int ghs_mst_emulated(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
                                 int num_ranks, const ghs_config_t *cfg, uint8_t *d_in_mst, ghs_result_t *result,
                                 ghs_round_stats_t *stats) {
-  if (num_ranks < 1 || num_ranks > 64) GHS_FAIL(GHS_E_ARG, "num_ranks must be in [1, 64]");
+  if (num_ranks < 1 || num_ranks > GHS_MAX_RANKS) GHS_FAIL(GHS_E_ARG, "num_ranks must be in [1, GHS_MAX_RANKS]");
   if (m && (!d_u || !d_v || !d_w || !d_in_mst)) GHS_FAIL(GHS_E_ARG, "NULL device pointer");
   if (m >= (1ull << 31)) GHS_FAIL(GHS_E_ARG, "m must be < 2^31");
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) GHS_FAIL(GHS_E_NODEVICE, "no current HIP device");
+  std::lock_guard<std::mutex> lock(g_drv_mu);
+  const auto t0 = std::chrono::steady_clock::now();
+  bool reused = false;
+  DriverCache *C = cache_acquire(2, std::vector<int>(num_ranks, dev), n, m, &reused);
   ghs::EmuGroup group(num_ranks);
   std::vector<Rank> d(num_ranks);
-  std::vector<ghs_comm> comms(num_ranks);
-  for (int i = 0; i < num_ranks; ++i) {
-    comms[i].nranks = num_ranks;
-    comms[i].rank = i;
-    comms[i].dev = dev;
-    comms[i].emu = &group;
-    d[i].dev = dev;
-    d[i].comm = &comms[i];
-  }
   int group_failed = 0;
-  for (auto &c : comms) c.group_cancel = &group_failed;
+  for (int i = 0; i < num_ranks; ++i) {
+    C->comms[i].emu = &group;
+    C->comms[i].group_cancel = &group_failed;
+    d[i].st = &C->ranks[i];
+    d[i].comm = &C->comms[i];
+  }
   std::vector<std::thread> th;
   for (int i = 0; i < num_ranks; ++i)
     th.emplace_back([&, i] {
       Rank &x = d[i];
+      RankState &st = *x.st;
       int setup = GHS_OK;
-      if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking) != hipSuccess) {
+      if (hipSetDevice(dev) != hipSuccess ||
+          (!st.stream && hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking) != hipSuccess)) {
         ghs::set_error("stream creation failed");
         setup = GHS_E_HIP;
       }
-      if (rank_solve(x, i, num_ranks, n, m, d_u, d_v, d_w, d_in_mst, cfg, setup)) return;
-      if (hipStreamSynchronize(x.stream) != hipSuccess) {
+      if (rank_solve(x, i, num_ranks, n, m, d_u, d_v, d_w, d_in_mst, cfg, setup, t0)) return;
+      const auto t2 = std::chrono::steady_clock::now();
+      if (hipStreamSynchronize(st.stream) != hipSuccess) {
         ghs::set_error("stream sync failed");
         rank_fail(x, GHS_E_HIP);
       }
+      x.ms_gather = ms_since(t2);
     });
   for (auto &t : th) t.join();
   std::string err;
-  const int rc = collect(d, result, stats, &err);
-  for (auto &x : d) rank_release(x);
-  for (auto &c : comms)
-    for (void *p : {(void *)c.dense, (void *)c.hook, (void *)c.gathered, (void *)c.pairs})
-      if (p) (void)hipFree(p);
+  const int rc = collect(d, reused, result, stats, &err);
+  for (auto &x : d) rank_detach(x);
+  for (ghs_comm &k : C->comms) {
+    k.emu = nullptr;
+    k.group_cancel = nullptr;
+  }
+  cache_release_on(rc);
   (void)hipSetDevice(dev);
   if (rc) GHS_FAIL(rc, err);
+  return GHS_OK;
+}
+
+extern "C" int ghs_release_cache(void) {
+  std::lock_guard<std::mutex> lock(g_drv_mu);
+  int prev = 0;
+  const bool have = hipGetDevice(&prev) == hipSuccess;
+  cache_free(g_drv);
+  g_drv = nullptr;
+  if (have) (void)hipSetDevice(prev);
   return GHS_OK;
 }

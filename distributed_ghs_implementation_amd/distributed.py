@@ -26,6 +26,7 @@ orchestration can be exercised on CPU with the gloo backend in tests (tests inje
 stepper from oracle/); the product stepper is `HipStepper` (libghs_mst.so).
 """
 import ctypes
+import hashlib
 import threading
 
 import torch
@@ -356,7 +357,7 @@ class DistributedMST:
         # raises on EVERY rank instead of leaving the others blocked in the next collective
         err = None
         try:
-            if config.fault_rank == self.rank + 1:  # test hook (ghs_config_t.fault_rank)
+            if config.fault_rank == self.rank + 1 and config.fault_round == 0:  # test hook (ghs_config_t.fault_rank)
                 raise _native.GHSError(_native.GHS_E_NOMEM, "injected setup failure (fault_rank)")
             self.engine = DeviceMST(edges, lo, hi, config)
         except Exception as ex:  # noqa: BLE001 (re-raised below, after the agreement)
@@ -372,6 +373,10 @@ class DistributedMST:
         if native is None:
             native = self.world > 1 and dist.is_initialized() and dist.get_backend(group) == "nccl"
         self.native = bool(native)
+        # the failure watchdog's store keys carry a value every rank of THIS instance shares and no
+        # other instance does (its RCCL unique id, broadcast by rank 0): a key left by a failed solve
+        # of an earlier instance — a retry, another group on the same store — never cancels this one
+        self._nonce = None
         self.comm = self._make_comm() if self.native and self.world > 1 else None
 
     def _make_comm(self):
@@ -381,6 +386,7 @@ class DistributedMST:
             uid.copy_(torch.frombuffer(bytearray(_native.comm_unique_id()), dtype=torch.uint8))
         src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
         dist.broadcast(uid, src=src, group=self.group)
+        self._nonce = hashlib.sha1(uid.cpu().numpy().tobytes()).hexdigest()[:16]
         # the communicator binds to the device current at ghs_comm_init: the edges' device
         with torch.cuda.device(self.edges.device):
             return _native.Comm(self.world, self.rank, bytes(uid.cpu().numpy().tobytes()))
@@ -420,7 +426,12 @@ class DistributedMST:
             store = dist.distributed_c10d._get_default_store()
         except Exception:  # noqa: BLE001
             return None
-        return _FailureWatch(store, f"ghs_failed/{self._solves}", self.stepper)
+        return _FailureWatch(store, self._failure_key(), self.stepper)
+
+    def _failure_key(self):
+        """The store key of this instance's current solve: instance nonce + solve index (a new
+        instance, or the same one's next solve, never sees an older failure)."""
+        return f"ghs_failed/{self._nonce}/{self._solves}"
 
     def close(self):
         if self.stepper is not None:

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GHS_MST_ABI_VERSION 6
+#define GHS_MST_ABI_VERSION 7
 
 #define GHS_OK 0
 #define GHS_NEED_EXCHANGE 1   /* ghs_solver_minedge on a multi-rank solver opened a level: OR-combine
@@ -47,6 +47,7 @@ extern "C" {
 #define GHS_E_STATE (-7)      /* solver handle used out of order */
 
 #define GHS_MAX_ROUND_STATS 64
+#define GHS_MAX_RANKS 64       /* ranks of one multi-rank solve (ghs_config_t.num_ranks, communicators) */
 
 /* Per-round record (one Boruvka round == one GHS level of the reference). */
 typedef struct ghs_round_stats {
@@ -69,7 +70,10 @@ typedef struct ghs_result {
   uint32_t num_stats;         /* entries filled in the stats array (<= GHS_MAX_ROUND_STATS) */
   uint32_t levels;            /* weight levels planned */
   uint32_t pass_flags;        /* bit 0: the solve ran bucketed rounds (k_bucket / k_bmin);
-                                 bit 1: the plan's span sample found the graph lattice-like */
+                                 bit 1: the plan's span sample found the graph lattice-like;
+                                 bit 2: level 0's round 0 ran windowed (k_wmin over the edge list;
+                                 unset when k_select's span flag sent it to k_bucket / k_bmin);
+                                 bit 3: a level finished in the LDS tail (k_tail_*) */
   double ms_total;            /* host wall time of the solve (device-resident input -> flags) */
   /* The two full streams over the canonical list (HIP events on the solve's stream). */
   float ms_select;            /* k_select: validation + level-0 split */
@@ -77,6 +81,15 @@ typedef struct ghs_result {
   uint64_t canon_edges;       /* canonical edges each pass streams (the solver's range) */
   uint64_t select_out;        /* entries k_select wrote (level-0 edges, incl. region padding) */
   uint64_t filter_out;        /* entries k_filter wrote (level-1 + pending edges, incl. padding) */
+  /* ABI 7: host-side phases of the multi-rank drivers (ghs_mst_multi / ghs_mst_emulated; 0
+     elsewhere), the maximum over the ranks: setup (stream, workspace, H2D copy, solver creation,
+     agreement), the ghs_solver_run loop, the flags' D2H gather. reused = 1 when the call ran on
+     the rank state cached by an earlier call of the same shape (no hipMalloc, no RCCL init). */
+  double ms_setup;
+  double ms_solve;
+  double ms_gather;
+  uint32_t reused;
+  uint32_t reserved;
 } ghs_result_t;
 
 /* Weight-level plan of the filter. Level 1 holds roughly the
@@ -103,6 +116,9 @@ typedef struct ghs_result {
                                       records instead of the windowed k_wmin over the edge list */
 #define GHS_OPT_BUCKETED_FIRST 0x80u /* one rank: bucketed first rounds of every level (whatever the
                                         graph), the other rounds unbucketed */
+#define GHS_OPT_NO_TAIL 0x200u     /* one rank: no LDS tail — every round of a level through the
+                                      per-round kernels (default: once a level's active fragments fit
+                                      the tail's LDS, its remaining rounds run in k_tail_*) */
 typedef struct ghs_config {
   uint32_t max_levels;
   uint32_t num_ranks;         /* ranks sharing the solve (1 = single GPU; >1: identical rounds on
@@ -114,7 +130,9 @@ typedef struct ghs_config {
                                  at most this many fragments are active (0 = off, the default) */
   uint32_t fault_rank;        /* test hook of the multi-rank drivers: 1 + the rank whose setup is
                                  made to fail (ghs_mst_multi / ghs_mst_emulated); 0 = none */
-  uint32_t reserved;
+  uint32_t fault_round;       /* ABI 7 test hook: with fault_rank set, that rank fails in the round
+                                 loop (ghs_solver_run) once it has completed this many rounds instead
+                                 of at setup; 0 = the setup failure above */
 } ghs_config_t;
 
 /* ---- library / device ------------------------------------------------------------------- */
@@ -147,6 +165,13 @@ int ghs_mst_host(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t *v, c
 int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t *v, const uint32_t *w,
                   int num_gpus, const int *devices, const ghs_config_t *cfg, uint8_t *in_mst,
                   ghs_result_t *result, ghs_round_stats_t *stats);
+/* ABI 7: the multi-rank drivers (ghs_mst_multi, ghs_mst_emulated) keep their per-rank state —
+ * streams, workspaces, replicated canonical copies, pinned report rings, collective scratch, and
+ * ghs_mst_multi's RCCL clique — in one process-wide cache keyed by (driver, devices, ranks, n, m);
+ * a later call of the same shape allocates nothing (ghs_result_t.reused = 1), a call of another
+ * shape or a failed call frees it first. ghs_release_cache frees it now (device memory back to
+ * the caller; safe to call at any time outside a driver call). */
+int ghs_release_cache(void);
 
 /* ---- device-resident API -----------------------------------------------------------------
  * Input: the canonical edge list in HBM (d_u, d_v, d_w: m uint32 each, 16-byte aligned) — the
@@ -293,7 +318,8 @@ enum ghs_kernel_id {
   GHS_K_SELECT = 0, GHS_K_FILTER, GHS_K_LEVEL_PASS, GHS_K_SEED_RUNS, GHS_K_MINEDGE_IDENT, GHS_K_MINEDGE_COMPACT,
   GHS_K_WIN, GHS_K_HOOK, GHS_K_JUMP_IDENT, GHS_K_JUMP, GHS_K_SELECT_LB, GHS_K_RESOLVE, GHS_K_GIANT, GHS_K_SCAN,
   GHS_K_PLAN, GHS_K_INIT, GHS_K_PACK, GHS_K_UNPACK, GHS_K_ROUND_REPORT, GHS_K_PACK_HOOK, GHS_K_UNPACK_HOOK,
-  GHS_K_DENSE, GHS_K_FLAG_BITS, GHS_K_BUCKET, GHS_K_BMIN, GHS_K_WSTARTS, GHS_K_WMIN, GHS_K_HOT_HOOK, GHS_K_COUNT
+  GHS_K_DENSE, GHS_K_FLAG_BITS, GHS_K_BUCKET, GHS_K_BMIN, GHS_K_WSTARTS, GHS_K_WMIN, GHS_K_HOT_HOOK,
+  GHS_K_TAIL_OPEN, GHS_K_TAIL_ROUND, GHS_K_TAIL_HOOK, GHS_K_BCOUNT, GHS_K_COUNT
 };
 typedef struct ghs_kernel_record {
   uint32_t kernel;  /* ghs_kernel_id */

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi():
     L = _native.load()
-    assert L.ghs_abi_version() == _native.ABI_VERSION == 6
+    assert L.ghs_abi_version() == _native.ABI_VERSION == 7
     assert _native.device_count() >= 0
 
 
@@ -45,7 +45,8 @@ def test_config_struct_and_no_environment_knobs():
     L = _native.load()
     assert ctypes.sizeof(_native.Config) == 40
     c = _native.make_config()
-    assert (c.options, c.dedup_max, c.fault_rank, c.max_levels, c.num_ranks) == (0, 0, 0, 8, 1)
+    assert (c.options, c.dedup_max, c.fault_rank, c.fault_round, c.max_levels, c.num_ranks) == (0, 0, 0, 0, 8, 1)
+    assert ctypes.sizeof(_native.Result) == 104  # ABI 7: + ms_setup / ms_solve / ms_gather / reused
     blob = open(_native.LIB_PATH, "rb").read()
     for knob in (b"GHS_LOOKAHEAD", b"GHS_HV", b"GHS_DEDUP_MAX", b"GHS_SEED_RUNS", b"GHS_DENSE", b"GHS_SEG_G",
                  b"GHS_MINEDGE_G", b"GHS_DEBUG", b"GHS_DETAIL", b"GHS_TIME_ROUNDS"):
@@ -57,6 +58,18 @@ def test_sizes_are_sane():
     L = _native.load()
     assert L.ghs_workspace_bytes(1000, 5000, 10000) >= 1000 * 20 + 10000 * 32
     assert L.ghs_rmat_temp_bytes(10, 16) >= 2 * 16 * 1024 * 8
+
+
+def test_rank_limits_rejected():
+    """GHS_MAX_RANKS bounds every multi-rank entry before any device work (the
+    reduce-scatter padding lives in 64 spare slots)."""
+    L = _native.load()
+    h = ctypes.c_void_p(0)
+    uid = (ctypes.c_uint8 * _native.GHS_COMM_ID_BYTES)()
+    assert L.ghs_comm_init(65, 0, uid, ctypes.byref(h)) == _native.GHS_E_ARG
+    assert L.ghs_comm_init(2, 2, uid, ctypes.byref(h)) == _native.GHS_E_ARG
+    assert L.ghs_mst_emulated(4, 0, None, None, None, 65, None, None, None, None) == _native.GHS_E_ARG
+    assert L.ghs_release_cache() == _native.GHS_OK
 
 
 def test_null_arguments_rejected():

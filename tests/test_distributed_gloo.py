@@ -85,3 +85,38 @@ def test_gloo_ranks_match_kruskal(world, name, levels, owner_hooks, use_rs):
         if not owner_hooks:  # fragment-form hooks on every rank: each rank holds the whole MSF
             assert np.array_equal(np.array(in_mst, np.uint8), ref_in)
     assert np.array_equal(flags, ref_in)
+
+
+def test_failure_watch_keys_are_per_instance():
+    """a failure key left in the store by one DistributedMST's failed solve must not
+    cancel another instance's solve (a retry, another group on the same store). The key carries the
+    instance's nonce (its RCCL unique id) and the solve index."""
+    import threading
+
+    import torch.distributed as dist
+    from distributed_ghs_implementation_amd.distributed import DistributedMST, _FailureWatch
+
+    class Stepper:
+        def __init__(self):
+            self.cancelled = threading.Event()
+
+        def cancel(self):
+            self.cancelled.set()
+
+    store = dist.HashStore()
+    a, b = DistributedMST.__new__(DistributedMST), DistributedMST.__new__(DistributedMST)
+    a._nonce, b._nonce = "aaaa", "bbbb"
+    a._solves = b._solves = 1
+    assert a._failure_key() != b._failure_key()
+    # instance a fails: its key is set
+    wa = _FailureWatch(store, a._failure_key(), Stepper())
+    wa.report()
+    wa.stop()
+    # instance b (same solve index, same store) is NOT cancelled ...
+    sb = Stepper()
+    wb = _FailureWatch(store, b._failure_key(), sb, period=0.005)
+    assert not sb.cancelled.wait(0.1)
+    # ... but a peer of b reporting b's key cancels it
+    _FailureWatch(store, b._failure_key(), Stepper()).report()
+    assert sb.cancelled.wait(2.0)
+    wb.stop()

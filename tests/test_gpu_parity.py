@@ -461,6 +461,56 @@ def test_rank_setup_failure_fails_every_rank(world, fault, torch_cuda):
     assert np.array_equal(flags.cpu().numpy().astype(bool), ref_in.astype(bool))
 
 
+@pytest.mark.parametrize("world,fault,round_", [(4, 2, 1), (4, 4, 3), (2, 1, 2)])
+def test_rank_mid_solve_failure_fails_every_rank(world, fault, round_, torch_cuda):
+    """One rank fails INSIDE the round loop (ghs_config_t.fault_round: after `round_` rounds, while
+    its peers go on into the next collective): every rank returns an error instead of hanging (the
+    group's cancel flag ends their waits), the failing rank's own error is reported, the drivers'
+    cached state is dropped, and the next call solves normally — then a call of the same shape runs
+    on the cached state (ABI 7: no allocation)."""
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import emulated_mst, generate_rmat
+    ora = _oracle()
+    e = generate_rmat(13, 16, seed=3, wseed=4)
+    g = e.to_host()
+    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    with pytest.raises(_native.GHSError) as ei:
+        emulated_mst(e, world, config=_native.make_config(fault_rank=fault, fault_round=round_))
+    assert ei.value.code == _native.GHS_E_STATE
+    assert "injected mid-solve failure" in str(ei.value)
+    for k in range(2):
+        res, _, flags = emulated_mst(e, world)
+        assert np.array_equal(flags.cpu().numpy().astype(bool), ref_in.astype(bool))
+        assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
+        assert res.reused == k  # the failed call left nothing cached; the second call reuses
+        assert res.ms_setup > 0 and res.ms_solve > 0
+    _native.release_cache()
+
+
+def test_driver_cache_follows_the_shape(torch_cuda):
+    """The drivers' cache holds one shape: another graph (or rank count) allocates afresh, the
+    same one reuses; ghs_mst_multi's 1-rank clique is cached too (its second call reuses)."""
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import emulated_mst, generate_rmat
+    from distributed_ghs_implementation_amd.mst import minimum_spanning_forest
+    ora = _oracle()
+    a, b = generate_rmat(11, 16, seed=1, wseed=2), generate_rmat(12, 16, seed=1, wseed=2)
+    seen = []
+    for e, world in ((a, 2), (a, 2), (b, 2), (b, 3), (b, 3)):
+        res, _, flags = emulated_mst(e, world)
+        g = e.to_host()
+        ref_in, _, _ = ora.kruskal_c(g.n, g.u, g.v, g.w)
+        assert np.array_equal(flags.cpu().numpy().astype(bool), ref_in.astype(bool))
+        seen.append(res.reused)
+    assert seen == [0, 1, 0, 0, 1]
+    g = b.to_host()
+    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    for k in range(2):
+        r = minimum_spanning_forest(g, devices=[0])
+        assert np.array_equal(r.in_mst, ref_in.astype(bool))
+    _native.release_cache()
+
+
 def test_multi_gpu_entry_setup_failure(torch_cuda):
     """ghs_mst_multi (a 1-rank RCCL clique on the box's device) with its rank's setup failing:
     the setup agreement's RCCL all-reduce runs and the call returns the error."""
@@ -512,9 +562,11 @@ def test_native_loop_s26_emulated(world, rmat_s26_reference, torch_cuda):
     """BASELINE config 4 through the library's round loop (ghs_mst_emulated, 8 ranks on this
     GPU): the s26 MSF of the single-GPU solve (== torch Boruvka checker)."""
     torch = torch_cuda
+    from distributed_ghs_implementation_amd import _native
     from distributed_ghs_implementation_amd.device import emulated_mst
     e, ref_flags, ref_tot = rmat_s26_reference
     res, _, flags = emulated_mst(e, world)
+    _native.release_cache()  # ~N workspaces of s26 stay cached otherwise
     assert torch.equal(flags, ref_flags)
     assert (res.total_weight, res.num_mst_edges) == ref_tot
     del flags

@@ -22,7 +22,8 @@ def main():
         res, _, flags = emulated_mst(e, world)
         torch.cuda.synchronize()
         print(f"rep {r} s{scale} x{world} {1e3 * (time.perf_counter() - t0):.2f} ms weight {res.total_weight} "
-              f"edges {res.num_mst_edges}", flush=True)
+              f"edges {res.num_mst_edges} reused {res.reused} setup {res.ms_setup:.2f} solve {res.ms_solve:.2f} "
+              f"gather {res.ms_gather:.2f} ms (max over ranks)", flush=True)
         del flags
 
 
