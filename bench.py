@@ -63,6 +63,8 @@ def parse():
                     help="ghs_config_t.options bits for N=1 (A/B of path options; 0 = the default path)")
     ap.add_argument("--dedup-max", type=int, default=None,
                     help="ghs_config_t.dedup_max for N=1 (parallel-edge filter at <= F fragments; A/B)")
+    ap.add_argument("--coll-timeout", type=int, default=300,
+                    help="N>1: seconds before a torch.distributed collective gives up (then every rank exits)")
     return ap.parse_args()
 
 
@@ -146,16 +148,15 @@ def launch_bytes(rec, stats, res, n, windowed=frozenset()):
 STAGE1 = ("k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>", "k_bucket", "k_bmin", "k_wstarts", "k_wmin")
 
 
+PASS_WINDOWED = 0x4  # ghs_result_t.pass_flags: level 0's round 0 ran windowed (k_select's span flag clear)
+
+
 def kernel_table(records, stats, res, n):
     """Per kernel: launches, ms per step, algorithmic bytes, achieved GB/s (one profiled step)."""
     tab = {}
-    # a round with k_wmin ran windowed unless its fallback k_bmin took longer (the span flag)
-    per_round = {}
-    for rec in records:
-        if rec["kernel"] in ("k_wmin", "k_bmin"):
-            per_round.setdefault(rec["round"], {}).setdefault(rec["kernel"], 0.0)
-            per_round[rec["round"]][rec["kernel"]] += max(rec["ms"], 0.0)
-    windowed = frozenset(r for r, d in per_round.items() if "k_wmin" in d and d["k_wmin"] >= d.get("k_bmin", 0.0))
+    # the windowed round is level 0's round 0; the library reports whether it ran (pass_flags bit 2)
+    # or fell back to k_bucket / k_bmin (ADVICE r03: no longer guessed from the kernels' times)
+    windowed = frozenset([0]) if res.pass_flags & PASS_WINDOWED else frozenset()
     for rec in records:
         t = tab.setdefault(rec["kernel"], {"launches": 0, "ms": 0.0, "bytes": 0.0})
         t["launches"] += 1
@@ -225,6 +226,25 @@ def roofline_obj(kernel, t, tag, note):
             "avg_launch_ms": round(t["ms"] / t["launches"], 4), "launches": t["launches"],
             "ms_per_step": t["ms"], "timing": t.get("timing", "HIP events around every launch of one profiled step"),
             "traffic_source": traffic["_path"] if traffic else None}
+
+
+def kernels_obj(ktab, tag):
+    """The line's per-kernel table; where a committed PMC profile of the workload has the kernel,
+    its measured HBM bytes per launch and their ratio to the algorithmic bytes (traffic well above
+    1x = re-reads / write-backs the byte model does not count)."""
+    out = {}
+    for k, v in sorted(ktab.items(), key=lambda kv: -kv[1]["ms"]):
+        e = {"launches": v["launches"], "ms_per_step": v["ms"], "algorithmic_bytes": round(v["bytes"]),
+             "achieved_gbs": round(v["achieved_gbs"], 1) if v["achieved_gbs"] else None,
+             "frac": round(v["achieved_gbs"] / HBM_PEAK_GBS, 4) if v["achieved_gbs"] else None}
+        tr = load_traffic(tag, k)
+        if tr and v["bytes"] > 0:
+            alg = v["bytes"] / v["launches"]
+            e["pmc_bytes_per_launch"] = round(tr["traffic_bytes_per_launch"])
+            e["pmc_ratio"] = round(tr["traffic_bytes_per_launch"] / alg, 3)
+            e["pmc_source"] = tr["_path"]
+        out[k] = e
+    return out
 
 
 def host_cpus():
@@ -346,6 +366,44 @@ def make_workload(args, world):
     return edges, tag, cfg
 
 
+def mark(rank, msg):
+    """A one-line progress mark on stderr per phase (a silent multi-minute phase looks hung)."""
+    print(f"[bench rank {rank} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+class PhaseFailed(RuntimeError):
+    pass
+
+
+def agreed(name, fn, rank, world, dist, dev):
+    """Run one phase on every rank, then agree on its outcome: a MAX all-reduce of a failure flag at
+    the same program point on every rank, so a rank whose phase raised ends EVERY rank with a
+    message naming the phase and the failing ranks (non-zero exit) instead of leaving its peers
+    waiting in the next collective. The phases' own collectives are bounded by the process group's
+    timeout (--coll-timeout)."""
+    import torch
+    mark(rank, f"{name} ...")
+    t0 = time.perf_counter()
+    out, err = None, None
+    try:
+        out = fn()
+    except Exception as ex:  # noqa: BLE001 (agreed on below, then raised on every rank)
+        import traceback
+        traceback.print_exc()
+        err = ex
+    if world > 1:
+        flags = torch.zeros(world, dtype=torch.int32, device=dev)
+        flags[rank] = 1 if err is not None else 0
+        dist.all_reduce(flags, op=dist.ReduceOp.MAX)
+        bad = [r for r in range(world) if int(flags[r].item())]
+        if bad:
+            raise PhaseFailed(f"phase '{name}' failed on rank(s) {bad}" + (f": {err}" if err is not None else ""))
+    elif err is not None:
+        raise PhaseFailed(f"phase '{name}' failed: {err}") from err
+    mark(rank, f"{name} done ({time.perf_counter() - t0:.1f} s)")
+    return out
+
+
 def dist_engine(edges, rank, world, dist, backend):
     """N > 1: DistributedMST with the library's round loop over its own RCCL communicator; if that
     fails on any rank (setup or the first solve; the ranks agree on it), every rank falls back to
@@ -419,38 +477,86 @@ def main():
             return 2
     torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if world > 1:
-        dist.init_process_group(args.backend)
+        import datetime
+        # every collective of the run ends (with an error, then the phase agreement) instead of
+        # waiting for the default 30 minutes behind a peer that died
+        dist.init_process_group(args.backend, timeout=datetime.timedelta(seconds=args.coll_timeout))
+    dev = "cuda" if world == 1 or args.backend == "nccl" else "cpu"
+    try:
+        return run(args, world, rank, dist, dev)
+    except PhaseFailed as ex:
+        mark(rank, f"FAILED: {ex}")
+        return 1
 
+
+def run(args, world, rank, dist, dev):
+    import torch
+
+    from distributed_ghs_implementation_amd import _native
     from distributed_ghs_implementation_amd.device import DeviceMST
-    from distributed_ghs_implementation_amd.distributed import DistributedMST
 
-    t_gen = time.perf_counter()
-    edges, tag, cfg = make_workload(args, world)
-    torch.cuda.synchronize()
-    gen_s = time.perf_counter() - t_gen
+    def gen():
+        # ranks sharing a GPU (a rehearsal) generate one after another: the radix sort's temporary
+        # buffers of N concurrent s26 generations need N x ~30 GB at once
+        t0 = time.perf_counter()
+        out, err = None, None
+        for r in range(world):
+            if r == rank:
+                try:
+                    out = make_workload(args, world)
+                    torch.cuda.synchronize()
+                    torch.cuda.empty_cache()
+                except Exception as ex:  # noqa: BLE001 (after the barriers: every rank reaches them)
+                    err = ex
+            if world > 1 and torch.cuda.device_count() < world:
+                dist.barrier()
+        if err is not None:
+            raise err
+        return out, time.perf_counter() - t0
+
+    (edges, tag, cfg), gen_s = agreed("generate", gen, rank, world, dist, dev)
     n, m = edges.n, edges.m
     cfg.update({"n": n, "m": m, "partition": f"canonical edge ranges x{world}", "parallelism": f"edges{world}"})
 
+    ref = None
+    if world > 1:
+        # the parity reference first, while no rank holds its engine: a one-GPU solve of the same
+        # resident graph on rank 0 (its ~80 GB s26 workspace freed before the ranks allocate theirs)
+        def reference():
+            if rank != 0:
+                return None
+            r1 = DeviceMST(edges)
+            rres, _ = r1.run()
+            eids = torch.nonzero(r1.in_mst[:m]).flatten().to(torch.int64).cpu()
+            del r1
+            torch.cuda.empty_cache()
+            return rres.total_weight, rres.num_mst_edges, eids
+
+        ref = agreed("reference solve (rank 0, one GPU)", reference, rank, world, dist, dev)
+
     loop = None
     if world > 1:
-        eng, loop = dist_engine(edges, rank, world, dist, args.backend)
+        eng, loop = agreed("engine setup + first solve", lambda: dist_engine(edges, rank, world, dist, args.backend),
+                           rank, world, dist, dev)
     else:
-        from distributed_ghs_implementation_amd import _native
         custom = args.options or args.dedup_max is not None
         eng = DeviceMST(edges, config=_native.make_config(options=args.options, dedup_max=args.dedup_max)
                         if custom else None)
     step = eng.run
+    dt_solve = None
     if world > 1:
         # N > 1: a step ends with the MSF on rank 0, as the reference's MPI run ends with
         # collect_results (ghs_implementation_mpi.py:760-779): each rank's own-range MSF edge ids
         # gathered to rank 0. The solve alone is timed separately (ms_per_step_solve).
-        dt_solve, _ = time_steps(eng.run, args.steps, args.warmup, world, dist)
+        dt_solve, _ = agreed("timed solves", lambda: time_steps(eng.run, args.steps, args.warmup, world, dist),
+                             rank, world, dist, dev)
 
         def step():
             out = eng.run()
             eng.collect_mst(0)
             return out
-    dt, outs = time_steps(step, args.steps, args.warmup, world, dist)
+    dt, outs = agreed("timed steps", lambda: time_steps(step, args.steps, args.warmup, world, dist),
+                      rank, world, dist, dev)
     results = [r for r, _ in outs]
     if len(set((r.total_weight, r.num_mst_edges) for r in results)) != 1:
         raise RuntimeError("non-deterministic MST across steps")
@@ -471,24 +577,24 @@ def main():
 
     parity = None
     if world > 1:
-        # outside the timed steps: the N-rank MSF (gathered to rank 0) against a one-GPU solve of
-        # the same resident graph on rank 0 — edge for edge
-        eids = eng.collect_mst(0)
-        if rank == 0:
-            ref = DeviceMST(edges)
-            rres, _ = ref.run()
-            ref_eids = torch.nonzero(ref.in_mst[:m]).flatten().to(torch.int64).cpu()
+        # outside the timed steps: the N-rank MSF (gathered to rank 0) against the one-GPU reference,
+        # edge for edge
+        def check():
+            eids = eng.collect_mst(0)
+            if rank != 0:
+                return None
+            rtw, rk, ref_eids = ref
             got = results[-1]
-            parity = {"against": "one-GPU solve of the same graph (DeviceMST), edge for edge",
-                      "total_weight": got.total_weight, "edges": got.num_mst_edges,
-                      "match": bool(rres.total_weight == got.total_weight and rres.num_mst_edges == got.num_mst_edges
-                                    and torch.equal(ref_eids, eids.cpu()))}
-            if not parity["match"]:
-                print(f"N={world} MSF differs from the one-GPU solve: {parity}", file=sys.stderr)
-            del ref, ref_eids
-            torch.cuda.empty_cache()
+            p = {"against": "one-GPU solve of the same graph (DeviceMST), edge for edge",
+                 "total_weight": got.total_weight, "edges": got.num_mst_edges,
+                 "match": bool(rtw == got.total_weight and rk == got.num_mst_edges and torch.equal(ref_eids, eids.cpu()))}
+            if not p["match"]:
+                print(f"N={world} MSF differs from the one-GPU solve: {p}", file=sys.stderr)
+            return p
 
-    ktab, s1, _ = profile_step(eng.run, n)
+        parity = agreed("parity vs the one-GPU solve", check, rank, world, dist, dev)
+
+    ktab, s1, _ = agreed("profiled step", lambda: profile_step(eng.run, n), rank, world, dist, dev)
     # the canonical passes are also timed inside the timed steps (two events per pass, no idle
     # between dependent kernels of note): prefer those averages for k_select / k_filter
     for name, attr in (("k_select", "ms_select"), ("k_filter", "ms_filter")):
@@ -512,16 +618,12 @@ def main():
         res0 = results[-1]
         breakdown = {
             "rounds": res0.rounds, "engine_ms_last_step": round(res0.ms_total, 3), "levels": res0.levels,
+            "pass_flags": res0.pass_flags,
             "per_round": [{"level": st["level"], "level_edges": st["level_arcs"], "live_edges": st["live_arcs"],
                            "fragments": st["active_components"], "hooks": st["hooks"]} for st in s0],
         }
-        kernels = {k: {"launches": v["launches"], "ms_per_step": v["ms"],
-                       "algorithmic_bytes": round(v["bytes"]),
-                       "achieved_gbs": round(v["achieved_gbs"], 1) if v["achieved_gbs"] else None,
-                       "frac": round(v["achieved_gbs"] / HBM_PEAK_GBS, 4) if v["achieved_gbs"] else None}
-                   for k, v in sorted(ktab.items(), key=lambda kv: -kv[1]["ms"])}
+        kernels = kernels_obj(ktab, tag)
         cpu = cpu_omp = cpu_nx = e2e = None
-        scaling_base = None
         if world == 1 and not args.no_cpu_baseline:
             e2e, g = end_to_end(edges, gen_s, res0)
             cpu_omp = cpu_baseline_omp(g, res0, tag)

@@ -2967,6 +2967,7 @@ struct RoundSlot {
   unsigned long long nact_in;  // active fragments this round started from (a level's first round: the level's)
   unsigned long long pending;  // pending edges after the level's pass (counter C_PENDING)
   unsigned long long weight;   // MSF weight so far (counter C_WEIGHT)
+  unsigned long long span;     // counter C_LONG: a level-0 edge spans > 1 bucket (the windowed round fell back)
 };
 
 __device__ __forceinline__ void write_report(RoundSlot *slot, unsigned long long seq, const unsigned long long *cnt,
@@ -2977,6 +2978,7 @@ __device__ __forceinline__ void write_report(RoundSlot *slot, unsigned long long
   const unsigned long long err = __hip_atomic_load(cnt + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned long long pending = __hip_atomic_load(cnt + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned long long weight = __hip_atomic_load(cnt + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long span = __hip_atomic_load(cnt + 10, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // The slot is coherent (uncached) host memory: its stores bypass the L2, so draining them
   // (vmcnt(0)) before the seq store orders them for the host's acquire load of seq. No
   // __threadfence_system(): its L2 write-back of every dirty line held the next round's first
@@ -2988,6 +2990,7 @@ __device__ __forceinline__ void write_report(RoundSlot *slot, unsigned long long
   slot->nact_in = nact_in;
   slot->pending = pending;
   slot->weight = weight;
+  slot->span = span;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(&slot->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -3345,11 +3348,14 @@ struct ghs_solver {
   bool rs_fold = false;         // apply_hooks left partial totals for contract to fold in
   uint64_t dense_n = 0;
   uint64_t hook_S = 0;          // the padded slot count of the last hook_slots (hook_owner's bound)
+  bool tail_ran = false;        // a level finished in the LDS tail (k_tail_*)
   // bucketed rounds (single rank, lattice-like graphs; k_bucket / k_bmin): the record buffers,
   // the offsets table, the bucket geometry, and the per-solve / per-round decisions
   uint4 *rec = nullptr;         // records (a, b, key): 16 B each
   uint64_t *wstart = nullptr;   // windowed round 0: each bucket's first edge (nb + 1)
   bool windowed = true;         // level 0 round 0 of a lattice-like solve windowed (k_wmin)
+  bool windowed_enq = false;    // ... was enqueued this solve (it ran unless k_select's span flag was set)
+  bool windowed_ran = false;    // ... and ran (the span flag of its round report was clear)
   bool state_init_pending = false;  // one rank: best / par initialised by level 0's first round
   uint32_t *bk_off = nullptr;
   uint32_t bk_bs = 13, bk_nb = 0;
@@ -4108,6 +4114,7 @@ static int enqueue_minedge(ghs_solver *s) {
       const unsigned g = s->arcs_known ? grid_for(s->cur_arcs, ARCS_PER_BLOCK, s->ident_g) : s->ident_g;
       const uint64_t items = s->arcs_known ? s->cur_arcs : 0;
       if (windowed0) {
+        s->windowed_enq = true;
         // windowed round 0 (k_wmin over the edge list); k_bucket / k_bmin run instead only if a
         // level-0 edge spans more than one bucket (k_select's flag)
         const unsigned long long *far = s->cnt + C_LONG;
@@ -4406,6 +4413,7 @@ static int run_level_pipelined(ghs_solver *s) {
       nact_prev = r.nact_in;
       if (s->level == 0) s->select_out = S;
       else if (s->filter_run && !s->filter_out) s->filter_out = S + s->rem_total;
+      if (s->level == 0 && s->windowed_enq) s->windowed_ran = hs->span == 0;
       if (s->debug) {
         uint32_t g[2] = {0, 0};
         (void)hipMemcpy(g, s->giant, 8, hipMemcpyDeviceToHost);
@@ -5012,7 +5020,11 @@ int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *
     result->canon_edges = s->e_hi - s->e_lo;
     result->select_out = s->select_out;
     result->filter_out = s->filter_out;
-    result->pass_flags = (s->bucketed ? 1u : 0u) | (s->lattice ? 2u : 0u);
+    result->pass_flags = (s->bucketed ? 1u : 0u) | (s->lattice ? 2u : 0u) | (s->windowed_ran ? 4u : 0u) |
+                         (s->tail_ran ? 8u : 0u);
+    result->ms_setup = result->ms_solve = result->ms_gather = 0;
+    result->reused = 0;
+    result->reserved = 0;
   }
   return GHS_OK;
 }

@@ -19,16 +19,23 @@ def _rec(kernel, ms, rnd=0):
     return {"kernel": kernel, "ms": ms, "round": rnd, "level": 0, "items": 0}
 
 
+class _Res:
+    def __init__(self, pass_flags):
+        self.pass_flags = pass_flags
+
+
 def test_windowed_round_charges_k_wmin_only():
-    recs = [_rec("k_wstarts", 0.01), _rec("k_wmin", 1.0), _rec("k_bucket", 0.005), _rec("k_bmin", 0.004)]
-    tab = bench.kernel_table(recs, STATS, None, N)
+    """pass_flags bit 2 (the library's span flag): level 0's round 0 ran windowed —
+    even where the fallback launches took longer than k_wmin, the bytes go to k_wmin."""
+    recs = [_rec("k_wstarts", 0.01), _rec("k_wmin", 1.0), _rec("k_bucket", 2.0), _rec("k_bmin", 2.0)]
+    tab = bench.kernel_table(recs, STATS, _Res(bench.PASS_WINDOWED), N)
     assert tab["k_wmin"]["bytes"] == 32.0 * 2 * N + 12.0 * N
     assert tab["k_bucket"]["bytes"] == 0.0 and tab["k_bmin"]["bytes"] == 0.0
 
 
 def test_fallback_round_charges_the_bucketed_kernels():
     recs = [_rec("k_wstarts", 0.01), _rec("k_wmin", 0.003), _rec("k_bucket", 0.8), _rec("k_bmin", 0.9)]
-    tab = bench.kernel_table(recs, STATS, None, N)
+    tab = bench.kernel_table(recs, STATS, _Res(0), N)
     assert tab["k_wmin"]["bytes"] == 0.0
     assert tab["k_bucket"]["bytes"] > 0 and tab["k_bmin"]["bytes"] > 0
 
