@@ -3148,6 +3148,419 @@ __global__ __launch_bounds__(BLOCK) void k_select_lb(const uint8_t *__restrict__
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// The LDS tail of a level (one rank). Once a level's active fragments fit a workgroup's LDS
+// (<= TAIL_MAX), its remaining rounds — the reference's last TEST / REPORT / CHANGEROOT /
+// INITIATE exchanges of a level, ghs_implementation.py:235-387 — run without any global atomic and
+// without n-sized arrays: the fragments get dense ids 0..F0-1 (their order in the active list),
+// every edge is relabelled ONCE to the dense pair of its fragments, and each later round keeps
+// every fragment's minimum in LDS per block.
+//   k_tail_map    dmap[act[i]] = i; the tail's control block, R = identity, the root list
+//   k_tail_open   (round 0 of the tail) every live edge: a, b -> lab -> dmap (its dense fragments);
+//                 intra-fragment edges dropped, the rest compacted to the block's region of the
+//                 tail buffer as one 12-byte record (da | db << 16, key); each end's candidate
+//                 min'ed into the block's LDS minima; the block's minima -> its row of `partial`
+//   k_tail_hook   one slot per active root: the minimum over the blocks' rows, and its CONNECT
+//                 target (the edge's canonical ends -> their fragments at the tail's start ->
+//                 their dense roots now); MSF flag of the edge
+//   k_tail_round  every block first applies the hooks in LDS (mutual pairs keep the smaller root,
+//                 pointer jumping, R[d] = dense root of every dense id, the next active roots) —
+//                 the same result in every block, no grid barrier — then streams its records
+//                 (a candidate only where R[da] != R[db]) into its LDS minima and row. A round that
+//                 starts with <= 1 active root finishes the level instead: lab of every fragment of
+//                 the level = its final root, the round report.
+// Per round: one stream of the 12-byte records + two launch boundaries, instead of the round
+// kernels' relabel gathers, LDS-cache misses to best[], hook, jump and select over n-sized arrays.
+// No grid barrier: a launch boundary orders A -> B -> A (so no co-residency assumption: ranks
+// sharing the device, e.g. ghs_mst_emulated, cannot deadlock it).
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t TAIL_MAX = 12288;        // dense fragments: LDS minima 96 KiB + 2 x 24 KiB of u16 tables
+constexpr uint32_t TAIL_T = 1024;           // threads of the streaming tail kernels (16 waves, 1 block per CU)
+constexpr uint32_t TAIL_G = 256;            // their blocks = rows of `partial`
+constexpr uint32_t TAIL_ROUNDS_MAX = 32;    // a tail round at least halves the roots: <= 14 rounds
+constexpr uint32_t TAIL_HS = 16;            // k_tail_hook: slots per 256-thread block (16 row groups)
+static_assert(TAIL_MAX <= 65536, "dense ids are packed as 16-bit pairs");
+
+struct TailCtl {
+  uint32_t F0;        // dense fragments (the active list at the tail's start)
+  uint32_t done;      // the level is complete (lab written)
+  uint32_t rounds;    // tail rounds streamed (set when done)
+  uint32_t err;
+  uint64_t Q;         // each block's region stride in the tail buffer
+  uint64_t nroots[TAIL_ROUNDS_MAX + 1];  // active roots of round r (its list: droot[r & 1])
+  uint64_t live[TAIL_ROUNDS_MAX];        // live (inter-fragment) edges round r scanned
+  uint64_t edges[TAIL_ROUNDS_MAX];       // MSF edges (C_EDGES) once round r's hooks are counted
+};
+
+struct TailBufs {
+  TailCtl *ctl;
+  uint32_t *dmap;      // root label -> dense id (n entries; only the tail's roots are meaningful)
+  uint64_t *partial;   // TAIL_G rows x TAIL_MAX block minima
+  uint32_t *R[2];      // dense id -> dense root during round r: R[r & 1]
+  uint32_t *droot[2];  // round r's active roots (ascending dense ids): droot[r & 1]
+  uint32_t *ghook;     // per dense root: CONNECT target (dense root) of its minimum edge
+  uint64_t *gkey;      // per dense root: its minimum key (KEY_NONE: no outgoing edge)
+  uint32_t *blive;     // per block: live edges of the round it streamed
+  uint32_t *bcnt;      // per block: records in its region of the tail buffer
+  uint32_t *rec;       // the tail buffer: da | db << 16
+  uint64_t *rkey;      //   ... and the key
+};
+
+__global__ void k_tail_map(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact, TailBufs tb) {
+  const uint32_t F = (uint32_t)*d_nact;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < F; i += gridDim.x * blockDim.x) {
+    tb.dmap[act[i]] = i;
+    tb.R[0][i] = i;
+    tb.droot[0][i] = i;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    TailCtl *c = tb.ctl;
+    c->F0 = F;
+    c->done = 0;
+    c->rounds = 0;
+    c->err = 0;
+    c->nroots[0] = F;
+  }
+}
+
+// a wave's survivors staged in LDS for coalesced stores (12-byte records)
+struct TailStage {
+  uint32_t p[WAVE * 4];
+  uint64_t k[WAVE * 4];
+};
+
+// the block's LDS minima -> its row of `partial` (one entry per active root, in root-list order)
+__device__ __forceinline__ void tail_row(const unsigned long long *s_best, const uint16_t *s_root, uint32_t nroot,
+                                         uint64_t *__restrict__ row) {
+  for (uint32_t i = threadIdx.x; i < nroot; i += blockDim.x) row[i] = s_best[s_root[i]];
+}
+
+__device__ __forceinline__ void lds_min_u64(unsigned long long *s, uint32_t i, uint64_t k) {
+  if (k < s[i]) atomicMin(&s[i], (unsigned long long)k);  // a plain read first: slots only decrease
+}
+
+__global__ __launch_bounds__(TAIL_T) void k_tail_open(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
+                                                      const uint64_t *__restrict__ key, SegView in,
+                                                      const uint32_t *__restrict__ lab, TailBufs tb) {
+  __shared__ unsigned long long s_best[TAIL_MAX];
+  __shared__ TailStage s_stage[TAIL_T / WAVE];
+  __shared__ uint32_t s_wcnt[TAIL_T / WAVE];
+  __shared__ uint32_t s_seg[2];
+  __shared__ uint32_t s_live;
+  const uint32_t F = tb.ctl->F0;
+  for (uint32_t i = threadIdx.x; i < F; i += TAIL_T) s_best[i] = KEY_NONE;
+  const uint64_t T = in.prefix[in.nseg];
+  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
+  const uint64_t vb = Q * blockIdx.x;
+  const uint64_t ve = (vb + Q < T) ? vb + Q : T;
+  if (threadIdx.x == 0) {
+    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
+    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
+    s_live = 0;
+    if (blockIdx.x == 0) tb.ctl->Q = Q;
+  }
+  __syncthreads();
+  const uint32_t slo = s_seg[0], shi = s_seg[1];
+  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+  constexpr uint64_t STEP = (uint64_t)TAIL_T * 4;
+  uint64_t out_n = 0;
+  uint32_t live_n = 0;
+  for (uint64_t v0 = vb; v0 < ve; v0 += STEP) {
+    const uint64_t v = v0 + (uint64_t)threadIdx.x * 4;
+    const bool in_range = v < ve;
+    const uint64_t ph = tile_phys(in, slo, shi, v, ve);
+    const uint4 a4 = *reinterpret_cast<const uint4 *>(src + ph), b4 = *reinterpret_cast<const uint4 *>(dst + ph);
+    const ulonglong2 k01 = *reinterpret_cast<const ulonglong2 *>(key + ph),
+                     k23 = *reinterpret_cast<const ulonglong2 *>(key + ph + 2);
+    const uint32_t A[4] = {a4.x, a4.y, a4.z, a4.w}, B[4] = {b4.x, b4.y, b4.z, b4.w};
+    const uint64_t K[4] = {k01.x, k01.y, k23.x, k23.y};
+    bool valid[4];
+    uint32_t la[4], lb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // the fragments now (one hop: lab of the carried labels is current)
+      valid[j] = in_range & (A[j] != LABEL_NONE);
+      la[j] = lab[valid[j] ? A[j] : 0u];
+      lb[j] = lab[valid[j] ? B[j] : 0u];
+    }
+    uint32_t da[4], db[4], mask = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool live = valid[j] & (la[j] != lb[j]);
+      da[j] = tb.dmap[live ? la[j] : 0u];
+      db[j] = tb.dmap[live ? lb[j] : 0u];
+      mask |= live ? (1u << j) : 0u;
+    }
+    uint32_t P[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!((mask >> j) & 1u)) continue;
+      if (da[j] >= F || db[j] >= F) {  // a live edge must join two active fragments
+        atomicOr(&tb.ctl->err, 1u);
+        mask &= ~(1u << j);
+        continue;
+      }
+      lds_min_u64(s_best, da[j], K[j]);
+      lds_min_u64(s_best, db[j], K[j]);
+      P[j] = da[j] | (db[j] << 16);
+    }
+    live_n += __popc(mask);
+    // survivors -> this block's region of the tail buffer [vb, vb + Q), staged per wave
+    uint32_t lane_excl, wave_before, wave_cnt, total;
+    block_offsets_w((uint32_t)__popc(mask), s_wcnt, &lane_excl, &wave_before, &wave_cnt, &total);
+    TailStage &ws = s_stage[wid];
+    uint32_t p = lane_excl;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if ((mask >> j) & 1u) {
+        ws.p[p] = P[j];
+        ws.k[p] = K[j];
+        ++p;
+      }
+    wave_sync_lds();
+    const uint64_t o = vb + out_n + wave_before;
+    for (uint32_t i = lane; i < wave_cnt; i += WAVE) {
+      tb.rec[o + i] = ws.p[i];
+      tb.rkey[o + i] = ws.k[i];
+    }
+    wave_sync_lds();
+    out_n += total;
+  }
+  for (int d = WAVE / 2; d > 0; d >>= 1) live_n += __shfl_xor(live_n, d);
+  if (lane == 0) atomicAdd(&s_live, live_n);
+  __syncthreads();
+  // the block's minima of every dense fragment (round 0: the root list is the identity)
+  uint64_t *row = tb.partial + (uint64_t)blockIdx.x * TAIL_MAX;
+  for (uint32_t i = threadIdx.x; i < F; i += TAIL_T) row[i] = s_best[i];
+  if (threadIdx.x == 0) {
+    tb.bcnt[blockIdx.x] = (uint32_t)out_n;
+    tb.blive[blockIdx.x] = s_live;
+  }
+}
+
+// One active root per slot (root-list order): the blocks' minima reduced (16 row groups per slot),
+// the root's CONNECT target, its MSF flag. Block 0 also totals the streamed round's live edges.
+__global__ __launch_bounds__(256) void k_tail_hook(TailBufs tb, uint32_t r, const uint32_t *__restrict__ act0,
+                                                   const uint32_t *__restrict__ lab, const uint32_t *__restrict__ eu,
+                                                   const uint32_t *__restrict__ ev, uint8_t *__restrict__ in_mst,
+                                                   uint32_t nblocks, unsigned long long *__restrict__ err) {
+  __shared__ unsigned long long s_part[256];
+  TailCtl *c = tb.ctl;
+  if (c->done) return;  // r: the round just streamed
+  const uint32_t nroot = (uint32_t)c->nroots[r];
+  if (blockIdx.x == 0 && threadIdx.x < WAVE) {
+    uint64_t t = 0;
+    for (uint32_t b = threadIdx.x; b < nblocks; b += WAVE) t += tb.blive[b];
+    for (int d = WAVE / 2; d > 0; d >>= 1) t += __shfl_xor(t, d);
+    if (threadIdx.x == 0) c->live[r] = t;
+  }
+  const uint32_t s = threadIdx.x % TAIL_HS, g = threadIdx.x / TAIL_HS;  // slot, row group
+  const uint32_t i = blockIdx.x * TAIL_HS + s;
+  if (blockIdx.x * TAIL_HS >= nroot) return;  // block-uniform
+  uint64_t m = KEY_NONE;
+  if (i < nroot) {
+    constexpr uint32_t GROUPS = 256 / TAIL_HS;
+    uint64_t x[TAIL_G / GROUPS];
+#pragma unroll
+    for (uint32_t k = 0; k < TAIL_G / GROUPS; ++k) {
+      const uint32_t b = g + k * GROUPS;
+      x[k] = b < nblocks ? tb.partial[(uint64_t)b * TAIL_MAX + i] : KEY_NONE;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < TAIL_G / GROUPS; ++k) m = umin64(m, x[k]);
+  }
+  s_part[threadIdx.x] = m;
+  __syncthreads();
+  if (g != 0 || i >= nroot) return;
+  for (uint32_t k = 1; k < 256 / TAIL_HS; ++k) m = umin64(m, s_part[k * TAIL_HS + s]);
+  const uint32_t d = tb.droot[r & 1][i];
+  const uint32_t *R = tb.R[r & 1];
+  const uint32_t F = c->F0;
+  uint32_t o = LABEL_NONE;
+  if (m != KEY_NONE) {
+    // the minimum edge's ends -> their fragments at the tail's start -> dense ids -> dense roots now
+    const uint32_t eid = (uint32_t)m;
+    const uint32_t fa = find_lab(lab, eu[eid], err), fb = find_lab(lab, ev[eid], err);
+    const uint32_t xa = tb.dmap[fa], xb = tb.dmap[fb];
+    if (xa >= F || xb >= F || act0[xa] != fa || act0[xb] != fb) {
+      atomicOr(err, 2ull);  // the ends' fragments must be the tail's
+      m = KEY_NONE;
+    } else {
+      const uint32_t ra = R[xa], rb = R[xb];
+      if (ra != d && rb != d) atomicOr(err, 2ull);  // the chosen edge must leave d
+      o = ra == d ? rb : ra;
+      in_mst[eid] = 1;  // both members of a mutual pair mark the same edge
+    }
+  }
+  tb.gkey[d] = m;
+  tb.ghook[d] = o;
+}
+
+// Every block applies the last round's hooks (identical LDS computation in every block), then
+// streams its records — or, when <= 1 root stays active, block 0 finishes the level.
+__global__ __launch_bounds__(TAIL_T) void k_tail_round(TailBufs tb, uint32_t r, const uint32_t *__restrict__ act0,
+                                                       uint32_t *__restrict__ lab, unsigned long long *__restrict__ cnt,
+                                                       unsigned long long *__restrict__ err) {
+  __shared__ unsigned long long s_best[TAIL_MAX];  // the prologue's pointer table first (u32 view)
+  __shared__ uint16_t s_R[TAIL_MAX];
+  __shared__ uint16_t s_root[TAIL_MAX];
+  __shared__ uint32_t s_wsum[TAIL_T / WAVE];
+  __shared__ unsigned long long s_tw, s_tc;
+  __shared__ uint32_t s_live;
+  TailCtl *c = tb.ctl;
+  if (c->done) return;
+  const uint32_t F = c->F0;  // r: the round about to stream (round r - 1 hooked last)
+  const uint32_t nprev = (uint32_t)c->nroots[r - 1];
+  const uint32_t *prev = tb.droot[(r - 1) & 1];
+  uint32_t *P = reinterpret_cast<uint32_t *>(s_best);  // dense pointer forest (prologue only)
+  constexpr uint32_t MARK = 0x80000000u;
+  if (threadIdx.x == 0) {
+    s_tw = 0;
+    s_tc = 0;
+    s_live = 0;
+  }
+  for (uint32_t d = threadIdx.x; d < F; d += TAIL_T) {
+    P[d] = d;
+    s_R[d] = (uint16_t)tb.R[(r - 1) & 1][d];
+  }
+  __syncthreads();
+  // the hooks of round r - 1's active roots
+  for (uint32_t i = threadIdx.x; i < nprev; i += TAIL_T) {
+    const uint32_t d = prev[i], o = tb.ghook[d];
+    if (o != LABEL_NONE) P[d] = o;
+  }
+  __syncthreads();
+  // a mutual pair (d <-> o over their shared minimum) keeps its smaller member as the root
+  for (uint32_t i = threadIdx.x; i < nprev; i += TAIL_T) {
+    const uint32_t d = prev[i], o = P[d] & ~MARK;
+    if (o != d && (P[o] & ~MARK) == d && d < o) atomicOr(&P[d], MARK);
+  }
+  __syncthreads();
+  unsigned long long tw = 0, tc = 0;
+  for (uint32_t i = threadIdx.x; i < nprev; i += TAIL_T) {
+    const uint32_t d = prev[i];
+    if (P[d] & MARK) {
+      P[d] = d;
+    } else if (P[d] != d) {  // d hooked: one MSF edge
+      tw += tb.gkey[d] >> 32;
+      tc += 1;
+    }
+  }
+  __syncthreads();
+  for (int it = 0; it < 32; ++it) {  // pointer jumping to the roots
+    int more = 0;
+    for (uint32_t d = threadIdx.x; d < F; d += TAIL_T) {
+      const uint32_t p = P[d], pp = P[p];
+      if (pp != p) {
+        P[d] = pp;
+        more = 1;
+      }
+    }
+    if (!__syncthreads_or(more)) break;
+  }
+  for (uint32_t d = threadIdx.x; d < F; d += TAIL_T) s_R[d] = (uint16_t)P[s_R[d]];
+  // next roots: round r - 1's roots that had an edge and stayed roots (ascending: a block scan)
+  uint32_t nroot = 0;
+  for (uint32_t base = 0; base < nprev; base += TAIL_T) {
+    const uint32_t i = base + threadIdx.x;
+    uint32_t d = 0;
+    bool keep = false;
+    if (i < nprev) {
+      d = prev[i];
+      keep = tb.gkey[d] != KEY_NONE && P[d] == d;
+    }
+    uint32_t tot;
+    const uint32_t before = block_excl_scan<TAIL_T>(keep ? 1u : 0u, s_wsum, &tot);
+    if (keep) s_root[nroot + before] = (uint16_t)d;
+    nroot += tot;
+  }
+  for (int dd = WAVE / 2; dd > 0; dd >>= 1) {
+    tw += __shfl_xor(tw, dd);
+    tc += __shfl_xor(tc, dd);
+  }
+  if ((threadIdx.x & (WAVE - 1)) == 0 && tc) {
+    atomicAdd(&s_tw, tw);
+    atomicAdd(&s_tc, tc);
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) {
+      if (s_tc) {
+        (void)atomicAdd(cnt + 2, s_tw);  // C_WEIGHT, C_EDGES (returning: complete before the report)
+        (void)atomicAdd(cnt + 3, s_tc);
+      }
+      const unsigned long long edges = __hip_atomic_load(cnt + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      c->edges[r - 1] = edges;
+    }
+    if (nroot <= 1 || r >= TAIL_ROUNDS_MAX) {
+      // the level is complete: every fragment of the level takes its final root's label
+      for (uint32_t d = threadIdx.x; d < F; d += TAIL_T) {
+        const uint32_t x = act0[d], root = act0[s_R[d]];
+        if (root != x) lab[x] = root;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        if (r >= TAIL_ROUNDS_MAX && nroot > 1) atomicOr(err, 4ull);
+        if (c->err) atomicOr(err, 2ull);
+        c->done = 1;
+        c->rounds = r;
+        cnt[0] = 0;  // C_LIVE: no live edge left in the level
+      }
+      return;
+    }
+    for (uint32_t d = threadIdx.x; d < F; d += TAIL_T) tb.R[r & 1][d] = s_R[d];
+    for (uint32_t i = threadIdx.x; i < nroot; i += TAIL_T) tb.droot[r & 1][i] = s_root[i];
+    if (threadIdx.x == 0) c->nroots[r] = nroot;
+  }
+  if (nroot <= 1 || r >= TAIL_ROUNDS_MAX) return;  // block 0 finishes the level
+  // stream this block's records into the LDS minima of the current roots
+  for (uint32_t d = threadIdx.x; d < F; d += TAIL_T) s_best[d] = KEY_NONE;
+  __syncthreads();
+  const uint64_t base = c->Q * blockIdx.x;
+  const uint32_t n = tb.bcnt[blockIdx.x];
+  uint32_t live_n = 0;
+  for (uint32_t e0 = threadIdx.x * 4; e0 < n; e0 += TAIL_T * 4) {
+    const uint32_t *pr = tb.rec + base + e0;
+    const uint64_t *pk = tb.rkey + base + e0;
+    uint32_t p[4];
+    uint64_t k[4];
+    if (e0 + 4 <= n) {  // base is a multiple of 4: 16-B aligned
+      const uint4 q = *reinterpret_cast<const uint4 *>(pr);
+      const ulonglong2 k01 = *reinterpret_cast<const ulonglong2 *>(pk), k23 = *reinterpret_cast<const ulonglong2 *>(pk + 2);
+      p[0] = q.x; p[1] = q.y; p[2] = q.z; p[3] = q.w;
+      k[0] = k01.x; k[1] = k01.y; k[2] = k23.x; k[3] = k23.y;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        p[j] = e0 + j < n ? pr[j] : 0u;
+        k[j] = e0 + j < n ? pk[j] : KEY_NONE;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (e0 + j >= n) continue;
+      const uint32_t ra = s_R[p[j] & 0xffffu], rb = s_R[p[j] >> 16];
+      if (ra == rb) continue;
+      ++live_n;
+      lds_min_u64(s_best, ra, k[j]);
+      lds_min_u64(s_best, rb, k[j]);
+    }
+  }
+  for (int dd = WAVE / 2; dd > 0; dd >>= 1) live_n += __shfl_xor(live_n, dd);
+  if ((threadIdx.x & (WAVE - 1)) == 0) atomicAdd(&s_live, live_n);
+  __syncthreads();
+  tail_row(s_best, s_root, nroot, tb.partial + (uint64_t)blockIdx.x * TAIL_MAX);
+  if (threadIdx.x == 0) tb.blive[blockIdx.x] = s_live;
+}
+
+// the report of a batch of tail rounds (enqueued after its copy of the control block): nact_out 0
+// when the level is complete, else the active roots of the last round streamed (more rounds follow)
+__global__ void k_tail_report(const TailBufs tb, uint32_t last, RoundSlot *slot, unsigned long long seq,
+                              unsigned long long *cnt) {
+  const TailCtl *c = tb.ctl;
+  write_report(slot, seq, cnt, c->done ? 0ull : (unsigned long long)c->nroots[last], c->F0);
+}
+
+
 static inline unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap) {
   uint64_t g = (items + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -3209,6 +3622,7 @@ struct HostRes {
   RoundSlot *h_slot = nullptr;          // pinned, coherent ring of round reports (host view)
   RoundSlot *d_slot = nullptr;          // the same ring, device view
   uint32_t *h_sample = nullptr;         // pinned sample buffer
+  TailCtl *h_tail = nullptr;            // pinned copy of the LDS tail's control block (its round stats)
   std::vector<hipEvent_t> ev_pool;      // timing events, 6 per round
   hipEvent_t pass_ev[4] = {};           // the canonical passes' events
   hipEvent_t plan_ev = nullptr;         // the weight sample has landed in h_sample
@@ -3227,6 +3641,7 @@ static int hostres_init(HostRes *r) {
   GHS_HIP_CHECK(hipHostMalloc((void **)&r->h_slot, SLOT_RING * sizeof(RoundSlot), hipHostMallocMapped | hipHostMallocCoherent));
   GHS_HIP_CHECK(hipHostGetDevicePointer((void **)&r->d_slot, r->h_slot, 0));
   GHS_HIP_CHECK(hipHostMalloc((void **)&r->h_sample, 16384 * 4, hipHostMallocDefault));
+  GHS_HIP_CHECK(hipHostMalloc((void **)&r->h_tail, sizeof(TailCtl), hipHostMallocDefault));
   for (int i = 0; i < 4; ++i) GHS_HIP_CHECK(hipEventCreateWithFlags(&r->pass_ev[i], TIMING_EVENT_FLAGS));
   GHS_HIP_CHECK(hipEventCreateWithFlags(&r->plan_ev, hipEventDisableTiming));
   GHS_HIP_CHECK(hipEventCreateWithFlags(&r->sync_ev, hipEventDisableTiming));
@@ -3246,6 +3661,8 @@ static void hostres_free(HostRes *r) {
   if (r->h_cnt) (void)hipHostFree(r->h_cnt);
   if (r->h_slot) (void)hipHostFree(r->h_slot);
   if (r->h_sample) (void)hipHostFree(r->h_sample);
+  if (r->h_tail) (void)hipHostFree(r->h_tail);
+  r->h_tail = nullptr;
   r->h_cnt = nullptr;
   r->h_slot = r->d_slot = nullptr;
   r->h_sample = nullptr;
@@ -3349,6 +3766,8 @@ struct ghs_solver {
   uint64_t dense_n = 0;
   uint64_t hook_S = 0;          // the padded slot count of the last hook_slots (hook_owner's bound)
   bool tail_ran = false;        // a level finished in the LDS tail (k_tail_*)
+  TailBufs tail{};              // the LDS tail's arrays (one rank; tail.ctl == nullptr: no tail)
+  bool tail_on = true;          // GHS_OPT_NO_TAIL clears it
   // bucketed rounds (single rank, lattice-like graphs; k_bucket / k_bmin): the record buffers,
   // the offsets table, the bucket geometry, and the per-solve / per-round decisions
   uint4 *rec = nullptr;         // records (a, b, key): 16 B each
@@ -3587,6 +4006,19 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
   }
   if (s) s->cap_arcs = cap;
   p = carve(C_COUNT * sizeof(unsigned long long)); if (s) s->cnt = (unsigned long long *)p;
+  if (local_edges == m) {  // one rank: the LDS tail's arrays (its records go to the idle edge buffer)
+    p = carve(N * 4); if (s) s->tail.dmap = (uint32_t *)p;
+    p = carve((size_t)TAIL_G * TAIL_MAX * 8); if (s) s->tail.partial = (uint64_t *)p;
+    for (int b = 0; b < 2; ++b) {
+      p = carve(TAIL_MAX * 4); if (s) s->tail.R[b] = (uint32_t *)p;
+      p = carve(TAIL_MAX * 4); if (s) s->tail.droot[b] = (uint32_t *)p;
+    }
+    p = carve(TAIL_MAX * 4); if (s) s->tail.ghook = (uint32_t *)p;
+    p = carve(TAIL_MAX * 8); if (s) s->tail.gkey = (uint64_t *)p;
+    p = carve(TAIL_G * 4); if (s) s->tail.blive = (uint32_t *)p;
+    p = carve(TAIL_G * 4); if (s) s->tail.bcnt = (uint32_t *)p;
+    p = carve(sizeof(TailCtl)); if (s) s->tail.ctl = (TailCtl *)p;
+  }
   // bucketed rounds (single rank, n <= 2^28): records (an edge gives at most two) + offsets
   uint32_t bs = 0, nb = 0;
   if (local_edges == m && bucket_geometry(n, &bs, &nb)) {
@@ -4369,6 +4801,85 @@ static int decide_bucketed(ghs_solver *s) {
   return GHS_OK;
 }
 
+
+// ---- the LDS tail: the rest of a level once its active fragments fit LDS (one rank) ---------
+// Enters at a round >= 1 of a level whose exact active count is in [2, TAIL_MAX] (the host has
+// read every earlier report); enqueues batches of tail rounds (k_tail_round + k_tail_hook, no-ops
+// once the level is done) behind k_tail_map + k_tail_open, each batch ending with a copy of the
+// control block and its report; reads the tail's per-round stats from that copy and closes the
+// level. Rounds whose launches follow the finishing round exit at once.
+constexpr uint32_t TAIL_BATCH = 6;  // tail rounds per batch (R-MAT levels finish in 3-5, lattices in 5-7)
+constexpr uint64_t TAIL_TRY = 32ull * TAIL_MAX;  // a bound below this: read the exact count first
+
+static bool tail_usable(const ghs_solver *s) {
+  return s->tail_on && s->tail.ctl && s->cfg.num_ranks <= 1 && !s->level_dense && s->level_round >= 1 &&
+         !s->act_ident;
+}
+
+static int run_tail(ghs_solver *s) {
+  hipStream_t st = s->stream;
+  TailBufs tb = s->tail;
+  const ArcBuf &I = s->buf[s->cur], &O = s->buf[s->cur ^ 1];
+  tb.rec = O.src;   // the idle edge buffer holds the tail's records
+  tb.rkey = O.key;
+  if (s->scan_pending) flush_scan(s);
+  const uint32_t *act0 = s->act[s->act_cur];
+  const unsigned long long *d_nact = cur_act_count(s);
+  SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
+  const uint32_t F0 = (uint32_t)s->nact;
+  const unsigned hook_g = (F0 + TAIL_HS - 1) / TAIL_HS;
+  const uint32_t round0 = s->round, lr0 = s->level_round;
+  unsigned long long *err = s->cnt + C_ERR;
+  {
+    KT(GHS_K_TAIL_OPEN, s->arcs_known ? s->cur_arcs : 0);
+    k_tail_map<<<grid_for(F0, 256, 64), 256, 0, st>>>(act0, d_nact, tb);
+    k_tail_open<<<TAIL_G, TAIL_T, 0, st>>>(I.src, I.dst, I.key, in, s->lab, tb);
+  }
+  {
+    KT(GHS_K_TAIL_HOOK, F0);
+    k_tail_hook<<<hook_g, 256, 0, st>>>(tb, 0, act0, s->lab, s->eu, s->ev, s->in_mst, TAIL_G, err);
+  }
+  GHS_HIP_CHECK(hipGetLastError());
+  uint32_t r = 1;  // the next tail round to stream
+  for (;;) {
+    const uint32_t last = std::min(r + TAIL_BATCH - 1, TAIL_ROUNDS_MAX);  // the batch's last round
+    for (; r <= last; ++r) {
+      s->round = round0 + r;  // the profile's round index of these launches
+      {
+        KT(GHS_K_TAIL_ROUND, 0);
+        k_tail_round<<<TAIL_G, TAIL_T, 0, st>>>(tb, r, act0, s->lab, s->cnt, err);
+      }
+      if (r < TAIL_ROUNDS_MAX) {
+        KT(GHS_K_TAIL_HOOK, 0);
+        k_tail_hook<<<hook_g, 256, 0, st>>>(tb, r, act0, s->lab, s->eu, s->ev, s->in_mst, TAIL_G, err);
+      }
+    }
+    GHS_HIP_CHECK(hipGetLastError());
+    const unsigned long long seq = ++s->res->seq;
+    RoundSlot *dslot = &s->d_slot[seq % SLOT_RING];
+    GHS_HIP_CHECK(hipMemcpyAsync(s->res->h_tail, tb.ctl, sizeof(TailCtl), hipMemcpyDeviceToHost, st));
+    k_tail_report<<<1, 1, 0, st>>>(tb, last, dslot, seq, s->cnt);
+    GHS_HIP_CHECK(hipGetLastError());
+    const RoundSlot *hs = s->h_slot + (seq % SLOT_RING);
+    if (int rc = wait_slot(s, hs, seq)) return rc;
+    if (hs->err) return fail_counters(s, hs->err, "in the LDS tail");
+    s->rep_weight = hs->weight;
+    s->rep_edges = hs->edges;
+    s->report_final = true;
+    if (hs->nact_out <= 1) break;
+    if (r > TAIL_ROUNDS_MAX) return fail_counters(s, 4, "in the LDS tail (round cap)");
+  }
+  const TailCtl &c = *s->res->h_tail;
+  const uint32_t rounds = std::min(c.rounds, TAIL_ROUNDS_MAX);
+  for (uint32_t t = 0; t < rounds; ++t) push_stats(s, lr0 + t, c.live[t], c.nroots[t], c.edges[t]);
+  s->round = round0 + rounds;
+  s->level_round = lr0 + rounds;
+  s->tail_ran = true;
+  if (s->ev_rec.size() > s->round) s->ev_rec.resize(s->round);
+  close_level(s);
+  return GHS_OK;
+}
+
 static int run_level_pipelined(ghs_solver *s) {
   if (!s->bucket_decided)
     if (int rc = decide_bucketed(s)) return rc;
@@ -4378,6 +4889,15 @@ static int run_level_pipelined(ghs_solver *s) {
   std::vector<unsigned long long> seqs(LEVEL_ROUND_CAP + s->lookahead + 1);
   for (;;) {
     if (issued < checked + 1 + s->lookahead) {
+      // the LDS tail: once the bound on the next round's active fragments is small, read the
+      // outstanding reports (the exact count), then finish the level there if it fits
+      if (issued >= 1 && s->nact <= TAIL_TRY && tail_usable(s)) {
+        if (checked < issued) goto check;
+        if (s->nact >= 2 && s->nact <= TAIL_MAX) {
+          s->round = round0 + issued;
+          return run_tail(s);
+        }
+      }
       if (issued >= LEVEL_ROUND_CAP) GHS_FAIL(GHS_E_ROUNDCAP, "round cap exceeded in a level");
       const unsigned long long seq = ++s->res->seq;
       seqs[issued] = seq;
@@ -4387,6 +4907,7 @@ static int run_level_pipelined(ghs_solver *s) {
       ++issued;
       continue;
     }
+  check:
     const RoundSlot *hs = s->h_slot + (checked % SLOT_RING);
     if (int rc = wait_slot(s, hs, seqs[checked])) return rc;
     RoundSlot r;
@@ -4565,6 +5086,7 @@ static int solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint
   s->time_rounds = (opt & GHS_OPT_TIME_ROUNDS) != 0;
   s->seed_runs = (opt & GHS_OPT_NO_SEED_RUNS) == 0;
   s->windowed = (opt & GHS_OPT_NO_WINDOW) == 0;
+  s->tail_on = (opt & GHS_OPT_NO_TAIL) == 0;
   s->dedup_max = s->cfg.dedup_max;
   {
     std::lock_guard<std::mutex> lock(g_prof_mutex);
@@ -5038,6 +5560,7 @@ int ghs_solver_reset(ghs_solver_t *s) {
   t.in_mst = s->in_mst; t.stream = s->stream; t.cfg = s->cfg;
   t.debug = s->debug; t.lookahead = s->lookahead; t.seed_runs = s->seed_runs; t.dedup_max = s->dedup_max;
   t.windowed = s->windowed;
+  t.tail_on = s->tail_on;
   t.detail = s->detail; t.time_rounds = s->time_rounds;
   t.group_cancel = s->group_cancel;
   { std::lock_guard<std::mutex> lock(g_prof_mutex); t.prof = g_prof_on; }

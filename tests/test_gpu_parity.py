@@ -908,5 +908,61 @@ def test_windowed_round0_vs_oracle(k, mode, extra, torch_cuda):
         eng = DeviceMST(e, config=_native.make_config(options=opt) if opt else None)
         res, _ = eng.run()
         assert res.pass_flags & 1 and res.pass_flags & 2  # lattice-like, bucketed level-0 rounds
+        # pass_flags bit 2: the windowed round ran (not with long edges: k_select's span flag)
+        assert bool(res.pass_flags & _native.PASS_WINDOWED) == (opt == 0 and extra == 0)
+        assert np.array_equal(eng.in_mst_host(), ref_in.astype(bool))
+        assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
+
+
+@pytest.mark.parametrize("graph", ["rmat", "rmat20", "ties", "forest", "readme", "grid", "grid-gradient"])
+@pytest.mark.parametrize("levels", [None, 1])
+@pytest.mark.parametrize("opt", ["default", "bucketed", "first"])
+def test_lds_tail_vs_oracle(graph, levels, opt, torch_cuda):
+    """The LDS tail (k_tail_*: a level's rounds once its active fragments fit LDS — dense fragment
+    ids, 12-byte records, per-block LDS minima, hooks and pointer jumping in LDS): the oracle's MSF
+    and totals on every graph kind and level plan, with the per-round kernels before it either
+    unbucketed or bucketed; the same flags as with the tail off (GHS_OPT_NO_TAIL); the round stats
+    add up (hooks = MSF edges) and pass_flags bit 3 says the tail ran."""
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import DeviceMST
+    ora = _oracle()
+    e = _test_graph(graph)
+    g = e.to_host()
+    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    kw = {} if levels is None else {"max_levels": levels}
+    base = {"default": 0, "bucketed": _native.OPT_BUCKETED, "first": _native.OPT_BUCKETED_FIRST}[opt]
+    on = DeviceMST(e, config=_native.make_config(options=base, **kw))
+    for _ in range(2):  # twice on the same workspace
+        res, stats = on.run()
+        assert np.array_equal(on.in_mst_host(), ref_in.astype(bool))
+        assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
+        assert sum(st["hooks"] for st in stats) == ref_k
+    if graph not in ("forest",):
+        assert res.pass_flags & _native.PASS_TAIL, (graph, list(stats))
+    off = DeviceMST(e, config=_native.make_config(options=base | _native.OPT_NO_TAIL, **kw))
+    res0, _ = off.run()
+    assert not res0.pass_flags & _native.PASS_TAIL
+    assert np.array_equal(off.in_mst_host(), ref_in.astype(bool))
+    assert res0.rounds == res.rounds  # the tail runs the same Boruvka rounds
+
+
+@pytest.mark.parametrize("seed,n,m,wmax", [(21, 300, 2000, 1), (22, 12000, 40000, 3), (23, 13000, 26000, 100),
+                                           (24, 40000, 400000, 0), (25, 200000, 300000, 7)])
+def test_lds_tail_tie_heavy_and_sizes(seed, n, m, wmax, torch_cuda):
+    """Tie-heavy random multigraphs around the tail's capacity (12288 dense fragments; graphs whose
+    first explicit round has just fewer or more fragments than that), all-equal weights: the
+    strict (w, eid) order decides every tie exactly as Kruskal."""
+    from distributed_ghs_implementation_amd import canonicalize
+    from distributed_ghs_implementation_amd.device import DeviceEdges, DeviceMST
+    ora = _oracle()
+    rng = np.random.default_rng(seed)
+    cg = canonicalize(n, u=rng.integers(0, n, m), v=rng.integers(0, n, m), w=rng.integers(0, wmax + 1, m))
+    e = DeviceEdges.from_host(cg)
+    g = e.to_host()
+    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    for levels in (None, 1):
+        from distributed_ghs_implementation_amd import _native
+        eng = DeviceMST(e, config=_native.make_config(**({} if levels is None else {"max_levels": levels})))
+        res, _ = eng.run()
         assert np.array_equal(eng.in_mst_host(), ref_in.astype(bool))
         assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
