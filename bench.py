@@ -142,10 +142,21 @@ def launch_bytes(rec, stats, res, n, windowed=frozenset()):
         return 21.0 * act  # act, par, lab, best, keep flag
     if k == "k_select_lb":
         return 2.0 * rec["items"]  # keep bytes, two passes
+    # the LDS tail (boruvka.hip k_tail_*): 256 blocks, one row of per-fragment minima each
+    if k == "k_tail_open":
+        # the live edges (a, b, key + lab / dense-id gathers) in, their 12-B records out, the rows
+        return 24.0 * live + 12.0 * live + 8.0 * act * TAIL_G
+    if k == "k_tail_round":
+        return 12.0 * live + 8.0 * act * TAIL_G  # the records, the rows of the round's roots
+    if k == "k_tail_hook":
+        return 8.0 * act * TAIL_G  # the rows, reduced per root
     return 0.0
 
 
-STAGE1 = ("k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>", "k_bucket", "k_bmin", "k_wstarts", "k_wmin")
+TAIL_G = 256  # boruvka.hip TAIL_G: the LDS tail's blocks (rows of block minima)
+# every kernel of a min-edge round's stage 1 (the tail's kernels and the bucketed ones also hook)
+STAGE1 = ("k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>", "k_bucket", "k_bmin", "k_wstarts", "k_wmin",
+          "k_tail_open", "k_tail_round", "k_tail_hook")
 
 
 PASS_WINDOWED = 0x4  # ghs_result_t.pass_flags: level 0's round 0 ran windowed (k_select's span flag clear)
