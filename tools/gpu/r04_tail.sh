@@ -21,3 +21,5 @@ for spec in rmat:24 grid:0; do
   timeout -k 10 240 python3 -u tools/round_profile.py $args > "$OUT/rounds_${wl}_$sc.txt" 2>&1 || { echo "round profile $spec failed"; tail -20 "$OUT/rounds_${wl}_$sc.txt"; exit 1; }
   cat "$OUT/rounds_${wl}_$sc.txt"
 done
+timeout -k 10 300 python3 -u tools/emu_native.py 26 8 4 > "$OUT/emu_native_s26_w8.txt" 2>&1 || { echo "emu failed"; tail -20 "$OUT/emu_native_s26_w8.txt"; exit 1; }
+cat "$OUT/emu_native_s26_w8.txt"
