@@ -182,6 +182,7 @@ __device__ __forceinline__ uint32_t block_offsets(uint32_t mine, uint32_t *s_wcn
 // Wave-level offsets for a block-wide compaction step: *lane_excl = items of lower lanes of the
 // wave, *wave_before = items of lower waves of the block, *wave_cnt = the wave's items,
 // *total = the block's. Every thread of the block must call it (two barriers).
+template <int NT = BLOCK>
 __device__ __forceinline__ void block_offsets_w(uint32_t mine, uint32_t *s_wcnt, uint32_t *lane_excl,
                                                 uint32_t *wave_before, uint32_t *wave_cnt, uint32_t *total) {
   const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
@@ -197,7 +198,7 @@ __device__ __forceinline__ void block_offsets_w(uint32_t mine, uint32_t *s_wcnt,
   __syncthreads();
   uint32_t before = 0, t = 0;
 #pragma unroll
-  for (int w = 0; w < BLOCK / WAVE; ++w) {
+  for (int w = 0; w < NT / WAVE; ++w) {
     if (w < wid) before += s_wcnt[w];
     t += s_wcnt[w];
   }
@@ -3350,7 +3351,7 @@ __global__ __launch_bounds__(TAIL_T) void k_tail_open(const uint32_t *__restrict
     live_n += __popc(mask);
     // survivors -> this block's region of the tail buffer [vb, vb + Q), staged per wave
     uint32_t lane_excl, wave_before, wave_cnt, total;
-    block_offsets_w((uint32_t)__popc(mask), s_wcnt, &lane_excl, &wave_before, &wave_cnt, &total);
+    block_offsets_w<TAIL_T>((uint32_t)__popc(mask), s_wcnt, &lane_excl, &wave_before, &wave_cnt, &total);
     TailStage &ws = s_stage[wid];
     uint32_t p = lane_excl;
 #pragma unroll
