@@ -3268,6 +3268,20 @@ __global__ void k_tail_map(const uint32_t *__restrict__ act, const unsigned long
   }
 }
 
+// The labels the live edges carry (the previous round's active list, or every vertex after a
+// level's identity round) -> the dense id of their fragment now: dmap[x] = dmap[lab[x]] (one hop:
+// lab of those labels is current; a root's own entry is k_tail_map's and is not rewritten here),
+// so k_tail_open relabels an end with ONE gather.
+__global__ void k_tail_labels(const uint32_t *__restrict__ prev, const unsigned long long *__restrict__ d_nprev,
+                              const uint32_t *__restrict__ lab, TailBufs tb) {
+  const uint64_t np = *d_nprev;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < np; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t x = prev ? prev[i] : (uint32_t)i;
+    const uint32_t l = lab[x];
+    if (l != x) tb.dmap[x] = tb.dmap[l];
+  }
+}
+
 // a wave's survivors staged in LDS for coalesced stores (12-byte records)
 struct TailStage {
   uint32_t p[WAVE * 4];
@@ -3285,8 +3299,7 @@ __device__ __forceinline__ void lds_min_u64(unsigned long long *s, uint32_t i, u
 }
 
 __global__ __launch_bounds__(TAIL_T) void k_tail_open(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
-                                                      const uint64_t *__restrict__ key, SegView in,
-                                                      const uint32_t *__restrict__ lab, TailBufs tb) {
+                                                      const uint64_t *__restrict__ key, SegView in, TailBufs tb) {
   __shared__ unsigned long long s_best[TAIL_MAX];
   __shared__ TailStage s_stage[TAIL_T / WAVE];
   __shared__ uint32_t s_wcnt[TAIL_T / WAVE];
@@ -3319,21 +3332,13 @@ __global__ __launch_bounds__(TAIL_T) void k_tail_open(const uint32_t *__restrict
                      k23 = *reinterpret_cast<const ulonglong2 *>(key + ph + 2);
     const uint32_t A[4] = {a4.x, a4.y, a4.z, a4.w}, B[4] = {b4.x, b4.y, b4.z, b4.w};
     const uint64_t K[4] = {k01.x, k01.y, k23.x, k23.y};
-    bool valid[4];
-    uint32_t la[4], lb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {  // the fragments now (one hop: lab of the carried labels is current)
-      valid[j] = in_range & (A[j] != LABEL_NONE);
-      la[j] = lab[valid[j] ? A[j] : 0u];
-      lb[j] = lab[valid[j] ? B[j] : 0u];
-    }
     uint32_t da[4], db[4], mask = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bool live = valid[j] & (la[j] != lb[j]);
-      da[j] = tb.dmap[live ? la[j] : 0u];
-      db[j] = tb.dmap[live ? lb[j] : 0u];
-      mask |= live ? (1u << j) : 0u;
+    for (int j = 0; j < 4; ++j) {  // the dense fragments now (k_tail_labels: one gather per end)
+      const bool valid = in_range & (A[j] != LABEL_NONE);
+      da[j] = tb.dmap[valid ? A[j] : 0u];
+      db[j] = tb.dmap[valid ? B[j] : 0u];
+      mask |= (valid & (da[j] != db[j])) ? (1u << j) : 0u;
     }
     uint32_t P[4];
 #pragma unroll
@@ -4887,7 +4892,14 @@ static int run_tail(ghs_solver *s) {
   {
     KT(GHS_K_TAIL_OPEN, s->arcs_known ? s->cur_arcs : 0);
     k_tail_map<<<grid_for(F0, 256, 64), 256, 0, st>>>(act0, d_nact, tb);
-    k_tail_open<<<TAIL_G, TAIL_T, 0, st>>>(I.src, I.dst, I.key, in, s->lab, tb);
+    // the labels the edges carry: the previous round's list (after the level's identity round 0:
+    // every vertex)
+    const bool prev_ident = lr0 == 1;
+    const uint32_t *prev = prev_ident ? nullptr : s->act[s->act_cur ^ 1];
+    const unsigned long long *d_nprev = prev_ident ? s->cnt + C_N : act_count(s, s->act_cur ^ 1);
+    const uint64_t nprev_bound = prev_ident ? s->n : s->level_nact;
+    k_tail_labels<<<grid_for(nprev_bound, 256, 8192), 256, 0, st>>>(prev, d_nprev, s->lab, tb);
+    k_tail_open<<<TAIL_G, TAIL_T, 0, st>>>(I.src, I.dst, I.key, in, tb);
   }
   {
     KT(GHS_K_TAIL_HOOK, F0);
