@@ -21,17 +21,18 @@ def main():
     opts = {"default": 0, "no_tail": _native.OPT_NO_TAIL, "no_bucketed": _native.OPT_NO_BUCKETED,
             "neither": _native.OPT_NO_TAIL | _native.OPT_NO_BUCKETED, "bucketed": _native.OPT_BUCKETED,
             "bucketed_no_tail": _native.OPT_BUCKETED | _native.OPT_NO_TAIL}
-    for levels in (None, 1, 2):
+    for levels in [int(x) if x != "None" else None for x in os.environ.get("LEVELS", "None,1,2").split(",")]:
         for name, opt in opts.items():
             kw = {} if levels is None else {"max_levels": levels}
             eng = DeviceMST(e, config=_native.make_config(options=opt, **kw))
             res, stats = eng.run()
             got = eng.in_mst_host()
             bad = int((got != ref_in).sum())
-            print(f"levels={levels} {name:18s} flags {res.pass_flags:2d} rounds {res.rounds:2d} "
-                  f"weight_ok {res.total_weight == ref_tw} edges {res.num_mst_edges}/{ref_k} mismatched {bad}",
-                  flush=True)
-            if bad and name == "default":
+            host_w = int(g.w[got].astype(np.uint64).sum())
+            print(f"levels={levels} {name:18s} flags {res.pass_flags:2d} rounds {res.rounds:2d} levels {res.levels} "
+                  f"weight_ok {res.total_weight == ref_tw} ({res.total_weight} vs {ref_tw}, flags sum {host_w}) "
+                  f"edges {res.num_mst_edges}/{ref_k} mismatched {bad}", flush=True)
+            if (bad or res.total_weight != ref_tw) and name in ("default", "neither"):
                 for i, st in enumerate(stats):
                     print("   ", i, st)
             del eng
