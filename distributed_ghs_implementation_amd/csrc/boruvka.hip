@@ -4932,6 +4932,9 @@ static int run_tail(ghs_solver *s) {
     s->rep_weight = hs->weight;
     s->rep_edges = hs->edges;
     s->report_final = true;
+    if (s->debug)
+      fprintf(stderr, "[ghs] level %u tail batch report: nact_out %llu edges %llu weight %llu\n", s->level, hs->nact_out,
+              hs->edges, hs->weight);
     if (hs->nact_out <= 1) break;
     if (r > TAIL_ROUNDS_MAX) return fail_counters(s, 4, "in the LDS tail (round cap)");
   }
@@ -4987,6 +4990,9 @@ static int run_level_pipelined(ghs_solver *s) {
     s->rep_weight = r.weight;
     s->rep_edges = r.edges;
     s->report_final = true;
+    if (s->debug)
+      fprintf(stderr, "[ghs] level %u round %u report: nact_in %llu nact_out %llu live_out %llu edges %llu weight %llu\n",
+              s->level, checked, r.nact_in, r.nact_out, r.live_out, r.edges, r.weight);
     if (r.err) return fail_counters(s, r.err, ("in round " + std::to_string(round0 + checked + 1)).c_str());
     if (checked == 0 && s->open_async) {  // the level's counts, from its first round
       const uint64_t S = r.live_out;  // round 0 does not compact: its live edges are the level's
