@@ -3006,14 +3006,21 @@ __global__ void k_unpack_best(const uint32_t *__restrict__ act, const unsigned l
 // host polls seq (written last, after a system-scope fence).
 constexpr int C_ERR_IDX = 4;  // == C_ERR (counter layout below)
 
-struct RoundSlot {
-  unsigned long long live_out, nact_out, edges, err;
+// ONE 64-byte line per slot: the host sees seq and the fields in the same line, so the drained
+// field stores are visible once seq is (a slot straddling two lines could show a new seq beside a
+// stale weight — round 4 measured exactly that with a 72-byte slot).
+struct alignas(64) RoundSlot {
+  unsigned long long live_out, nact_out, edges;
+  unsigned long long err;      // error bits (low word); bit 32: counter C_LONG, a level-0 edge spans > 1
+                               // bucket (the windowed round fell back) — not an error
   unsigned long long seq;
   unsigned long long nact_in;  // active fragments this round started from (a level's first round: the level's)
   unsigned long long pending;  // pending edges after the level's pass (counter C_PENDING)
   unsigned long long weight;   // MSF weight so far (counter C_WEIGHT)
-  unsigned long long span;     // counter C_LONG: a level-0 edge spans > 1 bucket (the windowed round fell back)
 };
+static_assert(sizeof(RoundSlot) == 64, "a round report is one 64-byte line");
+constexpr unsigned long long SLOT_SPAN = 1ull << 32;
+__host__ __device__ __forceinline__ unsigned long long slot_err(unsigned long long e) { return e & 0xffffffffull; }
 
 __device__ __forceinline__ void write_report(RoundSlot *slot, unsigned long long seq, const unsigned long long *cnt,
                                              unsigned long long nact_out, unsigned long long nact_in) {
@@ -3031,11 +3038,10 @@ __device__ __forceinline__ void write_report(RoundSlot *slot, unsigned long long
   slot->live_out = live;          // live edges after this round's compaction
   slot->nact_out = nact_out;      // active fragments of the next round
   slot->edges = edges;            // MSF edges so far
-  slot->err = err;                // error bits
+  slot->err = slot_err(err) | (span ? SLOT_SPAN : 0ull);  // error bits + the span flag
   slot->nact_in = nact_in;
   slot->pending = pending;
   slot->weight = weight;
-  slot->span = span;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(&slot->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -4928,7 +4934,7 @@ static int run_tail(ghs_solver *s) {
     GHS_HIP_CHECK(hipGetLastError());
     const RoundSlot *hs = s->h_slot + (seq % SLOT_RING);
     if (int rc = wait_slot(s, hs, seq)) return rc;
-    if (hs->err) return fail_counters(s, hs->err, "in the LDS tail");
+    if (slot_err(hs->err)) return fail_counters(s, slot_err(hs->err), "in the LDS tail");
     s->rep_weight = hs->weight;
     s->rep_edges = hs->edges;
     s->report_final = true;
@@ -4983,7 +4989,7 @@ static int run_level_pipelined(ghs_solver *s) {
     r.live_out = hs->live_out;
     r.nact_out = hs->nact_out;
     r.edges = hs->edges;
-    r.err = hs->err;
+    r.err = slot_err(hs->err);
     r.nact_in = hs->nact_in;
     r.pending = hs->pending;
     r.weight = hs->weight;
@@ -5006,7 +5012,7 @@ static int run_level_pipelined(ghs_solver *s) {
       nact_prev = r.nact_in;
       if (s->level == 0) s->select_out = S;
       else if (s->filter_run && !s->filter_out) s->filter_out = S + s->rem_total;
-      if (s->level == 0 && s->windowed_enq) s->windowed_ran = hs->span == 0;
+      if (s->level == 0 && s->windowed_enq) s->windowed_ran = (hs->err & SLOT_SPAN) == 0;
       if (s->debug) {
         uint32_t g[2] = {0, 0};
         (void)hipMemcpy(g, s->giant, 8, hipMemcpyDeviceToHost);
@@ -5530,7 +5536,7 @@ int ghs_solver_contract_async(ghs_solver *s, int *done) {
     s->pipe.erase(s->pipe.begin());
     const RoundSlot *hs = s->h_slot + (p.seq % SLOT_RING);
     if (int rc = wait_slot(s, hs, p.seq)) return rc;
-    const unsigned long long err = hs->err, nact_in = hs->nact_in, nact_out = hs->nact_out;
+    const unsigned long long err = slot_err(hs->err), nact_in = hs->nact_in, nact_out = hs->nact_out;
     const unsigned long long live_out = hs->live_out, edges = hs->edges;
     if (err) return fail_counters(s, err, ("in round " + std::to_string(p.round + 1)).c_str());
     push_stats(s, p.level_round, s->pipe_live, nact_in, edges);
@@ -5557,7 +5563,7 @@ int ghs_solver_contract_async(ghs_solver *s, int *done) {
         s->pipe.erase(s->pipe.begin());
         const RoundSlot *hs = s->h_slot + (p.seq % SLOT_RING);
         if (int rc = wait_slot(s, hs, p.seq)) return rc;
-        if (hs->err) return fail_counters(s, hs->err, ("in round " + std::to_string(p.round + 1)).c_str());
+        if (slot_err(hs->err)) return fail_counters(s, slot_err(hs->err), ("in round " + std::to_string(p.round + 1)).c_str());
         push_stats(s, p.level_round, s->pipe_live, hs->nact_in, hs->edges);
         s->pipe_live = hs->live_out;
       }
