@@ -937,7 +937,7 @@ def test_lds_tail_vs_oracle(graph, levels, opt, torch_cuda):
         assert np.array_equal(on.in_mst_host(), ref_in.astype(bool))
         assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
         assert sum(st["hooks"] for st in stats) == ref_k
-    if graph not in ("forest",):
+    if graph not in ("forest", "readme"):  # (their levels end in one or two rounds)
         assert res.pass_flags & _native.PASS_TAIL, (graph, list(stats))
     off = DeviceMST(e, config=_native.make_config(options=base | _native.OPT_NO_TAIL, **kw))
     res0, _ = off.run()
