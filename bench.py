@@ -115,15 +115,13 @@ def launch_bytes(rec, stats, res, n, windowed=frozenset()):
         return 24.0 * live + 16.0 * _next_live(stats, r)  # + lab[a], lab[b]; survivors out
     # bucketed rounds: a level's first round buckets its edges, later rounds their compacted
     # survivors; an edge is at least one record (a, b, key: 16 B)
-    if k in ("k_bcount", "k_bucket", "k_bmin") and r in windowed:
+    if k in ("k_bucket", "k_bmin") and r in windowed:
         return 0.0
     if k == "k_wmin" and r not in windowed:
         return 0.0  # exited at once: the fallback bucketed the round
     bucketed_edges = live if _first_round(stats, r) else _next_live(stats, r)
-    if k == "k_bcount":
-        return 8.0 * bucketed_edges  # a, b: the records per bucket
     if k == "k_bucket":
-        return 32.0 * bucketed_edges  # the edge in (16 B) + its record out (16 B)
+        return 40.0 * bucketed_edges  # pass A a, b (8 B) + pass B edge in (16 B) + record out (16 B)
     if k == "k_bmin":
         return 32.0 * bucketed_edges  # two sweeps over the records
     if k == "k_wmin":
@@ -157,7 +155,7 @@ def launch_bytes(rec, stats, res, n, windowed=frozenset()):
 
 TAIL_G = 256  # boruvka.hip TAIL_G: the LDS tail's blocks (rows of block minima)
 # every kernel of a min-edge round's stage 1 (the tail's kernels and the bucketed ones also hook)
-STAGE1 = ("k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>", "k_bcount", "k_bucket", "k_bmin", "k_wstarts", "k_wmin",
+STAGE1 = ("k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>", "k_bucket", "k_bmin", "k_wstarts", "k_wmin",
           "k_tail_open", "k_tail_round", "k_tail_hook")
 
 

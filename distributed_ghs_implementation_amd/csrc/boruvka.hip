@@ -2132,14 +2132,14 @@ GHS_STREAM_KERNEL_6 void k_level_pass(const uint32_t *__restrict__ ru, const uin
 // single writer per target, no global atomics and no separate CONNECT pass (the reference's
 // TEST/ACCEPT/REPORT convergecast and CHANGEROOT/CONNECT, ghs_implementation.py:155-353, as two
 // passes over a bucket). Mutual pairs stay 2-cycles for the jump (k_jump / k_jump_ident).
-//  k_bcount  block g counts its share's records per bucket (an edge is a record of bucket(a), and
-//            of bucket(b) when that differs): C[t][g]
-//  k_bscan   C's rows scanned in place, the bucket totals into the global starts S[t]
-//  k_bucket  block g writes its records (a, b, key) at LDS cursors S[t] + C[t][g]: bucket t's
-//            records are the one range [S[t], S[t+1]) of the global record array. On a lattice a
-//            block's edges touch a handful of buckets, so the records leave in long runs.
-//  k_bmin    one workgroup per bucket: one coalesced sweep of its range, min per target in LDS,
-//            winners.
+//  k_bucket  block g streams its share of the live edges twice: pass A counts records per bucket
+//            (an edge is a record of bucket(a), and of bucket(b) when that differs), one LDS
+//            scan turns the counts into offsets in the block's record region, written bucket-major
+//            (O[t][g]: a bucket's offsets are contiguous), pass B writes the records (a, b, key)
+//            at LDS cursors. On a lattice a block's edges touch a handful of buckets, so the
+//            records leave in long runs.
+//  k_bmin    one workgroup per bucket: its runs from every region (offsets and their scan in
+//            LDS), min per target in LDS, winners.
 // ------------------------------------------------------------------------------------------
 constexpr uint32_t BK_G = 512;        // k_bucket blocks = record regions
 constexpr uint32_t BK_T = 512;        // k_bucket threads
@@ -2231,39 +2231,55 @@ __device__ __forceinline__ uint32_t lds_bump(uint32_t *s_h, uint32_t bkt, bool a
   return slot;
 }
 
-// The records of a bucketed round in ONE global bucket-major layout (round 4): bucket t's records
-// are the contiguous range [S[t], S[t+1]) of `rec`, so k_bmin sweeps one coalesced range instead
-// of locating a run in each of the 512 block regions per record (a binary search over the bucket's
-// non-empty runs: R-MAT s24 buckets hold ~9.5K records from ~512 runs of ~18). Three steps:
-//   k_bcount     pass A of every block: records per bucket, C[t][g] (bucket-major table)
-//   k_bscan      each bucket's row of block counts scanned in place (a wave per bucket) and its
-//                total; then (last block) the bucket totals -> S[t] — the global starts
-//   k_bucket     pass B: the records at the LDS cursors S[t] + C[t][g] of the block's buckets
-// The block's share of the edges, the hot-fragment exclusion and the record format are those of
-// the region layout before (pass A and pass B read the same edges; the counts agree).
-template <bool PASS_B>
-__device__ __forceinline__ void bucket_pass(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
-                                            const uint64_t *__restrict__ key, SegView in, uint32_t bs,
-                                            uint32_t *s_h, uint32_t slo, uint32_t shi, uint64_t vb, uint64_t ve,
-                                            uint32_t nhot, const uint32_t *s_hl, const uint32_t *s_hi, uint32_t hot0,
-                                            unsigned long long *s_hmin, uint4 *__restrict__ rec) {
+__global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
+                                                 const uint64_t *__restrict__ key, SegView in, uint32_t bs,
+                                                 uint32_t nb, uint4 *__restrict__ rec, uint32_t *__restrict__ O,
+                                                 const unsigned long long *__restrict__ guard_nact,
+                                                 const uint32_t *__restrict__ hot, uint64_t *__restrict__ best,
+                                                 const unsigned long long *__restrict__ only_if) {
+  __shared__ uint32_t s_h[BK_MAX_B + 1];
+  __shared__ uint32_t s_seg[2];
+  __shared__ uint32_t s_wsum[BK_T / WAVE];
+  __shared__ uint32_t s_hl[HOT_HASH];          // hot label -> its index (linear probing)
+  __shared__ uint32_t s_hi[HOT_HASH];
+  __shared__ unsigned long long s_hmin[HOT_K];  // this block's minimum per hot fragment
+  // a lookahead round past the level's end (<= 1 active fragment) writes empty regions
+  const bool noop = guard_nact && *guard_nact <= 1;
+  // a level's first round past level 0: the hot fragments' candidates (the giant's: most of the
+  // level's edges) are reduced in LDS and leave the block as one atomicMin on best[] each, instead
+  // of filling one bucket each that a single k_bmin workgroup would have to sweep. A record's hot
+  // end is marked (bit 31: bucketed solves have n <= 2^28), so k_bmin never takes it as a target.
+  if (only_if && !*only_if) return;  // the windowed round ran (k_wmin)
+  const uint32_t nhot = hot ? hot[0] : 0u;
+  const uint32_t hot0 = nhot ? hot[1] : LABEL_NONE;  // one hot fragment (R-MAT: the giant): a compare
+  for (uint32_t i = threadIdx.x; i < HOT_HASH; i += BK_T) s_hl[i] = LABEL_NONE;
+  if (threadIdx.x < HOT_K) s_hmin[threadIdx.x] = KEY_NONE;
+  __syncthreads();
+  if (threadIdx.x < nhot) hot_insert(s_hl, s_hi, hot[1 + threadIdx.x], threadIdx.x);
   auto hidx = [&](uint32_t x) -> int { return nhot == 1 ? (x == hot0 ? 0 : -1) : hot_find(s_hl, s_hi, x); };
-  // every lane of a wave iterates while the wave's first tile is in range (the bumps are
-  // wave-collective); BK_TILES 4-edge tiles per lane per iteration, all loads issued first
+  const uint64_t T = noop ? 0 : in.prefix[in.nseg];
+  const uint64_t Q = bk_quota(T);
+  const uint64_t vb = Q * blockIdx.x;
+  const uint64_t ve = (vb + Q < T) ? vb + Q : T;
+  for (uint32_t i = threadIdx.x; i <= nb; i += BK_T) s_h[i] = 0;
+  if (threadIdx.x == 0) {
+    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
+    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
+  }
+  __syncthreads();
+  const uint32_t slo = s_seg[0], shi = s_seg[1];
+  // pass A: records per bucket (the a and b ends only); every lane of a wave iterates while the
+  // wave's first tile is in range (the bumps are wave-collective); BK_TILES 4-edge tiles per lane
+  // per iteration, all loads issued before the first bump
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   constexpr uint64_t STRIDE = (uint64_t)BK_T * 4;
   for (uint64_t v0 = vb + (uint64_t)threadIdx.x * 4; v0 - lane * 4 < ve; v0 += STRIDE * BK_TILES) {
     uint4 a4[BK_TILES], b4[BK_TILES];
-    ulonglong2 k01[BK_TILES], k23[BK_TILES];
 #pragma unroll
     for (int q = 0; q < BK_TILES; ++q) {
       const uint64_t i0 = tile_phys(in, slo, shi, v0 + STRIDE * q, ve);
       a4[q] = *reinterpret_cast<const uint4 *>(src + i0);
       b4[q] = *reinterpret_cast<const uint4 *>(dst + i0);
-      if (PASS_B) {
-        k01[q] = *reinterpret_cast<const ulonglong2 *>(key + i0);
-        k23[q] = *reinterpret_cast<const ulonglong2 *>(key + i0 + 2);
-      }
     }
 #pragma unroll
     for (int q = 0; q < BK_TILES; ++q) {
@@ -2273,154 +2289,69 @@ __device__ __forceinline__ void bucket_pass(const uint32_t *__restrict__ src, co
       for (int j = 0; j < 4; ++j) {
         const bool live = (v < ve) & (A[j] != LABEL_NONE);  // past the range / region padding
         const uint32_t ba = A[j] >> bs, bb = B[j] >> bs;
+        const bool ea = live && (!nhot || hidx(A[j]) < 0);
+        const bool eb = live && (!nhot || hidx(B[j]) < 0) && (bb != ba || !ea);
+        lds_bump<false>(s_h, ba, ea);
+        lds_bump<false>(s_h, bb, eb);
+      }
+    }
+  }
+  __syncthreads();
+  // counts -> offsets in place (each thread a run of consecutive buckets), s_h[nb] = total
+  const uint32_t per = (nb + BK_T - 1) / BK_T, c0 = threadIdx.x * per;
+  uint32_t sum = 0;
+  for (uint32_t i = 0; i < per && c0 + i < nb; ++i) sum += s_h[c0 + i];
+  uint32_t tot;
+  uint32_t run = block_excl_scan<BK_T>(sum, s_wsum, &tot);
+  for (uint32_t i = 0; i < per && c0 + i < nb; ++i) {
+    const uint32_t c = s_h[c0 + i];
+    s_h[c0 + i] = run;
+    run += c;
+  }
+  if (threadIdx.x == 0) s_h[nb] = tot;
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t <= nb; t += BK_T) O[(uint64_t)t * BK_G + blockIdx.x] = s_h[t];
+  __syncthreads();  // the cursors below advance s_h
+  // pass B: the records at the cursors of their buckets
+  const uint64_t base = 2 * vb;
+  for (uint64_t v0 = vb + (uint64_t)threadIdx.x * 4; v0 - lane * 4 < ve; v0 += STRIDE * BK_TILES) {
+    uint4 a4[BK_TILES], b4[BK_TILES];
+    ulonglong2 k01[BK_TILES], k23[BK_TILES];
+#pragma unroll
+    for (int q = 0; q < BK_TILES; ++q) {
+      const uint64_t i0 = tile_phys(in, slo, shi, v0 + STRIDE * q, ve);
+      a4[q] = *reinterpret_cast<const uint4 *>(src + i0);
+      b4[q] = *reinterpret_cast<const uint4 *>(dst + i0);
+      k01[q] = *reinterpret_cast<const ulonglong2 *>(key + i0);
+      k23[q] = *reinterpret_cast<const ulonglong2 *>(key + i0 + 2);
+    }
+#pragma unroll
+    for (int q = 0; q < BK_TILES; ++q) {
+      const uint64_t v = v0 + STRIDE * q;
+      const uint32_t A[4] = {a4[q].x, a4[q].y, a4[q].z, a4[q].w}, B[4] = {b4[q].x, b4[q].y, b4[q].z, b4[q].w};
+      const uint64_t K[4] = {k01[q].x, k01[q].y, k23[q].x, k23[q].y};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool live = (v < ve) & (A[j] != LABEL_NONE);
+        const uint32_t ba = A[j] >> bs, bb = B[j] >> bs;
         const int ha = (live && nhot) ? hidx(A[j]) : -1;
         const int hb = (live && nhot) ? hidx(B[j]) : -1;
         const bool ea = live && ha < 0;
         const bool eb = live && hb < 0 && (bb != ba || !ea);
-        if (!PASS_B) {
-          lds_bump<false>(s_h, ba, ea);
-          lds_bump<false>(s_h, bb, eb);
-        } else {
-          const uint64_t K = (j == 0) ? k01[q].x : (j == 1) ? k01[q].y : (j == 2) ? k23[q].x : k23[q].y;
-          const uint32_t pa = lds_bump<true>(s_h, ba, ea);
-          const uint32_t pb = lds_bump<true>(s_h, bb, eb);
-          const uint4 r = make_uint4(A[j] | (ha >= 0 ? HOT_MARK : 0u), B[j] | (hb >= 0 ? HOT_MARK : 0u), (uint32_t)K,
-                                     (uint32_t)(K >> 32));
-          if (ea) rec[pa] = r;
-          if (eb) rec[pb] = r;
-          if (ha >= 0 && K < s_hmin[ha]) atomicMin(&s_hmin[ha], (unsigned long long)K);
-          if (hb >= 0 && K < s_hmin[hb]) atomicMin(&s_hmin[hb], (unsigned long long)K);
-        }
+        const uint32_t pa = lds_bump<true>(s_h, ba, ea);
+        const uint32_t pb = lds_bump<true>(s_h, bb, eb);
+        const uint4 r = make_uint4(A[j] | (ha >= 0 ? HOT_MARK : 0u), B[j] | (hb >= 0 ? HOT_MARK : 0u), (uint32_t)K[j],
+                                   (uint32_t)(K[j] >> 32));
+        if (ea) rec[base + pa] = r;
+        if (eb) rec[base + pb] = r;
+        if (ha >= 0 && K[j] < s_hmin[ha]) atomicMin(&s_hmin[ha], (unsigned long long)K[j]);
+        if (hb >= 0 && K[j] < s_hmin[hb]) atomicMin(&s_hmin[hb], (unsigned long long)K[j]);
       }
     }
   }
-}
-
-// the shared prologue of k_bcount / k_bucket: the block's share, its regions, the hot hash
-struct BucketShare {
-  uint64_t vb, ve;
-  uint32_t slo, shi, nhot, hot0;
-};
-__device__ __forceinline__ bool bucket_share(SegView in, const unsigned long long *__restrict__ guard_nact,
-                                             const uint32_t *__restrict__ hot,
-                                             const unsigned long long *__restrict__ only_if, uint32_t *s_seg,
-                                             uint32_t *s_hl, uint32_t *s_hi, BucketShare *b) {
-  if (only_if && !*only_if) return false;  // the windowed round ran (k_wmin)
-  // a lookahead round past the level's end (<= 1 active fragment) has no records
-  const bool noop = guard_nact && *guard_nact <= 1;
-  b->nhot = hot ? hot[0] : 0u;
-  b->hot0 = b->nhot ? hot[1] : LABEL_NONE;  // one hot fragment (R-MAT: the giant): a compare
-  for (uint32_t i = threadIdx.x; i < HOT_HASH; i += BK_T) s_hl[i] = LABEL_NONE;
-  __syncthreads();
-  if (threadIdx.x < b->nhot) hot_insert(s_hl, s_hi, hot[1 + threadIdx.x], threadIdx.x);
-  const uint64_t T = noop ? 0 : in.prefix[in.nseg];
-  const uint64_t Q = bk_quota(T);
-  b->vb = Q * blockIdx.x;
-  b->ve = (b->vb + Q < T) ? b->vb + Q : T;
-  if (threadIdx.x == 0) {
-    s_seg[0] = b->vb < T ? seg_find(in.prefix, 0, in.nseg - 1, b->vb) : 0;
-    s_seg[1] = b->ve > b->vb ? seg_find(in.prefix, 0, in.nseg - 1, b->ve - 1) : 0;
-  }
-  __syncthreads();
-  b->slo = s_seg[0];
-  b->shi = s_seg[1];
-  return true;
-}
-
-__global__ __launch_bounds__(BK_T) void k_bcount(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
-                                                 SegView in, uint32_t bs, uint32_t nb, uint32_t *__restrict__ C,
-                                                 const unsigned long long *__restrict__ guard_nact,
-                                                 const uint32_t *__restrict__ hot,
-                                                 const unsigned long long *__restrict__ only_if) {
-  __shared__ uint32_t s_h[BK_MAX_B + 1];
-  __shared__ uint32_t s_seg[2];
-  __shared__ uint32_t s_hl[HOT_HASH], s_hi[HOT_HASH];
-  for (uint32_t i = threadIdx.x; i <= nb; i += BK_T) s_h[i] = 0;
-  BucketShare b;
-  if (!bucket_share(in, guard_nact, hot, only_if, s_seg, s_hl, s_hi, &b)) return;
-  bucket_pass<false>(src, dst, nullptr, in, bs, s_h, b.slo, b.shi, b.vb, b.ve, b.nhot, s_hl, s_hi, b.hot0, nullptr,
-                     nullptr);
-  __syncthreads();
-  for (uint32_t t = threadIdx.x; t < nb; t += BK_T) C[(uint64_t)t * BK_G + blockIdx.x] = s_h[t];
-}
-
-// Each bucket's row of block counts -> exclusive prefix in place (a wave per bucket, 8 per lane);
-// the row totals -> S[t]; the last block to finish scans S into the global starts (S[nb] = total).
-constexpr uint32_t BS_T = 256;
-__global__ __launch_bounds__(BS_T) void k_bscan(uint32_t nb, uint32_t *__restrict__ C, uint32_t *__restrict__ S,
-                                                unsigned int *__restrict__ ticket,
-                                                const unsigned long long *__restrict__ only_if) {
-  __shared__ uint32_t s_w[1024 / WAVE];
-  __shared__ int s_last;
-  if (only_if && !*only_if) return;
-  const uint32_t lane = threadIdx.x & (WAVE - 1);
-  const uint32_t t = blockIdx.x * (BS_T / WAVE) + threadIdx.x / WAVE;
-  static_assert(BK_G == 8 * WAVE, "8 block counts per lane");
-  if (t < nb) {
-    uint32_t *row = C + (uint64_t)t * BK_G + lane * 8;
-    const uint4 x0 = *reinterpret_cast<const uint4 *>(row), x1 = *reinterpret_cast<const uint4 *>(row + 4);
-    uint32_t v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-    uint32_t sum = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sum += v[j];
-    uint32_t tot;
-    uint32_t run = wave_excl_scan(sum, &tot);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t c = v[j];
-      v[j] = run;
-      run += c;
-    }
-    *reinterpret_cast<uint4 *>(row) = make_uint4(v[0], v[1], v[2], v[3]);
-    *reinterpret_cast<uint4 *>(row + 4) = make_uint4(v[4], v[5], v[6], v[7]);
-    if (lane == 0) S[t] = tot;
-  }
-  // the last block scans the bucket totals (S[0..nb) -> exclusive starts, S[nb] = total)
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();
-  if (threadIdx.x == 0) *ticket = 0;  // re-armed for the next round's launch
-  // 256 threads x ceil(nb / 256) consecutive totals each (nb <= 16384: <= 64)
-  const uint32_t per = (nb + BS_T - 1) / BS_T, c0 = threadIdx.x * per;
-  uint32_t sum = 0;
-  for (uint32_t i = 0; i < per && c0 + i < nb; ++i) sum += __hip_atomic_load(S + c0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  uint32_t tot;
-  uint32_t run = block_excl_scan<BS_T>(sum, s_w, &tot);
-  for (uint32_t i = 0; i < per && c0 + i < nb; ++i) {
-    const uint32_t c = __hip_atomic_load(S + c0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    S[c0 + i] = run;
-    run += c;
-  }
-  if (threadIdx.x == 0) S[nb] = tot;
-}
-
-__global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
-                                                 const uint64_t *__restrict__ key, SegView in, uint32_t bs,
-                                                 uint32_t nb, uint4 *__restrict__ rec, const uint32_t *__restrict__ C,
-                                                 const uint32_t *__restrict__ S,
-                                                 const unsigned long long *__restrict__ guard_nact,
-                                                 const uint32_t *__restrict__ hot, uint64_t *__restrict__ best,
-                                                 const unsigned long long *__restrict__ only_if) {
-  __shared__ uint32_t s_h[BK_MAX_B + 1];
-  __shared__ uint32_t s_seg[2];
-  __shared__ uint32_t s_hl[HOT_HASH], s_hi[HOT_HASH];  // hot label -> its index (linear probing)
-  __shared__ unsigned long long s_hmin[HOT_K];          // this block's minimum per hot fragment
-  // a level's first round past level 0: the hot fragments' candidates (the giant's: most of the
-  // level's edges) are reduced in LDS and leave the block as one atomicMin on best[] each, instead
-  // of filling one bucket each that a single k_bmin workgroup would have to sweep. A record's hot
-  // end is marked (bit 31: bucketed solves have n <= 2^28), so k_bmin never takes it as a target.
-  if (threadIdx.x < HOT_K) s_hmin[threadIdx.x] = KEY_NONE;
-  // the block's cursors: its first record of every bucket in the global bucket-major layout
-  for (uint32_t t = threadIdx.x; t < nb; t += BK_T) s_h[t] = S[t] + C[(uint64_t)t * BK_G + blockIdx.x];
-  BucketShare b;
-  if (!bucket_share(in, guard_nact, hot, only_if, s_seg, s_hl, s_hi, &b)) return;
-  bucket_pass<true>(src, dst, key, in, bs, s_h, b.slo, b.shi, b.vb, b.ve, b.nhot, s_hl, s_hi, b.hot0, s_hmin, rec);
-  if (b.nhot) {
+  if (nhot) {
     __syncthreads();
-    if (threadIdx.x < b.nhot && s_hmin[threadIdx.x] != KEY_NONE) flush_min(best, hot[1 + threadIdx.x], s_hmin[threadIdx.x]);
+    if (threadIdx.x < nhot && s_hmin[threadIdx.x] != KEY_NONE) flush_min(best, hot[1 + threadIdx.x], s_hmin[threadIdx.x]);
   }
 }
 
@@ -2542,36 +2473,61 @@ __device__ __forceinline__ void bucket_ident(uint32_t t, uint32_t *__restrict__ 
 }
 
 template <uint32_t BS, bool FULL = false>
-__global__ __launch_bounds__(BM_T) void k_bmin(const uint4 *__restrict__ rec, const uint32_t *__restrict__ S,
-                                               uint32_t *__restrict__ par, uint64_t *__restrict__ best,
+__global__ __launch_bounds__(BM_T) void k_bmin(const uint4 *__restrict__ rec, const uint32_t *__restrict__ O,
+                                               SegView in, uint32_t *__restrict__ par, uint64_t *__restrict__ best,
                                                uint8_t *__restrict__ in_mst,
                                                const unsigned long long *__restrict__ guard_nact,
                                                const unsigned long long *__restrict__ only_if, uint32_t n = 0) {
   constexpr uint32_t SPAN = 1u << BS;
   __shared__ unsigned long long s_min[SPAN];
+  __shared__ uint64_t s_pos[BK_G];  // non-empty run i: its first record's position
+  __shared__ uint32_t s_pre[BK_G];  // ... and its first index in the bucket's record order
+  __shared__ uint32_t s_wsum[BM_T / WAVE];
   if (only_if && !*only_if) return;  // the windowed round ran (k_wmin)
   const bool noop = guard_nact && *guard_nact <= 1;
+  const uint64_t T = noop ? 0 : in.prefix[in.nseg];
+  const uint64_t R2 = 2 * bk_quota(T);  // record region stride
   const uint32_t t = blockIdx.x;
-  const uint32_t r0 = noop ? 0u : S[t], R = noop ? 0u : S[t + 1] - r0;  // the bucket's records: one range
+  uint32_t cnt = 0, st = 0;
+  if (threadIdx.x < BK_G && !noop) {
+    st = O[(uint64_t)t * BK_G + threadIdx.x];
+    cnt = O[(uint64_t)(t + 1) * BK_G + threadIdx.x] - st;
+  }
+  // records before each run (scan of the counts), then the non-empty runs' slots (scan of their flags)
+  uint32_t R, NZ;
+  const uint32_t before = block_excl_scan<BM_T>(cnt, s_wsum, &R);
   if (R == 0) {  // block-uniform: no record of this bucket
     if (FULL) bucket_ident<BS>(t, par, best, n);
     return;
   }
+  const uint32_t zi = block_excl_scan<BM_T>(cnt ? 1u : 0u, s_wsum, &NZ);
+  if (cnt) {
+    s_pos[zi] = R2 * threadIdx.x + st;
+    s_pre[zi] = before;
+  }
   for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) s_min[i] = KEY_NONE;
   __syncthreads();
-  const uint4 *base = rec + r0;
+  auto locate = [&](uint32_t r) -> uint64_t {  // the non-empty run with s_pre <= r, the last one
+    uint32_t lo = 0, hi = NZ - 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (s_pre[mid] <= r) lo = mid; else hi = mid - 1;
+    }
+    return s_pos[lo] + (r - s_pre[lo]);
+  };
   constexpr uint32_t STEP = BM_T * BM_ILP;
   auto sweep = [&](auto f) {
-    for (uint32_t q0 = threadIdx.x; q0 < R; q0 += STEP) {
+    for (uint32_t r0 = threadIdx.x; r0 < R; r0 += STEP) {
       uint32_t a[BM_ILP], b[BM_ILP];
       unsigned long long k[BM_ILP];
 #pragma unroll
       for (int j = 0; j < BM_ILP; ++j) {
-        const uint32_t q = q0 + j * BM_T;
-        const uint4 x = base[q < R ? q : 0];
-        a[j] = q < R ? x.x : LABEL_NONE;
-        b[j] = q < R ? x.y : LABEL_NONE;
-        k[j] = q < R ? ((unsigned long long)x.w << 32 | x.z) : KEY_NONE;
+        const uint32_t r = r0 + j * BM_T;
+        const uint64_t p = r < R ? locate(r) : 0;
+        const uint4 x = rec[p];
+        a[j] = r < R ? x.x : LABEL_NONE;
+        b[j] = r < R ? x.y : LABEL_NONE;
+        k[j] = r < R ? ((unsigned long long)x.w << 32 | x.z) : KEY_NONE;
       }
 #pragma unroll
       for (int j = 0; j < BM_ILP; ++j) f(a[j], b[j], k[j]);
@@ -3832,8 +3788,7 @@ struct ghs_solver {
   bool windowed_enq = false;    // ... was enqueued this solve (it ran unless k_select's span flag was set)
   bool windowed_ran = false;    // ... and ran (the span flag of its round report was clear)
   bool state_init_pending = false;  // one rank: best / par initialised by level 0's first round
-  uint32_t *bk_off = nullptr;   // bucket-major block counts -> in-bucket prefixes (k_bcount, k_bscan)
-  uint32_t *bk_start = nullptr; // the buckets' global starts (nb + 1) and k_bscan's ticket after them
+  uint32_t *bk_off = nullptr;
   uint32_t bk_bs = 13, bk_nb = 0;
   bool bucketed = false;        // this solve runs bucketed rounds (decided once the plan landed)
   bool bucket_decided = false;
@@ -3893,7 +3848,7 @@ static const char *const KERNEL_NAMES[GHS_K_COUNT] = {
     "k_select", "k_filter", "k_level_pass", "k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>",
     "k_win", "k_hook", "k_jump_ident", "k_jump", "k_select_lb", "k_resolve", "k_giant", "k_scan_counts",
     "k_plan", "k_init", "k_pack_best", "k_unpack_best", "k_round_report", "k_pack_hook", "k_unpack_hook", "k_dense", "k_flag_bits", "k_bucket", "k_bmin", "k_wstarts", "k_wmin", "k_hot_hook",
-    "k_tail_open", "k_tail_round", "k_tail_hook", "k_bcount"};
+    "k_tail_open", "k_tail_round", "k_tail_hook"};
 
 struct KtScope {
   ghs_solver *s;
@@ -4082,7 +4037,6 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
     const uint64_t rc = 2 * cap + 8 * BK_G;
     p = carve(rc * 16); if (s) s->rec = (uint4 *)p;
     p = carve((size_t)(nb + 1) * BK_G * 4); if (s) s->bk_off = (uint32_t *)p;
-    p = carve((size_t)(nb + 1) * 4 + 256); if (s) s->bk_start = (uint32_t *)p;  // + k_bscan's ticket
     p = carve((size_t)(nb + 1) * 8 + SEG_MAX * 4); if (s) s->wstart = (uint64_t *)p;  // + region-first table
     if (s) {
       s->bk_bs = bs;
@@ -4553,31 +4507,24 @@ constexpr bool BK_RANDOM_L0 = GHS_BK_RANDOM_L0;
 static void enqueue_bmin(ghs_solver *s, const uint32_t *a, const uint32_t *b, const uint64_t *k, SegView in,
                          const unsigned long long *guard, uint64_t items, const uint32_t *hot,
                          const unsigned long long *only_if = nullptr, bool full = false) {
-  unsigned int *ticket = reinterpret_cast<unsigned int *>(s->bk_start + s->bk_nb + 1);
-  {
-    KT(GHS_K_BCOUNT, items);
-    k_bcount<<<BK_G, BK_T, 0, s->stream>>>(a, b, in, s->bk_bs, s->bk_nb, s->bk_off, guard, hot, only_if);
-    k_bscan<<<(s->bk_nb + BS_T / WAVE - 1) / (BS_T / WAVE), BS_T, 0, s->stream>>>(s->bk_nb, s->bk_off, s->bk_start,
-                                                                                 ticket, only_if);
-  }
   {
     KT(GHS_K_BUCKET, items);
-    k_bucket<<<BK_G, BK_T, 0, s->stream>>>(a, b, k, in, s->bk_bs, s->bk_nb, s->rec, s->bk_off, s->bk_start, guard, hot,
-                                         s->best, only_if);
+    k_bucket<<<BK_G, BK_T, 0, s->stream>>>(a, b, k, in, s->bk_bs, s->bk_nb, s->rec, s->bk_off, guard, hot, s->best,
+                                         only_if);
   }
   {
     KT(GHS_K_BMIN, items);
     if (full) {  // level 0's windowed round falling back: every vertex's best / par written
       if (s->bk_bs == 13)
-        k_bmin<13, true><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_start, s->par, s->best, s->in_mst, guard,
+        k_bmin<13, true><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard,
                                                            only_if, s->n);
       else
-        k_bmin<14, true><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_start, s->par, s->best, s->in_mst, guard,
+        k_bmin<14, true><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard,
                                                            only_if, s->n);
     } else if (s->bk_bs == 13) {
-      k_bmin<13><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_start, s->par, s->best, s->in_mst, guard, only_if);
+      k_bmin<13><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard, only_if);
     } else {
-      k_bmin<14><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_start, s->par, s->best, s->in_mst, guard, only_if);
+      k_bmin<14><<<s->bk_nb, BM_T, 0, s->stream>>>(s->rec, s->bk_off, in, s->par, s->best, s->in_mst, guard, only_if);
     }
   }
   if (hot) {
@@ -4873,7 +4820,16 @@ static int decide_bucketed(ghs_solver *s) {
 // once the level is done) behind k_tail_map + k_tail_open, each batch ending with a copy of the
 // control block and its report; reads the tail's per-round stats from that copy and closes the
 // level. Rounds whose launches follow the finishing round exit at once.
-constexpr uint32_t TAIL_BATCH = 6;  // tail rounds per batch (R-MAT levels finish in 3-5, lattices in 5-7)
+// Tail rounds per batch: the first batch is sized from the level's last observed contraction
+// (F0 fragments shrinking by `decay` per round finish in about log_decay(F0) rounds, plus the
+// finishing one), so few launches run after the level is done; later batches are short.
+constexpr uint32_t TAIL_BATCH_MIN = 2, TAIL_BATCH_MAX = 8, TAIL_BATCH_NEXT = 3;
+
+static uint32_t tail_first_batch(uint64_t F0, uint64_t prev_in) {
+  const double decay = std::max(2.0, prev_in > F0 ? (double)prev_in / (double)F0 : 2.0);
+  const double est = std::ceil(std::log((double)F0) / std::log(decay)) + 1.0;
+  return (uint32_t)std::min<double>(TAIL_BATCH_MAX, std::max<double>(TAIL_BATCH_MIN, est));
+}
 constexpr uint64_t TAIL_TRY = 32ull * TAIL_MAX;  // a bound below this: read the exact count first
 
 static bool tail_usable(const ghs_solver *s) {
@@ -4881,7 +4837,7 @@ static bool tail_usable(const ghs_solver *s) {
          !s->act_ident;
 }
 
-static int run_tail(ghs_solver *s) {
+static int run_tail(ghs_solver *s, uint64_t prev_in) {
   hipStream_t st = s->stream;
   TailBufs tb = s->tail;
   const ArcBuf &I = s->buf[s->cur], &O = s->buf[s->cur ^ 1];
@@ -4913,8 +4869,10 @@ static int run_tail(ghs_solver *s) {
   }
   GHS_HIP_CHECK(hipGetLastError());
   uint32_t r = 1;  // the next tail round to stream
+  uint32_t batch = tail_first_batch(F0, prev_in);
   for (;;) {
-    const uint32_t last = std::min(r + TAIL_BATCH - 1, TAIL_ROUNDS_MAX);  // the batch's last round
+    const uint32_t last = std::min(r + batch - 1, TAIL_ROUNDS_MAX);  // the batch's last round
+    batch = TAIL_BATCH_NEXT;
     for (; r <= last; ++r) {
       s->round = round0 + r;  // the profile's round index of these launches
       {
@@ -4961,6 +4919,7 @@ static int run_level_pipelined(ghs_solver *s) {
   const uint32_t round0 = s->round;
   uint64_t live_prev = s->cur_arcs, nact_prev = s->level_nact;  // inputs of the next checked round
   uint32_t issued = 0, checked = 0;
+  uint64_t last_in = s->level_nact;  // the active input of the last checked round
   std::vector<unsigned long long> seqs(LEVEL_ROUND_CAP + s->lookahead + 1);
   for (;;) {
     if (issued < checked + 1 + s->lookahead) {
@@ -4970,7 +4929,7 @@ static int run_level_pipelined(ghs_solver *s) {
         if (checked < issued) goto check;
         if (s->nact >= 2 && s->nact <= TAIL_MAX) {
           s->round = round0 + issued;
-          return run_tail(s);
+          return run_tail(s, last_in);
         }
       }
       if (issued >= LEVEL_ROUND_CAP) GHS_FAIL(GHS_E_ROUNDCAP, "round cap exceeded in a level");
@@ -5023,6 +4982,7 @@ static int run_level_pipelined(ghs_solver *s) {
       if (r.nact_in == 0) break;  // no edge in this level: its rounds were no-ops (checked stays 0)
     }
     push_stats(s, checked, live_prev, nact_prev, r.edges);
+    last_in = nact_prev;
     // the live edges of round k + 1: round 0 does not compact (its input is read again)
     live_prev = checked == 0 ? live_prev : r.live_out;
     nact_prev = r.nact_out;
@@ -5122,8 +5082,6 @@ static int solver_begin(ghs_solver *s) {
   // only the solver's own edge range: it never writes a flag outside [e_lo, e_hi)
   if (s->e_hi > s->e_lo && (e = hipMemsetAsync(s->in_mst + s->e_lo, 0, s->e_hi - s->e_lo, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset in_mst: ") + hipGetErrorString(e));
   if ((e = hipMemsetAsync(s->lb_state, 0, LB_MAX_TILES * 8, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset select state: ") + hipGetErrorString(e));
-  if (s->bk_start && (e = hipMemsetAsync(s->bk_start + s->bk_nb + 1, 0, 4, s->stream)) != hipSuccess)  // k_bscan's ticket
-    GHS_FAIL(GHS_E_HIP, std::string("memset bucket ticket: ") + hipGetErrorString(e));
   k_init_counters<<<1, 64, 0, s->stream>>>(s->cnt, n, s->hook_acc);
   if ((e = hipGetLastError()) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("init kernels: ") + hipGetErrorString(e));
   s->level = 0;

@@ -319,7 +319,7 @@ enum ghs_kernel_id {
   GHS_K_WIN, GHS_K_HOOK, GHS_K_JUMP_IDENT, GHS_K_JUMP, GHS_K_SELECT_LB, GHS_K_RESOLVE, GHS_K_GIANT, GHS_K_SCAN,
   GHS_K_PLAN, GHS_K_INIT, GHS_K_PACK, GHS_K_UNPACK, GHS_K_ROUND_REPORT, GHS_K_PACK_HOOK, GHS_K_UNPACK_HOOK,
   GHS_K_DENSE, GHS_K_FLAG_BITS, GHS_K_BUCKET, GHS_K_BMIN, GHS_K_WSTARTS, GHS_K_WMIN, GHS_K_HOT_HOOK,
-  GHS_K_TAIL_OPEN, GHS_K_TAIL_ROUND, GHS_K_TAIL_HOOK, GHS_K_BCOUNT, GHS_K_COUNT
+  GHS_K_TAIL_OPEN, GHS_K_TAIL_ROUND, GHS_K_TAIL_HOOK, GHS_K_COUNT
 };
 typedef struct ghs_kernel_record {
   uint32_t kernel;  /* ghs_kernel_id */
