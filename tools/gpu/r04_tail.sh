@@ -15,10 +15,11 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-me
 fatal $rc gpu-suite
 grep -E "FAILED|passed|failed" "$OUT/pytest_gpu.log" | tail -15
 fi
-for w in rmat grid grid-gradient; do
-  timeout -k 10 300 python3 -u bench.py --workload $w --no-cpu-baseline --no-scaling-base > "$OUT/bench_$w.json" 2> "$OUT/bench_$w.err"; rc=$?
-  fatal $rc bench-$w
-  [ $rc = 0 ] && python3 -c "import json;d=json.load(open('$OUT/bench_$w.json'));print('$w','value',round(d['value']/1e9,3),'ms',d['ms_per_step'],'s1',d['stage1_roofline']['frac'],'rounds',d['breakdown']['rounds'],'flags',d['breakdown']['pass_flags'])" || tail -5 "$OUT/bench_$w.err"
+for spec in rmat grid grid-gradient rmat:26; do
+  w=${spec%%:*}; extra=""; tag=$w; [ "$spec" != "$w" ] && { extra="--scale ${spec#*:}"; tag=${w}${spec#*:}; }
+  timeout -k 10 300 python3 -u bench.py --workload $w $extra --no-cpu-baseline --no-scaling-base > "$OUT/bench_$tag.json" 2> "$OUT/bench_$tag.err"; rc=$?
+  fatal $rc bench-$tag
+  [ $rc = 0 ] && python3 -c "import json;d=json.load(open('$OUT/bench_$tag.json'));print('$tag','value',round(d['value']/1e9,3),'ms',d['ms_per_step'],'s1',d['stage1_roofline']['frac'],'rounds',d['breakdown']['rounds'],'flags',d['breakdown']['pass_flags'])" || tail -5 "$OUT/bench_$tag.err"
 done
 for spec in rmat:24 grid:0; do
   wl=${spec%%:*}; sc=${spec#*:}
