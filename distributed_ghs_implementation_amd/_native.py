@@ -5,6 +5,7 @@ library. There is no CPU fallback — if the library is missing or no GPU is vis
 compute entry point raises. (The CPU restatement used to CHECK results lives in oracle/, which
 this package never imports.)
 """
+import atexit
 import collections.abc
 import ctypes
 import os
@@ -44,7 +45,7 @@ EXPORTED_SYMBOLS = (
     "ghs_rmat_temp_bytes", "ghs_rmat_generate", "ghs_rmat_tuples", "ghs_grid_generate",
     "ghs_profile_enable", "ghs_profile_read", "ghs_kernel_name",
     "ghs_comm_unique_id", "ghs_comm_init", "ghs_comm_destroy", "ghs_solver_run", "ghs_mst_emulated",
-    "ghs_release_cache",
+    "ghs_release_cache", "ghs_slot_retries",
 )
 
 
@@ -97,7 +98,7 @@ class RoundStatsList(collections.abc.Sequence):
         return repr(list(self))
 
 
-ABI_VERSION = 7  # include/ghs_mst.h GHS_MST_ABI_VERSION
+ABI_VERSION = 8  # include/ghs_mst.h GHS_MST_ABI_VERSION
 
 
 class Result(ctypes.Structure):
@@ -167,6 +168,8 @@ OPT_DETAIL = 0x40
 OPT_BUCKETED_FIRST = 0x80
 OPT_NO_WINDOW = 0x100
 OPT_NO_TAIL = 0x200
+OPT_CHECK_TOTALS = 0x400  # ABI 8: per level, report totals vs a stream-ordered copy of the counters
+OPT_KEEP_CACHE = 0x800    # ABI 8: the multi-rank drivers keep their per-rank state for the next call
 
 # ghs_result_t.pass_flags bits
 PASS_BUCKETED = 0x1
@@ -278,6 +281,7 @@ def load():
             "ghs_solver_run": (i32, [vp, vp]),
             "ghs_mst_emulated": (i32, [u32, u64, vp, vp, vp, i32, P(Config), vp, P(Result), P(RoundStats)]),
             "ghs_release_cache": (i32, []),
+            "ghs_slot_retries": (i32, [P(u64)]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(L, name)
@@ -286,7 +290,18 @@ def load():
         if L.ghs_abi_version() != ABI_VERSION:
             raise ImportError(f"libghs_mst.so ABI {L.ghs_abi_version()} != {ABI_VERSION}")
         _lib = L
+        # a driver call with OPT_KEEP_CACHE leaves per-rank workspaces (and an RCCL clique) cached:
+        # free them before the interpreter tears the HIP runtime down
+        atexit.register(_release_at_exit)
         return _lib
+
+
+def _release_at_exit():
+    if _lib is not None:
+        try:
+            _lib.ghs_release_cache()
+        except Exception:
+            pass
 
 
 def check(rc):
@@ -334,6 +349,13 @@ class Comm:
 def release_cache():
     """Free the multi-rank drivers' cached per-rank state (ghs_release_cache)."""
     check(load().ghs_release_cache())
+
+
+def slot_retries():
+    """Round reports the host re-read because their checksum failed (seq landed before a field)."""
+    c = ctypes.c_uint64(0)
+    check(load().ghs_slot_retries(ctypes.byref(c)))
+    return c.value
 
 
 def device_count():

@@ -2959,12 +2959,17 @@ __global__ void k_unpack_best(const uint32_t *__restrict__ act, const unsigned l
 }
 
 // Result of a round, written into coherent pinned host memory by the round's last kernel; the
-// host polls seq (written last, after a system-scope fence).
+// host polls seq (written last).
 constexpr int C_ERR_IDX = 4;  // == C_ERR (counter layout below)
+constexpr int C_LONG_IDX = 10;  // == C_LONG
 
-// ONE 64-byte line per slot: the host sees seq and the fields in the same line, so the drained
-// field stores are visible once seq is (a slot straddling two lines could show a new seq beside a
-// stale weight — round 4 measured exactly that with a 72-byte slot).
+// A report carries a checksum of (seq, every field): the host accepts a slot only when the fields
+// it read hash to the checksum it read. Nothing in the HIP memory model orders the field stores
+// before the seq store for a host reader short of a system-scope release (whose L2 write-back held
+// the next round's first kernel ~6 us, every round); round 4 saw a new seq beside a stale weight
+// when the slot straddled two 64-B lines. With the checksum, a stale or torn field (the slot's
+// previous report, or a store still in flight) fails the check and the host polls again, whatever
+// order the stores land in.
 struct alignas(64) RoundSlot {
   unsigned long long live_out, nact_out, edges;
   unsigned long long err;      // error bits (low word); bit 32: counter C_LONG, a level-0 edge spans > 1
@@ -2973,31 +2978,56 @@ struct alignas(64) RoundSlot {
   unsigned long long nact_in;  // active fragments this round started from (a level's first round: the level's)
   unsigned long long pending;  // pending edges after the level's pass (counter C_PENDING)
   unsigned long long weight;   // MSF weight so far (counter C_WEIGHT)
+  unsigned long long chk;      // slot_checksum(seq, the fields above)
 };
-static_assert(sizeof(RoundSlot) == 64, "a round report is one 64-byte line");
 constexpr unsigned long long SLOT_SPAN = 1ull << 32;
 __host__ __device__ __forceinline__ unsigned long long slot_err(unsigned long long e) { return e & 0xffffffffull; }
+
+__host__ __device__ __forceinline__ unsigned long long slot_mix(unsigned long long h, unsigned long long x) {
+  h ^= x + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+  h ^= h >> 30;  // splitmix64 finalizer
+  h *= 0xbf58476d1ce4e5b9ull;
+  h ^= h >> 27;
+  h *= 0x94d049bb133111ebull;
+  h ^= h >> 31;
+  return h;
+}
+
+__host__ __device__ __forceinline__ unsigned long long slot_checksum(unsigned long long seq, unsigned long long live_out,
+                                                                     unsigned long long nact_out, unsigned long long edges,
+                                                                     unsigned long long err, unsigned long long nact_in,
+                                                                     unsigned long long pending, unsigned long long weight) {
+  unsigned long long h = slot_mix(0x5107ull, seq);
+  h = slot_mix(h, live_out);
+  h = slot_mix(h, nact_out);
+  h = slot_mix(h, edges);
+  h = slot_mix(h, err);
+  h = slot_mix(h, nact_in);
+  h = slot_mix(h, pending);
+  return slot_mix(h, weight);
+}
 
 __device__ __forceinline__ void write_report(RoundSlot *slot, unsigned long long seq, const unsigned long long *cnt,
                                              unsigned long long nact_out, unsigned long long nact_in) {
   // device-scope loads: the error bits may come from other workgroups of the writing launch
   const unsigned long long live = __hip_atomic_load(cnt + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned long long edges = __hip_atomic_load(cnt + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long err = __hip_atomic_load(cnt + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long err = __hip_atomic_load(cnt + C_ERR_IDX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned long long pending = __hip_atomic_load(cnt + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned long long weight = __hip_atomic_load(cnt + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long span = __hip_atomic_load(cnt + 10, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // The slot is coherent (uncached) host memory: its stores bypass the L2, so draining them
-  // (vmcnt(0)) before the seq store orders them for the host's acquire load of seq. No
-  // __threadfence_system(): its L2 write-back of every dirty line held the next round's first
-  // kernel back by ~6 us (measured, every round).
-  slot->live_out = live;          // live edges after this round's compaction
-  slot->nact_out = nact_out;      // active fragments of the next round
-  slot->edges = edges;            // MSF edges so far
-  slot->err = slot_err(err) | (span ? SLOT_SPAN : 0ull);  // error bits + the span flag
-  slot->nact_in = nact_in;
-  slot->pending = pending;
-  slot->weight = weight;
+  const unsigned long long span = __hip_atomic_load(cnt + C_LONG_IDX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long e = slot_err(err) | (span ? SLOT_SPAN : 0ull);  // error bits + the span flag
+  // system-scope stores to the coherent (uncached) host slot; the checksum makes the host's read
+  // independent of the order in which they land
+  __hip_atomic_store(&slot->live_out, live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&slot->nact_out, nact_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&slot->edges, edges, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&slot->err, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&slot->nact_in, nact_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&slot->pending, pending, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&slot->weight, weight, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&slot->chk, slot_checksum(seq, live, nact_out, edges, e, nact_in, pending, weight),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(&slot->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -3611,7 +3641,8 @@ enum : int {
   C_RS_WEIGHT = 11,  // [11], [12]: a rank's own-range part of the reduce-scatter round's totals
   C_COUNT = 16
 };
-static_assert(C_WEIGHT == 2 && C_EDGES == 3 && C_ERR == 4 && C_PENDING == 5, "write_report reads the counters by index");
+static_assert(C_WEIGHT == 2 && C_EDGES == 3 && C_ERR == C_ERR_IDX && C_PENDING == 5 && C_LONG == C_LONG_IDX,
+              "write_report reads the counters by index");
 
 constexpr int SLOT_RING = 8;
 // rounds enqueued ahead of the host's termination check (GHS_LOOKAHEAD: 0..4). R-MAT s24: 1 ->
@@ -3780,6 +3811,8 @@ struct ghs_solver {
   bool tail_ran = false;        // a level finished in the LDS tail (k_tail_*)
   TailBufs tail{};              // the LDS tail's arrays (one rank; tail.ctl == nullptr: no tail)
   bool tail_on = true;          // GHS_OPT_NO_TAIL clears it
+  bool check_totals = false;    // GHS_OPT_CHECK_TOTALS: report totals vs a stream-ordered counter copy per level
+  uint32_t totals_checked = 0;  // levels whose totals were checked (diagnostic)
   // bucketed rounds (single rank, lattice-like graphs; k_bucket / k_bmin): the record buffers,
   // the offsets table, the bucket geometry, and the per-solve / per-round decisions
   uint4 *rec = nullptr;         // records (a, b, key): 16 B each
@@ -4717,19 +4750,42 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
   return GHS_OK;
 }
 
-// spin until the round report with this seq has landed in the pinned slot (the stream keeps
-// running); a failed or drained stream without the report is an error, never a hang. The stream
-// is queried only after SLOT_QUIET_MS of waiting: hipStreamQuery enqueues a marker behind the
-// last launch, and its system-scope release idled the GPU ~5.6 us before every round >= 2.
+// spin until the round report with this seq has landed in the pinned slot and its fields match
+// its checksum, and copy it to *out (the stream keeps running); a failed or drained stream without
+// the report is an error, never a hang. The stream is queried only after SLOT_QUIET_MS of waiting:
+// hipStreamQuery enqueues a marker behind the last launch, and its system-scope release idled the
+// GPU ~5.6 us before every round >= 2.
 constexpr int SLOT_QUIET_MS = 20;
 constexpr int SLOT_QUERY_MS = 5;
-static int wait_slot(ghs_solver *s, const RoundSlot *hs, unsigned long long seq) {
-  if (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) == seq) return GHS_OK;
+
+// one read of the slot: true when seq is the expected one and the fields hash to the checksum
+static bool slot_read(const RoundSlot *hs, unsigned long long seq, RoundSlot *out) {
+  if (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) != seq) return false;
+  RoundSlot r;
+  r.live_out = __atomic_load_n(&hs->live_out, __ATOMIC_ACQUIRE);
+  r.nact_out = __atomic_load_n(&hs->nact_out, __ATOMIC_ACQUIRE);
+  r.edges = __atomic_load_n(&hs->edges, __ATOMIC_ACQUIRE);
+  r.err = __atomic_load_n(&hs->err, __ATOMIC_ACQUIRE);
+  r.nact_in = __atomic_load_n(&hs->nact_in, __ATOMIC_ACQUIRE);
+  r.pending = __atomic_load_n(&hs->pending, __ATOMIC_ACQUIRE);
+  r.weight = __atomic_load_n(&hs->weight, __ATOMIC_ACQUIRE);
+  r.chk = __atomic_load_n(&hs->chk, __ATOMIC_ACQUIRE);
+  r.seq = seq;
+  if (r.chk != slot_checksum(seq, r.live_out, r.nact_out, r.edges, r.err, r.nact_in, r.pending, r.weight)) return false;
+  *out = r;
+  return true;
+}
+
+static uint64_t g_slot_retries = 0;  // reads whose seq had landed before every field did (diagnostic)
+
+static int wait_slot(ghs_solver *s, const RoundSlot *hs, unsigned long long seq, RoundSlot *out) {
+  if (slot_read(hs, seq, out)) return GHS_OK;
   const auto t0 = std::chrono::steady_clock::now();
   unsigned spins = 0;
   bool quiet = true;
   auto last_query = t0;
-  while (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) != seq) {
+  while (!slot_read(hs, seq, out)) {
+    if (__atomic_load_n(&hs->seq, __ATOMIC_RELAXED) == seq) __atomic_fetch_add(&g_slot_retries, 1, __ATOMIC_RELAXED);
     if ((spins & 255) == 0 && solver_cancelled(s)) GHS_FAIL(GHS_E_STATE, "cancelled: another rank of the solve failed");
     if ((++spins & 255) == 0 && quiet)
       quiet = std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(SLOT_QUIET_MS);
@@ -4744,8 +4800,11 @@ static int wait_slot(ghs_solver *s, const RoundSlot *hs, unsigned long long seq)
         last_query = now;
         const hipError_t q = hipStreamQuery(s->stream);
         if (q != hipSuccess && q != hipErrorNotReady) GHS_HIP_CHECK(q);
-        if (q == hipSuccess && __atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) != seq)
+        if (q == hipSuccess && !slot_read(hs, seq, out)) {
+          if (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) == seq)
+            GHS_FAIL(GHS_E_STATE, "round report fails its checksum after the stream drained");
           GHS_FAIL(GHS_E_STATE, "round report missing after the stream drained");
+        }
       }
     }
   }
@@ -4773,6 +4832,20 @@ static void push_stats(ghs_solver *s, uint32_t level_round, uint64_t live_in, ui
   st.hooks = edges_total - s->edges_before;
   s->edges_before = edges_total;
   s->stats.push_back(st);
+}
+
+// GHS_OPT_CHECK_TOTALS: the device counters behind the level's last kernel (a stream-ordered copy)
+// against the totals of the level's last report (the trailing lookahead rounds change no counter)
+static int check_level_totals(ghs_solver *s) {
+  if (!s->check_totals || !s->report_final) return GHS_OK;
+  GHS_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->cnt, C_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
+  if (int rc = solver_sync(s)) return rc;
+  if (s->h_cnt[C_WEIGHT] != s->rep_weight || s->h_cnt[C_EDGES] != s->rep_edges)
+    GHS_FAIL(GHS_E_STATE, "level " + std::to_string(s->level) + ": report totals (" + std::to_string(s->rep_weight) + ", " +
+                              std::to_string(s->rep_edges) + ") differ from the device counters (" +
+                              std::to_string(s->h_cnt[C_WEIGHT]) + ", " + std::to_string(s->h_cnt[C_EDGES]) + ")");
+  ++s->totals_checked;
+  return GHS_OK;
 }
 
 static void close_level(ghs_solver *s) {
@@ -4890,16 +4963,16 @@ static int run_tail(ghs_solver *s, uint64_t prev_in) {
     GHS_HIP_CHECK(hipMemcpyAsync(s->res->h_tail, tb.ctl, sizeof(TailCtl), hipMemcpyDeviceToHost, st));
     k_tail_report<<<1, 1, 0, st>>>(tb, last, dslot, seq, s->cnt);
     GHS_HIP_CHECK(hipGetLastError());
-    const RoundSlot *hs = s->h_slot + (seq % SLOT_RING);
-    if (int rc = wait_slot(s, hs, seq)) return rc;
-    if (slot_err(hs->err)) return fail_counters(s, slot_err(hs->err), "in the LDS tail");
-    s->rep_weight = hs->weight;
-    s->rep_edges = hs->edges;
+    RoundSlot rep;
+    if (int rc = wait_slot(s, s->h_slot + (seq % SLOT_RING), seq, &rep)) return rc;
+    if (slot_err(rep.err)) return fail_counters(s, slot_err(rep.err), "in the LDS tail");
+    s->rep_weight = rep.weight;
+    s->rep_edges = rep.edges;
     s->report_final = true;
     if (s->debug)
-      fprintf(stderr, "[ghs] level %u tail batch report: nact_out %llu edges %llu weight %llu\n", s->level, hs->nact_out,
-              hs->edges, hs->weight);
-    if (hs->nact_out <= 1) break;
+      fprintf(stderr, "[ghs] level %u tail batch report: nact_out %llu edges %llu weight %llu\n", s->level, rep.nact_out,
+              rep.edges, rep.weight);
+    if (rep.nact_out <= 1) break;
     if (r > TAIL_ROUNDS_MAX) return fail_counters(s, 4, "in the LDS tail (round cap)");
   }
   const TailCtl &c = *s->res->h_tail;
@@ -4909,6 +4982,7 @@ static int run_tail(ghs_solver *s, uint64_t prev_in) {
   s->level_round = lr0 + rounds;
   s->tail_ran = true;
   if (s->ev_rec.size() > s->round) s->ev_rec.resize(s->round);
+  if (int rc = check_level_totals(s)) return rc;
   close_level(s);
   return GHS_OK;
 }
@@ -4942,16 +5016,10 @@ static int run_level_pipelined(ghs_solver *s) {
       continue;
     }
   check:
-    const RoundSlot *hs = s->h_slot + (checked % SLOT_RING);
-    if (int rc = wait_slot(s, hs, seqs[checked])) return rc;
     RoundSlot r;
-    r.live_out = hs->live_out;
-    r.nact_out = hs->nact_out;
-    r.edges = hs->edges;
-    r.err = slot_err(hs->err);
-    r.nact_in = hs->nact_in;
-    r.pending = hs->pending;
-    r.weight = hs->weight;
+    if (int rc = wait_slot(s, s->h_slot + (checked % SLOT_RING), seqs[checked], &r)) return rc;
+    const unsigned long long span_flag = r.err & SLOT_SPAN;
+    r.err = slot_err(r.err);
     s->rep_weight = r.weight;
     s->rep_edges = r.edges;
     s->report_final = true;
@@ -4971,7 +5039,7 @@ static int run_level_pipelined(ghs_solver *s) {
       nact_prev = r.nact_in;
       if (s->level == 0) s->select_out = S;
       else if (s->filter_run && !s->filter_out) s->filter_out = S + s->rem_total;
-      if (s->level == 0 && s->windowed_enq) s->windowed_ran = (hs->err & SLOT_SPAN) == 0;
+      if (s->level == 0 && s->windowed_enq) s->windowed_ran = span_flag == 0;
       if (s->debug) {
         uint32_t g[2] = {0, 0};
         (void)hipMemcpy(g, s->giant, 8, hipMemcpyDeviceToHost);
@@ -4997,6 +5065,7 @@ static int run_level_pipelined(ghs_solver *s) {
   // are forgotten and re-recorded by the next level)
   s->round = round0 + checked;
   if (s->ev_rec.size() > s->round) s->ev_rec.resize(s->round);
+  if (int rc = check_level_totals(s)) return rc;
   close_level(s);
   return GHS_OK;
 }
@@ -5004,6 +5073,12 @@ static int run_level_pipelined(ghs_solver *s) {
 extern "C" {
 
 int ghs_abi_version(void) { return GHS_MST_ABI_VERSION; }
+
+int ghs_slot_retries(uint64_t *count) {
+  if (!count) GHS_FAIL(GHS_E_ARG, "count is NULL");
+  *count = __atomic_load_n(&g_slot_retries, __ATOMIC_RELAXED);
+  return GHS_OK;
+}
 
 int ghs_profile_enable(int on) {
   std::lock_guard<std::mutex> lock(g_prof_mutex);
@@ -5125,6 +5200,7 @@ static int solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint
   s->seed_runs = (opt & GHS_OPT_NO_SEED_RUNS) == 0;
   s->windowed = (opt & GHS_OPT_NO_WINDOW) == 0;
   s->tail_on = (opt & GHS_OPT_NO_TAIL) == 0;
+  s->check_totals = (opt & GHS_OPT_CHECK_TOTALS) != 0;
   s->dedup_max = s->cfg.dedup_max;
   {
     std::lock_guard<std::mutex> lock(g_prof_mutex);
@@ -5492,10 +5568,10 @@ int ghs_solver_contract_async(ghs_solver *s, int *done) {
   while (s->pipe.size() > 1 && !level_done) {  // read every report but the newest round's
     const ghs_solver::PipeRound p = s->pipe.front();
     s->pipe.erase(s->pipe.begin());
-    const RoundSlot *hs = s->h_slot + (p.seq % SLOT_RING);
-    if (int rc = wait_slot(s, hs, p.seq)) return rc;
-    const unsigned long long err = slot_err(hs->err), nact_in = hs->nact_in, nact_out = hs->nact_out;
-    const unsigned long long live_out = hs->live_out, edges = hs->edges;
+    RoundSlot rep;
+    if (int rc = wait_slot(s, s->h_slot + (p.seq % SLOT_RING), p.seq, &rep)) return rc;
+    const unsigned long long err = slot_err(rep.err), nact_in = rep.nact_in, nact_out = rep.nact_out;
+    const unsigned long long live_out = rep.live_out, edges = rep.edges;
     if (err) return fail_counters(s, err, ("in round " + std::to_string(p.round + 1)).c_str());
     push_stats(s, p.level_round, s->pipe_live, nact_in, edges);
     s->pipe_live = live_out;
@@ -5519,11 +5595,11 @@ int ghs_solver_contract_async(ghs_solver *s, int *done) {
       while (!s->pipe.empty()) {
         const ghs_solver::PipeRound p = s->pipe.front();
         s->pipe.erase(s->pipe.begin());
-        const RoundSlot *hs = s->h_slot + (p.seq % SLOT_RING);
-        if (int rc = wait_slot(s, hs, p.seq)) return rc;
-        if (slot_err(hs->err)) return fail_counters(s, slot_err(hs->err), ("in round " + std::to_string(p.round + 1)).c_str());
-        push_stats(s, p.level_round, s->pipe_live, hs->nact_in, hs->edges);
-        s->pipe_live = hs->live_out;
+        RoundSlot rep;
+        if (int rc = wait_slot(s, s->h_slot + (p.seq % SLOT_RING), p.seq, &rep)) return rc;
+        if (slot_err(rep.err)) return fail_counters(s, slot_err(rep.err), ("in round " + std::to_string(p.round + 1)).c_str());
+        push_stats(s, p.level_round, s->pipe_live, rep.nact_in, rep.edges);
+        s->pipe_live = rep.live_out;
       }
       if (int rc = dense_close(s)) return rc;
       close_level(s);
@@ -5540,9 +5616,9 @@ extern "C" {
 int ghs_solver_finish(ghs_solver_t *s, ghs_result_t *result, ghs_round_stats_t *stats) {
   if (!s) GHS_FAIL(GHS_E_ARG, "solver is NULL");
   if (s->phase != 2) GHS_FAIL(GHS_E_STATE, "finish before the loop terminated");
-  if (s->report_final) {
-    // the pipelined loop's last report already holds the final totals: no copy, no sync (a
-    // trailing no-op lookahead round may still run on the stream; it changes no counter)
+  if (s->report_final && !s->check_totals) {
+    // the pipelined loop's last report (checksum-validated) holds the final totals: no copy, no
+    // sync (a trailing no-op lookahead round may still run on the stream; it changes no counter)
     s->h_cnt[C_WEIGHT] = s->rep_weight;
     s->h_cnt[C_EDGES] = s->rep_edges;
   } else {
@@ -5599,6 +5675,7 @@ int ghs_solver_reset(ghs_solver_t *s) {
   t.debug = s->debug; t.lookahead = s->lookahead; t.seed_runs = s->seed_runs; t.dedup_max = s->dedup_max;
   t.windowed = s->windowed;
   t.tail_on = s->tail_on;
+  t.check_totals = s->check_totals;
   t.detail = s->detail; t.time_rounds = s->time_rounds;
   t.group_cancel = s->group_cancel;
   { std::lock_guard<std::mutex> lock(g_prof_mutex); t.prof = g_prof_on; }

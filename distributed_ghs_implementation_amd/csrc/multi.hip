@@ -461,9 +461,12 @@ DriverCache *cache_acquire(int kind, const std::vector<int> &devs, uint32_t n, u
   return g_drv;
 }
 
-// after a call: a failed call leaves no state behind (aborted communicators, cancelled solvers)
-void cache_release_on(int rc) {
-  if (rc == GHS_OK || !g_drv) return;
+// after a call: a failed call leaves no state behind (aborted communicators, cancelled solvers),
+// and a successful one keeps it only when the caller asked (GHS_OPT_KEEP_CACHE): the cached
+// workspaces are invisible to the caller's allocator (s26 x 8 emulated: ~8 x 11 GB on one device)
+void cache_release_on(int rc, const ghs_config_t *cfg) {
+  const bool keep = rc == GHS_OK && cfg && (cfg->options & GHS_OPT_KEEP_CACHE);
+  if (keep || !g_drv) return;
   cache_free(g_drv);
   g_drv = nullptr;
 }
@@ -498,6 +501,10 @@ int rank_solve(Rank &d, int r, int N, uint32_t n, uint64_t m, const uint32_t *du
   if (!rc && hipSetDevice(x.dev) != hipSuccess) {
     ghs::set_error("hipSetDevice failed");
     rc = GHS_E_HIP;
+  }
+  if (!rc && c2.fault_rank && c2.fault_round && N == 1) {  // a one-rank loop has no round exchange to fail in
+    ghs::set_error("fault_round needs num_ranks > 1");
+    rc = GHS_E_ARG;
   }
   if (!rc && c2.fault_rank == (uint32_t)r + 1 && c2.fault_round == 0) {  // test hook (ghs_config_t.fault_rank)
     ghs::set_error("injected setup failure (fault_rank)");
@@ -733,7 +740,7 @@ extern "C" int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const ui
   }
   for (auto &x : d) rank_detach(x);
   for (ghs_comm &k : C->comms) k.group_cancel = nullptr;
-  cache_release_on(rc);
+  cache_release_on(rc, cfg);
   (void)hipSetDevice(prev);
   if (rc) GHS_FAIL(rc, err);
   return GHS_OK;
@@ -787,7 +794,7 @@ extern "C" int ghs_mst_emulated(uint32_t n, uint64_t m, const uint32_t *d_u, con
     k.emu = nullptr;
     k.group_cancel = nullptr;
   }
-  cache_release_on(rc);
+  cache_release_on(rc, cfg);
   (void)hipSetDevice(dev);
   if (rc) GHS_FAIL(rc, err);
   return GHS_OK;

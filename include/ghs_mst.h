@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GHS_MST_ABI_VERSION 7
+#define GHS_MST_ABI_VERSION 8
 
 #define GHS_OK 0
 #define GHS_NEED_EXCHANGE 1   /* ghs_solver_minedge on a multi-rank solver opened a level: OR-combine
@@ -119,6 +119,15 @@ typedef struct ghs_result {
 #define GHS_OPT_NO_TAIL 0x200u     /* one rank: no LDS tail — every round of a level through the
                                       per-round kernels (default: once a level's active fragments fit
                                       the tail's LDS, its remaining rounds run in k_tail_*) */
+/* ABI 8 */
+#define GHS_OPT_CHECK_TOTALS 0x400u /* one rank: at the end of every level the device counters are copied
+                                       behind the level's last kernel (stream-ordered) and compared with
+                                       the totals of the level's last round report (GHS_E_STATE if they
+                                       differ); the solve's totals then come from that copy (test /
+                                       diagnostic: one host sync per level) */
+#define GHS_OPT_KEEP_CACHE 0x800u  /* ghs_mst_multi / ghs_mst_emulated: keep the per-rank state for the
+                                      next call of the same shape (default: freed when the call returns;
+                                      see ghs_release_cache) */
 typedef struct ghs_config {
   uint32_t max_levels;
   uint32_t num_ranks;         /* ranks sharing the solve (1 = single GPU; >1: identical rounds on
@@ -132,7 +141,8 @@ typedef struct ghs_config {
                                  made to fail (ghs_mst_multi / ghs_mst_emulated); 0 = none */
   uint32_t fault_round;       /* ABI 7 test hook: with fault_rank set, that rank fails in the round
                                  loop (ghs_solver_run) once it has completed this many rounds instead
-                                 of at setup; 0 = the setup failure above */
+                                 of at setup; 0 = the setup failure above. ABI 8: GHS_E_ARG with
+                                 num_ranks == 1 (a one-rank loop has no exchange to fail in) */
 } ghs_config_t;
 
 /* ---- library / device ------------------------------------------------------------------- */
@@ -165,12 +175,13 @@ int ghs_mst_host(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t *v, c
 int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t *v, const uint32_t *w,
                   int num_gpus, const int *devices, const ghs_config_t *cfg, uint8_t *in_mst,
                   ghs_result_t *result, ghs_round_stats_t *stats);
-/* ABI 7: the multi-rank drivers (ghs_mst_multi, ghs_mst_emulated) keep their per-rank state —
- * streams, workspaces, replicated canonical copies, pinned report rings, collective scratch, and
- * ghs_mst_multi's RCCL clique — in one process-wide cache keyed by (driver, devices, ranks, n, m);
- * a later call of the same shape allocates nothing (ghs_result_t.reused = 1), a call of another
- * shape or a failed call frees it first. ghs_release_cache frees it now (device memory back to
- * the caller; safe to call at any time outside a driver call). */
+/* ABI 7/8: with GHS_OPT_KEEP_CACHE the multi-rank drivers (ghs_mst_multi, ghs_mst_emulated) keep
+ * their per-rank state — streams, workspaces, replicated canonical copies, pinned report rings,
+ * collective scratch, and ghs_mst_multi's RCCL clique — in one process-wide cache keyed by (driver,
+ * devices, ranks, n, m); a later call of the same shape allocates nothing (ghs_result_t.reused = 1),
+ * a call of another shape or a failed call frees it first. Without the option (ABI 8 default) a
+ * call frees its state before returning. ghs_release_cache frees it now (device memory back to the
+ * caller; safe to call at any time outside a driver call). */
 int ghs_release_cache(void);
 
 /* ---- device-resident API -----------------------------------------------------------------
@@ -307,6 +318,10 @@ int ghs_solver_run(ghs_solver_t *h, ghs_comm_t *comm);
 int ghs_mst_emulated(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
                      int num_ranks, const ghs_config_t *cfg, uint8_t *d_in_mst, ghs_result_t *result,
                      ghs_round_stats_t *stats);
+
+/* ABI 8 diagnostic: round reports whose sequence number the host read before every field had
+ * landed (the checksum of the report failed and the host polled again), since the process started */
+int ghs_slot_retries(uint64_t *count);
 
 /* ---- per-launch profile ------------------------------------------------------------------
  * The reference measured only wall time (time.time(), ghs_implementation.py:453-464,

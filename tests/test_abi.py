@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi():
     L = _native.load()
-    assert L.ghs_abi_version() == _native.ABI_VERSION == 7
+    assert L.ghs_abi_version() == _native.ABI_VERSION == 8
     assert _native.device_count() >= 0
 
 
@@ -70,6 +70,13 @@ def test_rank_limits_rejected():
     assert L.ghs_comm_init(2, 2, uid, ctypes.byref(h)) == _native.GHS_E_ARG
     assert L.ghs_mst_emulated(4, 0, None, None, None, 65, None, None, None, None) == _native.GHS_E_ARG
     assert L.ghs_release_cache() == _native.GHS_OK
+
+
+def test_slot_retries_diagnostic():
+    """ABI 8: the count of round reports re-read for a failed checksum (none without a GPU)."""
+    assert _native.slot_retries() == 0
+    L = _native.load()
+    assert L.ghs_slot_retries(None) == _native.GHS_E_ARG
 
 
 def test_null_arguments_rejected():

@@ -478,13 +478,25 @@ def test_rank_mid_solve_failure_fails_every_rank(world, fault, round_, torch_cud
         emulated_mst(e, world, config=_native.make_config(fault_rank=fault, fault_round=round_))
     assert ei.value.code == _native.GHS_E_STATE
     assert "injected mid-solve failure" in str(ei.value)
+    keep = _native.make_config(options=_native.OPT_KEEP_CACHE)
     for k in range(2):
-        res, _, flags = emulated_mst(e, world)
+        res, _, flags = emulated_mst(e, world, config=keep)
         assert np.array_equal(flags.cpu().numpy().astype(bool), ref_in.astype(bool))
         assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
         assert res.reused == k  # the failed call left nothing cached; the second call reuses
         assert res.ms_setup > 0 and res.ms_solve > 0
     _native.release_cache()
+
+
+def test_fault_round_rejected_with_one_rank(torch_cuda):
+    """fault_round on a one-rank loop (no exchange to fail in) is GHS_E_ARG, not a
+    silent success."""
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import emulated_mst, generate_rmat
+    e = generate_rmat(11, 16, seed=1, wseed=2)
+    with pytest.raises(_native.GHSError) as ei:
+        emulated_mst(e, 1, config=_native.make_config(fault_rank=1, fault_round=1))
+    assert ei.value.code == _native.GHS_E_ARG
 
 
 def test_driver_cache_follows_the_shape(torch_cuda):
@@ -495,19 +507,44 @@ def test_driver_cache_follows_the_shape(torch_cuda):
     from distributed_ghs_implementation_amd.mst import minimum_spanning_forest
     ora = _oracle()
     a, b = generate_rmat(11, 16, seed=1, wseed=2), generate_rmat(12, 16, seed=1, wseed=2)
+    keep = _native.make_config(options=_native.OPT_KEEP_CACHE)
     seen = []
-    for e, world in ((a, 2), (a, 2), (b, 2), (b, 3), (b, 3)):
-        res, _, flags = emulated_mst(e, world)
+    # the last call is without OPT_KEEP_CACHE: it runs on the kept state, then frees it (ABI 8)
+    for e, world, cfg in ((a, 2, keep), (a, 2, keep), (b, 2, keep), (b, 3, keep), (b, 3, None), (b, 3, keep)):
+        res, _, flags = emulated_mst(e, world, config=cfg)
         g = e.to_host()
         ref_in, _, _ = ora.kruskal_c(g.n, g.u, g.v, g.w)
         assert np.array_equal(flags.cpu().numpy().astype(bool), ref_in.astype(bool))
         seen.append(res.reused)
-    assert seen == [0, 1, 0, 0, 1]
+    assert seen == [0, 1, 0, 0, 1, 0]
     g = b.to_host()
     ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
     for k in range(2):
-        r = minimum_spanning_forest(g, devices=[0])
+        r = minimum_spanning_forest(g, devices=[0], config=keep)
         assert np.array_equal(r.in_mst, ref_in.astype(bool))
+    _native.release_cache()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_driver_cache_reuse_with_other_graph_same_shape(world, torch_cuda):
+    """the cached per-rank state re-solving a DIFFERENT graph of the same (n, m) — other
+    edges, other weights — so leftover workspace contents (tail buffers, collective scratch, report
+    rings) cannot pass for fresh memory: both graphs' MSFs equal the oracle's, the second call runs
+    on the first's state (reused = 1)."""
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import DeviceEdges, emulated_mst, generate_rmat
+    ora = _oracle()
+    a, b = generate_rmat(13, 16, seed=1, wseed=2), generate_rmat(13, 16, seed=9, wseed=10)
+    mm = min(a.m, b.m) & ~3
+    graphs = [DeviceEdges(x.n, x.u[:mm], x.v[:mm], x.w[:mm]) for x in (a, b)]  # a canonical prefix is canonical
+    keep = _native.make_config(options=_native.OPT_KEEP_CACHE)
+    for i, e in enumerate(graphs + graphs[:1]):
+        res, _, flags = emulated_mst(e, world, config=keep)
+        g = e.to_host()
+        ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+        assert np.array_equal(flags.cpu().numpy().astype(bool), ref_in.astype(bool)), i
+        assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
+        assert res.reused == (1 if i else 0)
     _native.release_cache()
 
 
@@ -948,6 +985,31 @@ def test_lds_tail_vs_oracle(graph, levels, opt, torch_cuda):
     eligible = any(0 < i and st0[i - 1]["level"] == st["level"] and 2 <= st["active_components"] <= 12288
                    for i, st in enumerate(st0))
     assert bool(res.pass_flags & _native.PASS_TAIL) == eligible, (graph, st0)
+
+
+@pytest.mark.parametrize("graph", ["rmat", "rmat20", "ties", "forest", "readme", "grid", "grid-gradient"])
+@pytest.mark.parametrize("opt", ["default", "no_tail", "bucketed"])
+def test_report_totals_match_ordered_counters(graph, opt, torch_cuda):
+    """VERDICT r04 #4 / ADVICE r04: the running totals the host takes from each level's last round
+    report (a checksum-validated pinned slot) equal a stream-ordered copy of the device counters made
+    behind the level's last kernel (GHS_OPT_CHECK_TOTALS: the library compares them at the end of
+    EVERY level and fails with GHS_E_STATE if they differ), on the tail and non-tail paths; the
+    solve's totals then come from that copy and equal the oracle's."""
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import DeviceMST
+    ora = _oracle()
+    e = _test_graph(graph)
+    g = e.to_host()
+    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    base = {"default": 0, "no_tail": _native.OPT_NO_TAIL, "bucketed": _native.OPT_BUCKETED}[opt]
+    for levels in (None, 1):
+        kw = {} if levels is None else {"max_levels": levels}
+        eng = DeviceMST(e, config=_native.make_config(options=base | _native.OPT_CHECK_TOTALS, **kw))
+        for _ in range(2):
+            res, _ = eng.run()
+            assert np.array_equal(eng.in_mst_host(), ref_in.astype(bool))
+            assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
+    assert _native.slot_retries() >= 0
 
 
 @pytest.mark.parametrize("seed,n,m,wmax", [(21, 300, 2000, 1), (22, 12000, 40000, 3), (23, 13000, 26000, 100),
