@@ -444,6 +444,46 @@ __device__ __forceinline__ uint32_t seg_find(const uint64_t *__restrict__ prefix
   return lo;
 }
 
+// The same search by one full wave (every lane of it calls): a 64-ary search — each step one load
+// per lane and a ballot — so nseg <= 4096 takes 2 dependent loads and SEG_MAX 3, where the binary
+// search by one thread took ~13, all of them on the critical path of a streaming kernel's first
+// tile (the block waits on them at its first barrier). Both ends of a block's range at once.
+__device__ __forceinline__ void seg_find_wave2(const uint64_t *__restrict__ prefix, uint32_t nseg, uint64_t v0,
+                                               uint64_t v1, uint32_t *r0, uint32_t *r1) {
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  uint32_t lo0 = 0, c0 = nseg, lo1 = 0, c1 = nseg;  // candidates [lo, lo + c): prefix[lo] <= v
+  while (c0 > 1 || c1 > 1) {
+    const uint32_t st0 = (c0 + WAVE - 1) / WAVE, st1 = (c1 + WAVE - 1) / WAVE;
+    const bool in0 = c0 > 1 && lane * st0 < c0, in1 = c1 > 1 && lane * st1 < c1;
+    const uint64_t p0 = in0 ? prefix[lo0 + lane * st0] : ~0ull;
+    const uint64_t p1 = in1 ? prefix[lo1 + lane * st1] : ~0ull;
+    const uint64_t m0 = __ballot(in0 && p0 <= v0), m1 = __ballot(in1 && p1 <= v1);
+    if (c0 > 1) {  // m0 has lane 0's bit: prefix[lo0] <= v0
+      const uint32_t L = 63u - (uint32_t)__clzll((long long)m0);
+      lo0 += L * st0;
+      c0 = min(st0, c0 - L * st0);
+    }
+    if (c1 > 1) {
+      const uint32_t L = 63u - (uint32_t)__clzll((long long)m1);
+      lo1 += L * st1;
+      c1 = min(st1, c1 - L * st1);
+    }
+  }
+  *r0 = lo0;
+  *r1 = lo1;
+}
+
+// a block's range [vb, ve) of T virtual entries -> its first and last region (wave 0 calls)
+__device__ __forceinline__ void seg_range_wave(const uint64_t *__restrict__ prefix, uint32_t nseg, uint64_t vb,
+                                               uint64_t ve, uint64_t T, uint32_t *s_seg) {
+  uint32_t a = 0, b = 0;
+  seg_find_wave2(prefix, nseg, vb < T ? vb : 0, ve > vb ? ve - 1 : 0, &a, &b);
+  if (threadIdx.x == 0) {
+    s_seg[0] = vb < T ? a : 0;
+    s_seg[1] = ve > vb ? b : 0;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Segmented edge input: every region holds a multiple of 4 entries and starts at a multiple of
 // 4 (dead entries, a == LABEL_NONE, pad the regions), so a lane's 4-entry tile at a virtual
@@ -518,10 +558,7 @@ GHS_STREAM_KERNEL_6 void k_minedge(const uint32_t *__restrict__ src, const uint3
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;  // multiple of 4
   const uint64_t vb = Q * blockIdx.x;
   const uint64_t ve = (vb + Q < T) ? vb + Q : T;
-  if (threadIdx.x == 0) {
-    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
-    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
-  }
+  if (threadIdx.x < WAVE) seg_range_wave(in.prefix, in.nseg, vb, ve, T, s_seg);
   __syncthreads();
   const uint32_t slo = s_seg[0], shi = s_seg[1];
   uint64_t out_n = 0;  // survivors written so far by this block
@@ -717,10 +754,7 @@ GHS_STREAM_KERNEL_6 void k_seed_runs(const uint32_t *__restrict__ src, const uin
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
   const uint64_t vb = Q * blockIdx.x;
   const uint64_t ve = (vb + Q < T) ? vb + Q : T;
-  if (threadIdx.x == 0) {
-    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
-    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
-  }
+  if (threadIdx.x < WAVE) seg_range_wave(in.prefix, in.nseg, vb, ve, T, s_seg);
   __syncthreads();
   const uint32_t slo = s_seg[0], shi = s_seg[1];
   uint64_t ph = tile_phys(in, slo, shi, vb + (uint64_t)threadIdx.x * 4, ve);
@@ -978,10 +1012,7 @@ GHS_STREAM_KERNEL_6 void k_win(const uint32_t *__restrict__ src, const uint32_t 
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
   const uint64_t vb = Q * blockIdx.x;
   const uint64_t ve = (vb + Q < T) ? vb + Q : T;
-  if (threadIdx.x == 0) {
-    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
-    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
-  }
+  if (threadIdx.x < WAVE) seg_range_wave(in.prefix, in.nseg, vb, ve, T, s_seg);
   __syncthreads();
   const uint32_t slo = s_seg[0], shi = s_seg[1];
   unsigned long long wsum = 0, cnt = 0;
@@ -1998,10 +2029,7 @@ GHS_STREAM_KERNEL_6 void k_level_pass(const uint32_t *__restrict__ ru, const uin
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
   const uint64_t vb = Q * blockIdx.x;
   const uint64_t ve = (vb + Q < T) ? vb + Q : T;
-  if (threadIdx.x == 0) {
-    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
-    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
-  }
+  if (threadIdx.x < WAVE) seg_range_wave(in.prefix, in.nseg, vb, ve, T, s_seg);
   __syncthreads();
   const uint32_t slo = s_seg[0], shi = s_seg[1];
   // regions hold multiples of 4 entries and start at multiples of 4, so a lane's 4-entry tile
@@ -2262,10 +2290,7 @@ __global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ sr
   const uint64_t vb = Q * blockIdx.x;
   const uint64_t ve = (vb + Q < T) ? vb + Q : T;
   for (uint32_t i = threadIdx.x; i <= nb; i += BK_T) s_h[i] = 0;
-  if (threadIdx.x == 0) {
-    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
-    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
-  }
+  if (threadIdx.x < WAVE) seg_range_wave(in.prefix, in.nseg, vb, ve, T, s_seg);
   __syncthreads();
   const uint32_t slo = s_seg[0], shi = s_seg[1];
   // pass A: records per bucket (the a and b ends only); every lane of a wave iterates while the
@@ -2641,10 +2666,7 @@ __global__ __launch_bounds__(BM_T) void k_wmin(const uint32_t *__restrict__ src,
     bucket_ident<BS>(t, par, best, n);
     return;
   }
-  if (threadIdx.x == 0) {
-    s_seg[0] = seg_find(in.prefix, 0, in.nseg - 1, wlo);
-    s_seg[1] = seg_find(in.prefix, 0, in.nseg - 1, whi - 1);
-  }
+  if (threadIdx.x < WAVE) seg_range_wave(in.prefix, in.nseg, wlo, whi, whi, s_seg);
   for (uint32_t i = threadIdx.x; i < SPAN; i += BM_T) s_min[i] = KEY_NONE;
   __syncthreads();
   const uint32_t slo = s_seg[0], shi = s_seg[1];
@@ -2825,10 +2847,7 @@ __global__ __launch_bounds__(BLOCK) void k_relabel_dense(uint32_t *__restrict__ 
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
   const uint64_t vb = Q * blockIdx.x;
   const uint64_t ve = (vb + Q < T) ? vb + Q : T;
-  if (threadIdx.x == 0) {
-    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
-    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
-  }
+  if (threadIdx.x < WAVE) seg_range_wave(in.prefix, in.nseg, vb, ve, T, s_seg);
   __syncthreads();
   const uint32_t slo = s_seg[0], shi = s_seg[1];
   for (uint64_t v = vb + (uint64_t)threadIdx.x * 4; v < ve; v += ARCS_PER_BLOCK) {
@@ -3191,32 +3210,39 @@ __global__ __launch_bounds__(BLOCK) void k_select_lb(const uint8_t *__restrict__
 // INITIATE exchanges of a level, ghs_implementation.py:235-387 — run without any global atomic and
 // without n-sized arrays: the fragments get dense ids 0..F0-1 (their order in the active list),
 // every edge is relabelled ONCE to the dense pair of its fragments, and each later round keeps
-// every fragment's minimum in LDS per block.
+// every root's minimum in LDS per block.
 //   k_tail_map    dmap[act[i]] = i; the tail's control block, R = identity, the root list
-//   k_tail_open   (round 0 of the tail) every live edge: a, b -> lab -> dmap (its dense fragments);
-//                 intra-fragment edges dropped, the rest compacted to the block's region of the
-//                 tail buffer as one 12-byte record (da | db << 16, key); each end's candidate
-//                 min'ed into the block's LDS minima; the block's minima -> its row of `partial`
-//   k_tail_hook   one slot per active root: the minimum over the blocks' rows, and its CONNECT
-//                 target (the edge's canonical ends -> their fragments at the tail's start ->
-//                 their dense roots now); MSF flag of the edge
-//   k_tail_round  every block first applies the hooks in LDS (mutual pairs keep the smaller root,
-//                 pointer jumping, R[d] = dense root of every dense id, the next active roots) —
-//                 the same result in every block, no grid barrier — then streams its records
-//                 (a candidate only where R[da] != R[db]) into its LDS minima and row. A round that
+//   k_tail_open   (round 0 of the tail) every live edge: a, b -> dmap (its dense fragments);
+//                 intra-fragment edges dropped, the rest compacted in order to the block's region of
+//                 the tail buffer as one 12-byte record (da | db << 16, key); each end's candidate
+//                 min'ed into the block's LDS minima; the block's row: each minimum's key and other end
+//   k_tail_hook   one slot per active root: the minimum over the blocks' rows and its other end
+//                 (the CONNECT target), the MSF flag of the edge
+//   k_tail_round  every block applies the last round's hooks in LDS — over the ROOTS only: mutual
+//                 pairs keep the smaller root, pointer jumping among the roots, then every dense id's
+//                 root through one lookup (R[d] = P[R[d]]), the next root list — identically in every
+//                 block (no grid barrier: the launch boundaries order open -> hook -> round -> hook,
+//                 so ranks sharing a device cannot deadlock it), then streams its records (a
+//                 candidate only where R[da] != R[db]) into its LDS minima and row. A round that
 //                 starts with <= 1 active root finishes the level instead: lab of every fragment of
 //                 the level = its final root, the round report.
+// The LDS minima carry (w << 32 | the record's index in the block's region) instead of the key:
+// a block's region holds its records in canonical (eid) order — a level's live edges keep the
+// canonical order within and across their regions (k_select / k_filter / k_level_pass emit it,
+// every compaction keeps it) and the open compacts in order — so within a block that order IS the
+// (w, eid) order, and each minimum's record is one load away: its true key for the row and its
+// other end. (Round 4's hook found the other end through the canonical list and the label chains,
+// and its prologue jumped pointers over all F0 dense ids.)
 // Per round: one stream of the 12-byte records + two launch boundaries, instead of the round
 // kernels' relabel gathers, LDS-cache misses to best[], hook, jump and select over n-sized arrays.
-// No grid barrier: a launch boundary orders A -> B -> A (so no co-residency assumption: ranks
-// sharing the device, e.g. ghs_mst_emulated, cannot deadlock it).
 // ------------------------------------------------------------------------------------------
 constexpr uint32_t TAIL_MAX = 12288;        // dense fragments: LDS minima 96 KiB + 2 x 24 KiB of u16 tables
 constexpr uint32_t TAIL_T = 1024;           // threads of the streaming tail kernels (16 waves, 1 block per CU)
 constexpr uint32_t TAIL_G = 256;            // their blocks = rows of `partial`
 constexpr uint32_t TAIL_ROUNDS_MAX = 32;    // a tail round at least halves the roots: <= 14 rounds
 constexpr uint32_t TAIL_HS = 16;            // k_tail_hook: slots per 256-thread block (16 row groups)
-static_assert(TAIL_MAX <= 65536, "dense ids are packed as 16-bit pairs");
+constexpr uint16_t TAIL_NONE = 0xffffu;     // a row's other end where the block has no candidate
+static_assert(TAIL_MAX <= 32768, "dense ids are packed as 16-bit pairs");
 
 struct TailCtl {
   uint32_t F0;        // dense fragments (the active list at the tail's start)
@@ -3232,7 +3258,8 @@ struct TailCtl {
 struct TailBufs {
   TailCtl *ctl;
   uint32_t *dmap;      // root label -> dense id (n entries; only the tail's roots are meaningful)
-  uint64_t *partial;   // TAIL_G rows x TAIL_MAX block minima
+  uint64_t *partial;   // TAIL_G rows x TAIL_MAX block minima (root-list order)
+  uint16_t *poth;      // ... and each minimum's other end (dense root id at the time of the stream)
   uint32_t *R[2];      // dense id -> dense root during round r: R[r & 1]
   uint32_t *droot[2];  // round r's active roots (ascending dense ids): droot[r & 1]
   uint32_t *ghook;     // per dense root: CONNECT target (dense root) of its minimum edge
@@ -3274,26 +3301,52 @@ __global__ void k_tail_labels(const uint32_t *__restrict__ prev, const unsigned 
   }
 }
 
-// a wave's survivors staged in LDS for coalesced stores (12-byte records)
-struct TailStage {
-  uint32_t p[WAVE * 4];
-  uint64_t k[WAVE * 4];
-};
-
-// the block's LDS minima -> its row of `partial` (one entry per active root, in root-list order)
-__device__ __forceinline__ void tail_row(const unsigned long long *s_best, const uint16_t *s_root, uint32_t nroot,
-                                         uint64_t *__restrict__ row) {
-  for (uint32_t i = threadIdx.x; i < nroot; i += blockDim.x) row[i] = s_best[s_root[i]];
-}
-
 __device__ __forceinline__ void lds_min_u64(unsigned long long *s, uint32_t i, uint64_t k) {
   if (k < s[i]) atomicMin(&s[i], (unsigned long long)k);  // a plain read first: slots only decrease
+}
+
+// a block-local candidate: the key's weight with the record's index in the block's region (the
+// region is in eid order, so this orders the block's candidates exactly as (w, eid))
+__device__ __forceinline__ uint64_t tail_local(uint64_t key, uint32_t idx) { return (key & ~0xffffffffull) | idx; }
+
+// The block's row (root-list order: root i of the round = droots[i]): each root's minimum
+// record (one load: its index is in the LDS minimum) gives the true key and the other end's dense
+// root (through R: rmap == nullptr is the identity, the open). Every record load in flight first.
+__device__ __forceinline__ void tail_row_out(const TailBufs tb, const unsigned long long *s_best, const uint16_t *droots,
+                                             uint32_t nroot, const uint32_t *__restrict__ pr, const uint64_t *__restrict__ pk,
+                                             const uint16_t *rmap) {
+  constexpr uint32_t PER = TAIL_MAX / TAIL_T;
+  uint64_t *row = tb.partial + (uint64_t)blockIdx.x * TAIL_MAX;
+  uint16_t *orow = tb.poth + (uint64_t)blockIdx.x * TAIL_MAX;
+  uint32_t p[PER], d[PER];
+  uint64_t k[PER];
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q) {
+    const uint32_t i = threadIdx.x + q * TAIL_T;
+    d[q] = i < nroot ? (droots ? droots[i] : i) : 0u;
+    const uint64_t v = i < nroot ? s_best[d[q]] : KEY_NONE;
+    const bool has = v != KEY_NONE;
+    p[q] = has ? pr[(uint32_t)v] : 0u;
+    k[q] = has ? pk[(uint32_t)v] : KEY_NONE;
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q) {
+    const uint32_t i = threadIdx.x + q * TAIL_T;
+    if (i >= nroot) break;
+    uint16_t o = TAIL_NONE;
+    if (k[q] != KEY_NONE) {
+      const uint32_t da = p[q] & 0xffffu, db = p[q] >> 16;
+      const uint32_t ra = rmap ? rmap[da] : da, rb = rmap ? rmap[db] : db;
+      o = (uint16_t)(ra == d[q] ? rb : ra);
+    }
+    row[i] = k[q];
+    orow[i] = o;
+  }
 }
 
 __global__ __launch_bounds__(TAIL_T) void k_tail_open(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
                                                       const uint64_t *__restrict__ key, SegView in, TailBufs tb) {
   __shared__ unsigned long long s_best[TAIL_MAX];
-  __shared__ TailStage s_stage[TAIL_T / WAVE];
   __shared__ uint32_t s_wcnt[TAIL_T / WAVE];
   __shared__ uint32_t s_seg[2];
   __shared__ uint32_t s_live;
@@ -3303,18 +3356,17 @@ __global__ __launch_bounds__(TAIL_T) void k_tail_open(const uint32_t *__restrict
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
   const uint64_t vb = Q * blockIdx.x;
   const uint64_t ve = (vb + Q < T) ? vb + Q : T;
+  if (threadIdx.x < WAVE) seg_range_wave(in.prefix, in.nseg, vb, ve, T, s_seg);
   if (threadIdx.x == 0) {
-    s_seg[0] = vb < T ? seg_find(in.prefix, 0, in.nseg - 1, vb) : 0;
-    s_seg[1] = ve > vb ? seg_find(in.prefix, 0, in.nseg - 1, ve - 1) : 0;
     s_live = 0;
     if (blockIdx.x == 0) tb.ctl->Q = Q;
   }
   __syncthreads();
   const uint32_t slo = s_seg[0], shi = s_seg[1];
-  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+  uint32_t *orec = tb.rec + vb;
+  uint64_t *okey = tb.rkey + vb;
   constexpr uint64_t STEP = (uint64_t)TAIL_T * 4;
-  uint64_t out_n = 0;
-  uint32_t live_n = 0;
+  uint32_t out_n = 0, live_n = 0;
   for (uint64_t v0 = vb; v0 < ve; v0 += STEP) {
     const uint64_t v = v0 + (uint64_t)threadIdx.x * 4;
     const bool in_range = v < ve;
@@ -3332,60 +3384,47 @@ __global__ __launch_bounds__(TAIL_T) void k_tail_open(const uint32_t *__restrict
       db[j] = tb.dmap[valid ? B[j] : 0u];
       mask |= (valid & (da[j] != db[j])) ? (1u << j) : 0u;
     }
-    uint32_t P[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (!((mask >> j) & 1u)) continue;
-      if (da[j] >= F || db[j] >= F) {  // a live edge must join two active fragments
+    for (int j = 0; j < 4; ++j)
+      if (((mask >> j) & 1u) && (da[j] >= F || db[j] >= F)) {  // a live edge must join two active fragments
         atomicOr(&tb.ctl->err, 1u);
         mask &= ~(1u << j);
-        continue;
       }
-      lds_min_u64(s_best, da[j], K[j]);
-      lds_min_u64(s_best, db[j], K[j]);
-      P[j] = da[j] | (db[j] << 16);
-    }
     live_n += __popc(mask);
-    // survivors -> this block's region of the tail buffer [vb, vb + Q), staged per wave
+    // survivors -> this block's region of the tail buffer, in order; their candidates carry their index
     uint32_t lane_excl, wave_before, wave_cnt, total;
     block_offsets_w<TAIL_T>((uint32_t)__popc(mask), s_wcnt, &lane_excl, &wave_before, &wave_cnt, &total);
-    TailStage &ws = s_stage[wid];
-    uint32_t p = lane_excl;
+    uint32_t o = out_n + wave_before + lane_excl;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       if ((mask >> j) & 1u) {
-        ws.p[p] = P[j];
-        ws.k[p] = K[j];
-        ++p;
+        orec[o] = da[j] | (db[j] << 16);
+        okey[o] = K[j];
+        const uint64_t c = tail_local(K[j], o);
+        lds_min_u64(s_best, da[j], c);
+        lds_min_u64(s_best, db[j], c);
+        ++o;
       }
-    wave_sync_lds();
-    const uint64_t o = vb + out_n + wave_before;
-    for (uint32_t i = lane; i < wave_cnt; i += WAVE) {
-      tb.rec[o + i] = ws.p[i];
-      tb.rkey[o + i] = ws.k[i];
-    }
-    wave_sync_lds();
     out_n += total;
   }
   for (int d = WAVE / 2; d > 0; d >>= 1) live_n += __shfl_xor(live_n, d);
-  if (lane == 0) atomicAdd(&s_live, live_n);
-  __syncthreads();
+  if ((threadIdx.x & (WAVE - 1)) == 0) atomicAdd(&s_live, live_n);
+  __syncthreads();  // every wave's record stores drained: the row reads them back through L2
   // the block's minima of every dense fragment (round 0: the root list is the identity)
-  uint64_t *row = tb.partial + (uint64_t)blockIdx.x * TAIL_MAX;
-  for (uint32_t i = threadIdx.x; i < F; i += TAIL_T) row[i] = s_best[i];
+  tail_row_out(tb, s_best, nullptr, F, orec, okey, nullptr);
   if (threadIdx.x == 0) {
-    tb.bcnt[blockIdx.x] = (uint32_t)out_n;
+    tb.bcnt[blockIdx.x] = out_n;
     tb.blive[blockIdx.x] = s_live;
   }
 }
 
-// One active root per slot (root-list order): the blocks' minima reduced (16 row groups per slot),
-// the root's CONNECT target, its MSF flag. Block 0 also totals the streamed round's live edges.
-__global__ __launch_bounds__(256) void k_tail_hook(TailBufs tb, uint32_t r, const uint32_t *__restrict__ act0,
-                                                   const uint32_t *__restrict__ lab, const uint32_t *__restrict__ eu,
-                                                   const uint32_t *__restrict__ ev, uint8_t *__restrict__ in_mst,
+// One active root per slot (root-list order): the blocks' minima reduced (16 row groups per slot)
+// with their other ends, the root's CONNECT target, its MSF flag. Block 0 also totals the
+// streamed round's live edges.
+__global__ __launch_bounds__(256) void k_tail_hook(TailBufs tb, uint32_t r, uint8_t *__restrict__ in_mst,
                                                    uint32_t nblocks, unsigned long long *__restrict__ err) {
   __shared__ unsigned long long s_part[256];
+  __shared__ uint32_t s_prow[256];
   TailCtl *c = tb.ctl;
   if (c->done) return;  // r: the round just streamed
   const uint32_t nroot = (uint32_t)c->nroots[r];
@@ -3398,9 +3437,10 @@ __global__ __launch_bounds__(256) void k_tail_hook(TailBufs tb, uint32_t r, cons
   const uint32_t s = threadIdx.x % TAIL_HS, g = threadIdx.x / TAIL_HS;  // slot, row group
   const uint32_t i = blockIdx.x * TAIL_HS + s;
   if (blockIdx.x * TAIL_HS >= nroot) return;  // block-uniform
+  constexpr uint32_t GROUPS = 256 / TAIL_HS;
   uint64_t m = KEY_NONE;
+  uint32_t w = 0;
   if (i < nroot) {
-    constexpr uint32_t GROUPS = 256 / TAIL_HS;
     uint64_t x[TAIL_G / GROUPS];
 #pragma unroll
     for (uint32_t k = 0; k < TAIL_G / GROUPS; ++k) {
@@ -3408,37 +3448,41 @@ __global__ __launch_bounds__(256) void k_tail_hook(TailBufs tb, uint32_t r, cons
       x[k] = b < nblocks ? tb.partial[(uint64_t)b * TAIL_MAX + i] : KEY_NONE;
     }
 #pragma unroll
-    for (uint32_t k = 0; k < TAIL_G / GROUPS; ++k) m = umin64(m, x[k]);
+    for (uint32_t k = 0; k < TAIL_G / GROUPS; ++k)
+      if (x[k] < m) {
+        m = x[k];
+        w = g + k * GROUPS;
+      }
   }
   s_part[threadIdx.x] = m;
+  s_prow[threadIdx.x] = w;
   __syncthreads();
   if (g != 0 || i >= nroot) return;
-  for (uint32_t k = 1; k < 256 / TAIL_HS; ++k) m = umin64(m, s_part[k * TAIL_HS + s]);
+  for (uint32_t k = 1; k < GROUPS; ++k) {
+    const uint64_t x = s_part[k * TAIL_HS + s];
+    if (x < m) {
+      m = x;
+      w = s_prow[k * TAIL_HS + s];
+    }
+  }
   const uint32_t d = tb.droot[r & 1][i];
-  const uint32_t *R = tb.R[r & 1];
-  const uint32_t F = c->F0;
   uint32_t o = LABEL_NONE;
   if (m != KEY_NONE) {
-    // the minimum edge's ends -> their fragments at the tail's start -> dense ids -> dense roots now
-    const uint32_t eid = (uint32_t)m;
-    const uint32_t fa = find_lab(lab, eu[eid], err), fb = find_lab(lab, ev[eid], err);
-    const uint32_t xa = tb.dmap[fa], xb = tb.dmap[fb];
-    if (xa >= F || xb >= F || act0[xa] != fa || act0[xb] != fb) {
-      atomicOr(err, 2ull);  // the ends' fragments must be the tail's
+    o = tb.poth[(uint64_t)w * TAIL_MAX + i];
+    if (o >= c->F0 || o == d) {  // the minimum edge must leave root d towards another root
+      atomicOr(err, 2ull);
+      o = LABEL_NONE;
       m = KEY_NONE;
     } else {
-      const uint32_t ra = R[xa], rb = R[xb];
-      if (ra != d && rb != d) atomicOr(err, 2ull);  // the chosen edge must leave d
-      o = ra == d ? rb : ra;
-      in_mst[eid] = 1;  // both members of a mutual pair mark the same edge
+      in_mst[(uint32_t)m] = 1;  // both members of a mutual pair mark the same edge
     }
   }
   tb.gkey[d] = m;
   tb.ghook[d] = o;
 }
 
-// Every block applies the last round's hooks (identical LDS computation in every block), then
-// streams its records — or, when <= 1 root stays active, block 0 finishes the level.
+// Every block applies the last round's hooks (identical LDS computation in every block, over the
+// roots only), then streams its records — or, when <= 1 root stays active, block 0 finishes the level.
 __global__ __launch_bounds__(TAIL_T) void k_tail_round(TailBufs tb, uint32_t r, const uint32_t *__restrict__ act0,
                                                        uint32_t *__restrict__ lab, unsigned long long *__restrict__ cnt,
                                                        unsigned long long *__restrict__ err) {
@@ -3453,67 +3497,103 @@ __global__ __launch_bounds__(TAIL_T) void k_tail_round(TailBufs tb, uint32_t r, 
   const uint32_t F = c->F0;  // r: the round about to stream (round r - 1 hooked last)
   const uint32_t nprev = (uint32_t)c->nroots[r - 1];
   const uint32_t *prev = tb.droot[(r - 1) & 1];
-  uint32_t *P = reinterpret_cast<uint32_t *>(s_best);  // dense pointer forest (prologue only)
+  uint32_t *P = reinterpret_cast<uint32_t *>(s_best);  // dense pointer forest over the roots (prologue only)
   constexpr uint32_t MARK = 0x80000000u;
   if (threadIdx.x == 0) {
     s_tw = 0;
     s_tc = 0;
     s_live = 0;
   }
-  for (uint32_t d = threadIdx.x; d < F; d += TAIL_T) {
-    P[d] = d;
-    s_R[d] = (uint16_t)tb.R[(r - 1) & 1][d];
+  // every global load of the prologue first: the dense ids' roots, the roots' hooks and keys
+  constexpr uint32_t PER = TAIL_MAX / TAIL_T;
+  const uint32_t *Rp = tb.R[(r - 1) & 1];
+  uint32_t rr[PER], pd[PER], ph[PER];
+  uint64_t pk[PER];
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q) {
+    const uint32_t d = threadIdx.x + q * TAIL_T, i = d;
+    rr[q] = d < F ? Rp[d] : 0u;
+    pd[q] = i < nprev ? prev[i] : 0u;
   }
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q) {
+    const uint32_t i = threadIdx.x + q * TAIL_T;
+    ph[q] = i < nprev ? tb.ghook[pd[q]] : LABEL_NONE;
+    pk[q] = i < nprev ? tb.gkey[pd[q]] : KEY_NONE;
+  }
+  // every dense id a root of itself (an inactive root of round r - 1 stays one), then the hooks of
+  // round r - 1's active roots
+  for (uint32_t d = threadIdx.x; d < F; d += TAIL_T) P[d] = d;
   __syncthreads();
-  // the hooks of round r - 1's active roots
-  for (uint32_t i = threadIdx.x; i < nprev; i += TAIL_T) {
-    const uint32_t d = prev[i], o = tb.ghook[d];
-    if (o != LABEL_NONE) P[d] = o;
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q) {
+    const uint32_t i = threadIdx.x + q * TAIL_T;
+    if (i < nprev && ph[q] != LABEL_NONE) P[pd[q]] = ph[q];
   }
   __syncthreads();
   // a mutual pair (d <-> o over their shared minimum) keeps its smaller member as the root
-  for (uint32_t i = threadIdx.x; i < nprev; i += TAIL_T) {
-    const uint32_t d = prev[i], o = P[d] & ~MARK;
-    if (o != d && (P[o] & ~MARK) == d && d < o) atomicOr(&P[d], MARK);
-  }
-  __syncthreads();
-  unsigned long long tw = 0, tc = 0;
-  for (uint32_t i = threadIdx.x; i < nprev; i += TAIL_T) {
-    const uint32_t d = prev[i];
-    if (P[d] & MARK) {
-      P[d] = d;
-    } else if (P[d] != d) {  // d hooked: one MSF edge
-      tw += tb.gkey[d] >> 32;
-      tc += 1;
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q) {
+    const uint32_t i = threadIdx.x + q * TAIL_T;
+    if (i < nprev) {
+      const uint32_t d = pd[q], o = P[d] & ~MARK;
+      if (o != d && (P[o] & ~MARK) == d && d < o) atomicOr(&P[d], MARK);
     }
   }
   __syncthreads();
-  for (int it = 0; it < 32; ++it) {  // pointer jumping to the roots
+  unsigned long long tw = 0, tc = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q) {
+    const uint32_t i = threadIdx.x + q * TAIL_T;
+    if (i < nprev) {
+      const uint32_t d = pd[q];
+      if (P[d] & MARK) {
+        P[d] = d;
+      } else if (P[d] != d) {  // d hooked: one MSF edge
+        tw += pk[q] >> 32;
+        tc += 1;
+      }
+    }
+  }
+  __syncthreads();
+  for (int it = 0; it < 32; ++it) {  // pointer jumping among the roots (a hook targets a root)
     int more = 0;
-    for (uint32_t d = threadIdx.x; d < F; d += TAIL_T) {
-      const uint32_t p = P[d], pp = P[p];
-      if (pp != p) {
-        P[d] = pp;
-        more = 1;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+      const uint32_t i = threadIdx.x + q * TAIL_T;
+      if (i < nprev) {
+        const uint32_t d = pd[q], p = P[d], pp = P[p];
+        if (pp != p) {
+          P[d] = pp;
+          more = 1;
+        }
       }
     }
     if (!__syncthreads_or(more)) break;
   }
-  for (uint32_t d = threadIdx.x; d < F; d += TAIL_T) s_R[d] = (uint16_t)P[s_R[d]];
+  // every dense id's root: its round r - 1 root's final root (a root that was not active keeps itself)
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q) {
+    const uint32_t d = threadIdx.x + q * TAIL_T;
+    if (d < F) s_R[d] = (uint16_t)P[rr[q]];
+  }
   // next roots: round r - 1's roots that had an edge and stayed roots (ascending: a block scan)
+  uint32_t keep = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q) {
+    const uint32_t i = threadIdx.x + q * TAIL_T;
+    if (i < nprev && pk[q] != KEY_NONE && P[pd[q]] == pd[q]) keep |= 1u << q;
+  }
   uint32_t nroot = 0;
-  for (uint32_t base = 0; base < nprev; base += TAIL_T) {
-    const uint32_t i = base + threadIdx.x;
-    uint32_t d = 0;
-    bool keep = false;
-    if (i < nprev) {
-      d = prev[i];
-      keep = tb.gkey[d] != KEY_NONE && P[d] == d;
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q) {  // root-list order = prev order (chunks of TAIL_T)
+    if (q * TAIL_T < nprev) {  // block-uniform
+      uint32_t tot;
+      const uint32_t k = (keep >> q) & 1u;
+      const uint32_t before = block_excl_scan<TAIL_T>(k, s_wsum, &tot);
+      if (k) s_root[nroot + before] = (uint16_t)pd[q];
+      nroot += tot;
     }
-    uint32_t tot;
-    const uint32_t before = block_excl_scan<TAIL_T>(keep ? 1u : 0u, s_wsum, &tot);
-    if (keep) s_root[nroot + before] = (uint16_t)d;
-    nroot += tot;
   }
   for (int dd = WAVE / 2; dd > 0; dd >>= 1) {
     tw += __shfl_xor(tw, dd);
@@ -3535,9 +3615,17 @@ __global__ __launch_bounds__(TAIL_T) void k_tail_round(TailBufs tb, uint32_t r, 
     }
     if (nroot <= 1 || r >= TAIL_ROUNDS_MAX) {
       // the level is complete: every fragment of the level takes its final root's label
-      for (uint32_t d = threadIdx.x; d < F; d += TAIL_T) {
-        const uint32_t x = act0[d], root = act0[s_R[d]];
-        if (root != x) lab[x] = root;
+      uint32_t xs[PER], roots[PER];
+#pragma unroll
+      for (uint32_t q = 0; q < PER; ++q) {  // every gather in flight, then the stores
+        const uint32_t d = threadIdx.x + q * TAIL_T;
+        xs[q] = d < F ? act0[d] : 0u;
+        roots[q] = d < F ? act0[s_R[d]] : 0u;
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t d = threadIdx.x + q * TAIL_T;
+        if (d < F && roots[q] != xs[q]) lab[xs[q]] = roots[q];
       }
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -3555,26 +3643,26 @@ __global__ __launch_bounds__(TAIL_T) void k_tail_round(TailBufs tb, uint32_t r, 
   }
   if (nroot <= 1 || r >= TAIL_ROUNDS_MAX) return;  // block 0 finishes the level
   // stream this block's records into the LDS minima of the current roots
-  for (uint32_t d = threadIdx.x; d < F; d += TAIL_T) s_best[d] = KEY_NONE;
+  for (uint32_t i = threadIdx.x; i < nroot; i += TAIL_T) s_best[s_root[i]] = KEY_NONE;
   __syncthreads();
   const uint64_t base = c->Q * blockIdx.x;
   const uint32_t n = tb.bcnt[blockIdx.x];
+  const uint32_t *pr = tb.rec + base;
+  const uint64_t *prk = tb.rkey + base;
   uint32_t live_n = 0;
   for (uint32_t e0 = threadIdx.x * 4; e0 < n; e0 += TAIL_T * 4) {
-    const uint32_t *pr = tb.rec + base + e0;
-    const uint64_t *pk = tb.rkey + base + e0;
     uint32_t p[4];
     uint64_t k[4];
-    if (e0 + 4 <= n) {  // base is a multiple of 4: 16-B aligned
-      const uint4 q = *reinterpret_cast<const uint4 *>(pr);
-      const ulonglong2 k01 = *reinterpret_cast<const ulonglong2 *>(pk), k23 = *reinterpret_cast<const ulonglong2 *>(pk + 2);
-      p[0] = q.x; p[1] = q.y; p[2] = q.z; p[3] = q.w;
+    if (e0 + 4 <= n) {  // a region starts at a multiple of 4: 16-B aligned
+      const uint4 qv = *reinterpret_cast<const uint4 *>(pr + e0);
+      const ulonglong2 k01 = *reinterpret_cast<const ulonglong2 *>(prk + e0), k23 = *reinterpret_cast<const ulonglong2 *>(prk + e0 + 2);
+      p[0] = qv.x; p[1] = qv.y; p[2] = qv.z; p[3] = qv.w;
       k[0] = k01.x; k[1] = k01.y; k[2] = k23.x; k[3] = k23.y;
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        p[j] = e0 + j < n ? pr[j] : 0u;
-        k[j] = e0 + j < n ? pk[j] : KEY_NONE;
+        p[j] = e0 + j < n ? pr[e0 + j] : 0u;
+        k[j] = e0 + j < n ? prk[e0 + j] : KEY_NONE;
       }
     }
 #pragma unroll
@@ -3583,14 +3671,15 @@ __global__ __launch_bounds__(TAIL_T) void k_tail_round(TailBufs tb, uint32_t r, 
       const uint32_t ra = s_R[p[j] & 0xffffu], rb = s_R[p[j] >> 16];
       if (ra == rb) continue;
       ++live_n;
-      lds_min_u64(s_best, ra, k[j]);
-      lds_min_u64(s_best, rb, k[j]);
+      const uint64_t cand = tail_local(k[j], e0 + j);
+      lds_min_u64(s_best, ra, cand);
+      lds_min_u64(s_best, rb, cand);
     }
   }
   for (int dd = WAVE / 2; dd > 0; dd >>= 1) live_n += __shfl_xor(live_n, dd);
   if ((threadIdx.x & (WAVE - 1)) == 0) atomicAdd(&s_live, live_n);
   __syncthreads();
-  tail_row(s_best, s_root, nroot, tb.partial + (uint64_t)blockIdx.x * TAIL_MAX);
+  tail_row_out(tb, s_best, s_root, nroot, pr, prk, s_R);
   if (threadIdx.x == 0) tb.blive[blockIdx.x] = s_live;
 }
 
@@ -4054,6 +4143,7 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
   if (local_edges == m) {  // one rank: the LDS tail's arrays (its records go to the idle edge buffer)
     p = carve(N * 4); if (s) s->tail.dmap = (uint32_t *)p;
     p = carve((size_t)TAIL_G * TAIL_MAX * 8); if (s) s->tail.partial = (uint64_t *)p;
+    p = carve((size_t)TAIL_G * TAIL_MAX * 2); if (s) s->tail.poth = (uint16_t *)p;
     for (int b = 0; b < 2; ++b) {
       p = carve(TAIL_MAX * 4); if (s) s->tail.R[b] = (uint32_t *)p;
       p = carve(TAIL_MAX * 4); if (s) s->tail.droot[b] = (uint32_t *)p;
@@ -4914,7 +5004,7 @@ static int run_tail(ghs_solver *s, uint64_t prev_in) {
   hipStream_t st = s->stream;
   TailBufs tb = s->tail;
   const ArcBuf &I = s->buf[s->cur], &O = s->buf[s->cur ^ 1];
-  tb.rec = O.src;   // the idle edge buffer holds the tail's records
+  tb.rec = O.src;  // the idle edge buffer holds the tail's records
   tb.rkey = O.key;
   if (s->scan_pending) flush_scan(s);
   const uint32_t *act0 = s->act[s->act_cur];
@@ -4938,7 +5028,7 @@ static int run_tail(ghs_solver *s, uint64_t prev_in) {
   }
   {
     KT(GHS_K_TAIL_HOOK, F0);
-    k_tail_hook<<<hook_g, 256, 0, st>>>(tb, 0, act0, s->lab, s->eu, s->ev, s->in_mst, TAIL_G, err);
+    k_tail_hook<<<hook_g, 256, 0, st>>>(tb, 0, s->in_mst, TAIL_G, err);
   }
   GHS_HIP_CHECK(hipGetLastError());
   uint32_t r = 1;  // the next tail round to stream
@@ -4954,7 +5044,7 @@ static int run_tail(ghs_solver *s, uint64_t prev_in) {
       }
       if (r < TAIL_ROUNDS_MAX) {
         KT(GHS_K_TAIL_HOOK, 0);
-        k_tail_hook<<<hook_g, 256, 0, st>>>(tb, r, act0, s->lab, s->eu, s->ev, s->in_mst, TAIL_G, err);
+        k_tail_hook<<<hook_g, 256, 0, st>>>(tb, r, s->in_mst, TAIL_G, err);
       }
     }
     GHS_HIP_CHECK(hipGetLastError());
@@ -4986,6 +5076,7 @@ static int run_tail(ghs_solver *s, uint64_t prev_in) {
   close_level(s);
   return GHS_OK;
 }
+
 
 static int run_level_pipelined(ghs_solver *s) {
   if (!s->bucket_decided)
