@@ -3305,6 +3305,12 @@ __device__ __forceinline__ void lds_min_u64(unsigned long long *s, uint32_t i, u
   if (k < s[i]) atomicMin(&s[i], (unsigned long long)k);  // a plain read first: slots only decrease
 }
 
+// a wave's survivors staged in LDS for coalesced stores (12-byte records)
+struct TailStage {
+  uint32_t p[WAVE * 4];
+  uint64_t k[WAVE * 4];
+};
+
 // a block-local candidate: the key's weight with the record's index in the block's region (the
 // region is in eid order, so this orders the block's candidates exactly as (w, eid))
 __device__ __forceinline__ uint64_t tail_local(uint64_t key, uint32_t idx) { return (key & ~0xffffffffull) | idx; }
@@ -3347,6 +3353,7 @@ __device__ __forceinline__ void tail_row_out(const TailBufs tb, const unsigned l
 __global__ __launch_bounds__(TAIL_T) void k_tail_open(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
                                                       const uint64_t *__restrict__ key, SegView in, TailBufs tb) {
   __shared__ unsigned long long s_best[TAIL_MAX];
+  __shared__ TailStage s_stage[TAIL_T / WAVE];
   __shared__ uint32_t s_wcnt[TAIL_T / WAVE];
   __shared__ uint32_t s_seg[2];
   __shared__ uint32_t s_live;
@@ -3363,6 +3370,7 @@ __global__ __launch_bounds__(TAIL_T) void k_tail_open(const uint32_t *__restrict
   }
   __syncthreads();
   const uint32_t slo = s_seg[0], shi = s_seg[1];
+  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
   uint32_t *orec = tb.rec + vb;
   uint64_t *okey = tb.rkey + vb;
   constexpr uint64_t STEP = (uint64_t)TAIL_T * 4;
@@ -3394,17 +3402,24 @@ __global__ __launch_bounds__(TAIL_T) void k_tail_open(const uint32_t *__restrict
     // survivors -> this block's region of the tail buffer, in order; their candidates carry their index
     uint32_t lane_excl, wave_before, wave_cnt, total;
     block_offsets_w<TAIL_T>((uint32_t)__popc(mask), s_wcnt, &lane_excl, &wave_before, &wave_cnt, &total);
-    uint32_t o = out_n + wave_before + lane_excl;
+    TailStage &ws = s_stage[wid];
+    uint32_t o = lane_excl;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       if ((mask >> j) & 1u) {
-        orec[o] = da[j] | (db[j] << 16);
-        okey[o] = K[j];
-        const uint64_t c = tail_local(K[j], o);
+        ws.p[o] = da[j] | (db[j] << 16);
+        ws.k[o] = K[j];
+        const uint64_t c = tail_local(K[j], out_n + wave_before + o);
         lds_min_u64(s_best, da[j], c);
         lds_min_u64(s_best, db[j], c);
         ++o;
       }
+    wave_sync_lds();  // the wave's records leave LDS as consecutive stores
+    for (uint32_t i = lane; i < wave_cnt; i += WAVE) {
+      orec[out_n + wave_before + i] = ws.p[i];
+      okey[out_n + wave_before + i] = ws.k[i];
+    }
+    wave_sync_lds();
     out_n += total;
   }
   for (int d = WAVE / 2; d > 0; d >>= 1) live_n += __shfl_xor(live_n, d);
