@@ -448,7 +448,13 @@ def time_steps(step, steps, warmup, world, dist):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    out = [step() for _ in range(steps)]
+    out = []
+    for i in range(steps):
+        ts = time.perf_counter()
+        out.append(step())
+        # a progress mark after a slow step only (N > 1 rehearsals over gloo: a minute per step)
+        if world > 1 and time.perf_counter() - ts > 5.0:
+            mark(dist.get_rank(), f"step {i + 1}/{steps} done ({time.perf_counter() - t0:.1f} s)")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -476,6 +482,9 @@ def profile_step(step, n):
 
 def main():
     args = parse()
+    if os.environ.get("GHS_BENCH_STACKS"):  # diagnostic: every rank's Python stacks every N seconds
+        import faulthandler
+        faulthandler.dump_traceback_later(int(os.environ["GHS_BENCH_STACKS"]), repeat=True)
     import torch
     import torch.distributed as dist
 
@@ -504,7 +513,7 @@ def run(args, world, rank, dist, dev):
     import torch
 
     from distributed_ghs_implementation_amd import _native
-    from distributed_ghs_implementation_amd.device import DeviceMST
+    from distributed_ghs_implementation_amd.device import DeviceMST, flags_to_eids
 
     def gen():
         # ranks sharing a GPU (a rehearsal) generate one after another: the radix sort's temporary
@@ -538,7 +547,7 @@ def run(args, world, rank, dist, dev):
                 return None
             r1 = DeviceMST(edges)
             rres, _ = r1.run()
-            eids = torch.nonzero(r1.in_mst[:m]).flatten().to(torch.int64).cpu()
+            eids = flags_to_eids(r1.in_mst, 0, m, min(m, n)).cpu()
             del r1
             torch.cuda.empty_cache()
             return rres.total_weight, rres.num_mst_edges, eids
@@ -574,7 +583,7 @@ def run(args, world, rank, dist, dev):
     if world > 1 and args.verify_ranks:
         # every rank must hold the same MSF: (weight, edges, checksum of the chosen eids)
         flags = eng.gather_in_mst()
-        chk = int((torch.nonzero(flags).flatten().to(torch.int64) % 1000003).sum().item())
+        chk = int((flags_to_eids(flags, 0, flags.numel(), min(flags.numel(), n)) % 1000003).sum().item())
         mine = torch.tensor([results[-1].total_weight, results[-1].num_mst_edges, chk], dtype=torch.int64)
         if args.backend == "nccl":
             mine = mine.cuda()

@@ -45,7 +45,7 @@ EXPORTED_SYMBOLS = (
     "ghs_rmat_temp_bytes", "ghs_rmat_generate", "ghs_rmat_tuples", "ghs_grid_generate",
     "ghs_profile_enable", "ghs_profile_read", "ghs_kernel_name",
     "ghs_comm_unique_id", "ghs_comm_init", "ghs_comm_destroy", "ghs_solver_run", "ghs_mst_emulated",
-    "ghs_release_cache", "ghs_slot_retries",
+    "ghs_release_cache", "ghs_slot_retries", "ghs_flags_to_eids",
 )
 
 
@@ -282,6 +282,7 @@ def load():
             "ghs_mst_emulated": (i32, [u32, u64, vp, vp, vp, i32, P(Config), vp, P(Result), P(RoundStats)]),
             "ghs_release_cache": (i32, []),
             "ghs_slot_retries": (i32, [P(u64)]),
+            "ghs_flags_to_eids": (i32, [vp, u64, u64, vp, u64, P(u64), vp]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(L, name)

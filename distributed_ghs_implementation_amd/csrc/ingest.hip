@@ -9,6 +9,12 @@
 // The CPU restatement of both generators (test infrastructure) is oracle/generators.c.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/device/device_reduce.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <mutex>
+#include <unordered_map>
 
 #include <string>
 
@@ -270,6 +276,73 @@ int ghs_rmat_generate(uint32_t scale, uint32_t edgefactor, uint64_t seed, uint64
   GHS_HIP_CHECK(hipMemcpyAsync(&cnt, nsel, 8, hipMemcpyDeviceToHost, st));
   GHS_HIP_CHECK(hipStreamSynchronize(st));
   *m_out = cnt;
+  return GHS_OK;
+}
+
+struct FlagOne {
+  __host__ __device__ uint32_t operator()(uint8_t f) const { return f ? 1u : 0u; }
+};
+
+// The MSF edge ids of a flag range (a rank's own range for collect_results,
+// ghs_implementation_mpi.py:760-779): rocPRIM's flagged select over a counting input. Its temporary
+// storage is kept per device (grown on demand); the count comes back through pinned memory.
+int ghs_flags_to_eids(const uint8_t *d_in_mst, uint64_t lo, uint64_t hi, uint32_t *d_eids, uint64_t capacity,
+                      uint64_t *count, void *stream) {
+  if (!count || (hi > lo && (!d_in_mst || !d_eids))) GHS_FAIL(GHS_E_ARG, "NULL pointer");
+  if (hi < lo || hi >= (1ull << 32)) GHS_FAIL(GHS_E_ARG, "bad range (need lo <= hi < 2^32)");
+  *count = 0;
+  if (hi == lo) return GHS_OK;
+  struct Temp {
+    void *p = nullptr;
+    size_t bytes = 0;
+    uint32_t *h_cnt = nullptr;  // pinned: the selected count
+    uint32_t *d_cnt = nullptr;
+  };
+  static std::mutex mu;
+  static std::unordered_map<int, Temp> temps;
+  std::lock_guard<std::mutex> lock(mu);
+  int dev = 0;
+  GHS_HIP_CHECK(hipGetDevice(&dev));
+  Temp &t = temps[dev];
+  hipStream_t st = (hipStream_t)stream;
+  const size_t N = (size_t)(hi - lo);
+  rocprim::counting_iterator<uint32_t> in((uint32_t)lo);
+  size_t need = 0;
+  GHS_HIP_CHECK(rocprim::select(nullptr, need, in, d_in_mst + lo, d_eids, (uint32_t *)nullptr, N, st));
+  if (!t.h_cnt) {
+    GHS_HIP_CHECK(hipHostMalloc((void **)&t.h_cnt, sizeof(uint32_t), hipHostMallocDefault));
+    GHS_HIP_CHECK(hipMalloc((void **)&t.d_cnt, sizeof(uint32_t)));
+  }
+  if (t.bytes < need) {
+    if (t.p) (void)hipFree(t.p);
+    t.p = nullptr;
+    t.bytes = 0;
+    GHS_HIP_CHECK(hipMalloc(&t.p, need));
+    t.bytes = need;
+  }
+  // the output holds at most `capacity` ids: when the range is longer, count the flags first
+  // (rocPRIM writes every selected id) and refuse the call instead of writing past it
+  if (N > capacity) {
+    auto ones = rocprim::make_transform_iterator(d_in_mst + lo, FlagOne());
+    size_t rneed = 0;
+    GHS_HIP_CHECK(rocprim::reduce(nullptr, rneed, ones, t.d_cnt, 0u, N, rocprim::plus<uint32_t>(), st));
+    if (rneed > need) need = rneed;
+    if (t.bytes < need) {
+      if (t.p) (void)hipFree(t.p);
+      t.p = nullptr;
+      t.bytes = 0;
+      GHS_HIP_CHECK(hipMalloc(&t.p, need));
+      t.bytes = need;
+    }
+    GHS_HIP_CHECK(rocprim::reduce(t.p, rneed, ones, t.d_cnt, 0u, N, rocprim::plus<uint32_t>(), st));
+    GHS_HIP_CHECK(hipMemcpyAsync(t.h_cnt, t.d_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    GHS_HIP_CHECK(hipStreamSynchronize(st));
+    if (*t.h_cnt > capacity) GHS_FAIL(GHS_E_NOMEM, "more flagged edges than the output's capacity");
+  }
+  GHS_HIP_CHECK(rocprim::select(t.p, need, in, d_in_mst + lo, d_eids, t.d_cnt, N, st));
+  GHS_HIP_CHECK(hipMemcpyAsync(t.h_cnt, t.d_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  GHS_HIP_CHECK(hipStreamSynchronize(st));
+  *count = *t.h_cnt;
   return GHS_OK;
 }
 

@@ -125,6 +125,18 @@ class DeviceMST:
         return self.in_mst[: self.edges.m].cpu().numpy().astype(bool)
 
 
+def flags_to_eids(in_mst, lo, hi, capacity=None):
+    """The edge ids e in [lo, hi) with in_mst[e] != 0, ascending, as an int64 device tensor — on the
+    device (ghs_flags_to_eids: a flagged select), never through torch.nonzero (whose first call per
+    process loaded for ~100 s with 4 ranks sharing one GPU, the gloo rehearsal's stall)."""
+    lo, hi = int(lo), int(hi)
+    cap = (hi - lo) if capacity is None else int(capacity)
+    out = torch.empty(max(cap, 1), dtype=torch.int32, device=in_mst.device)
+    cnt = ctypes.c_uint64(0)
+    _native.check(_native.load().ghs_flags_to_eids(_ptr(in_mst), lo, hi, _ptr(out), cap, ctypes.byref(cnt), _stream()))
+    return out[: cnt.value].to(torch.int64)
+
+
 def emulated_mst(edges, num_ranks, config=None):
     """The multi-rank loop of an N-GPU solve (ghs_solver_run, every rank its own solver, stream
     and host thread over its edge range) with all N ranks on THIS device and in-process

@@ -33,7 +33,7 @@ import torch
 import torch.distributed as dist
 
 from . import _native
-from .device import DeviceEdges, DeviceMST, _ptr, _stream, edge_range  # noqa: F401
+from .device import DeviceEdges, DeviceMST, _ptr, _stream, edge_range, flags_to_eids  # noqa: F401
 
 
 class HipStepper:
@@ -469,7 +469,8 @@ class DistributedMST:
         `dst` (the ranks' ranges ascend, so the concatenation is sorted), None elsewhere."""
         m = self.edges.m
         lo, hi = edge_range(m, self.rank, self.world)
-        mine = torch.nonzero(self.engine.in_mst[lo:hi]).flatten().to(torch.int64) + lo
+        # the MSF has < n edges: a range's ids fit min(hi - lo, n) slots
+        mine = flags_to_eids(self.engine.in_mst, lo, hi, min(hi - lo, self.edges.n))
         if not (dist.is_initialized() and dist.get_world_size(self.group) > 1):
             return mine
         world = dist.get_world_size(self.group)

@@ -183,6 +183,13 @@ int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t *v, 
  * call frees its state before returning. ghs_release_cache frees it now (device memory back to the
  * caller; safe to call at any time outside a driver call). */
 int ghs_release_cache(void);
+/* ABI 8: the MSF edge ids of the flag range [lo, hi) in order — d_eids[k] = the k-th e with
+ * d_in_mst[e] != 0 (uint32; room for `capacity` ids), *count (host) = how many — on the device
+ * (a flagged select), the form a rank's own-range MSF is gathered in (the reference's
+ * collect_results, ghs_implementation_mpi.py:760-779). Returns once *count is known (one stream
+ * sync); GHS_E_NOMEM without writing when more than `capacity` edges are flagged. hi < 2^32. */
+int ghs_flags_to_eids(const uint8_t *d_in_mst, uint64_t lo, uint64_t hi, uint32_t *d_eids, uint64_t capacity,
+                      uint64_t *count, void *stream);
 
 /* ---- device-resident API -----------------------------------------------------------------
  * Input: the canonical edge list in HBM (d_u, d_v, d_w: m uint32 each, 16-byte aligned) — the

@@ -1032,3 +1032,22 @@ def test_lds_tail_tie_heavy_and_sizes(seed, n, m, wmax, torch_cuda):
         res, _ = eng.run()
         assert np.array_equal(eng.in_mst_host(), ref_in.astype(bool))
         assert (res.total_weight, res.num_mst_edges) == (ref_tw, ref_k)
+
+
+@pytest.mark.parametrize("lo,hi,cap", [(0, 0, 1), (0, 1000, None), (3, 997, None), (0, 100000, 5000), (12345, 90001, 20000)])
+def test_flags_to_eids(lo, hi, cap, torch_cuda):
+    """ABI 8 ghs_flags_to_eids (the device-side compaction a rank's MSF slice is gathered in):
+    the ascending ids of the flagged edges of [lo, hi), as torch.nonzero would give them; a
+    capacity below the flagged count is refused (GHS_E_NOMEM) without writing."""
+    torch = torch_cuda
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import flags_to_eids
+    g = torch.Generator().manual_seed(lo + hi)
+    flags = (torch.rand(100001, generator=g) < 0.03).to(torch.uint8).cuda()
+    want = torch.nonzero(flags[lo:hi]).flatten().cpu() + lo
+    got = flags_to_eids(flags, lo, hi, cap)
+    assert torch.equal(got.cpu(), want)
+    if want.numel() > 1:
+        with pytest.raises(_native.GHSError) as ei:
+            flags_to_eids(flags, lo, hi, want.numel() - 1)
+        assert ei.value.code == _native.GHS_E_NOMEM

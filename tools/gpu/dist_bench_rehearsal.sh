@@ -8,7 +8,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 port=29611
 for N in ${NS:-2}; do
-  timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 --master-port $port bench.py --gpus $N --backend gloo --steps ${STEPS:-2} --warmup 1 > "$OUT/bench_n$N.json" 2> "$OUT/bench_n$N.err" || { echo "N=$N failed"; tail -30 "$OUT/bench_n$N.err"; exit 1; }
+  timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 --master-port $port bench.py --gpus $N --backend gloo --steps ${STEPS:-2} --warmup 1 $BARGS > "$OUT/bench_n$N.json" 2> "$OUT/bench_n$N.err" || { echo "N=$N failed"; tail -30 "$OUT/bench_n$N.err"; exit 1; }
   python3 -c "
 import json
 d=json.loads([l for l in open('$OUT/bench_n$N.json') if l.startswith('{')][-1])
