@@ -212,7 +212,9 @@ def _pmc_match(name, key):
 
 def load_traffic(workload_tag, kernel):
     """Per-launch HBM bytes of `kernel` from a committed PMC profile (profiles/**/*_pmc.json,
-    the newest round's wins)."""
+    the newest round's wins). A profile name covering several template instantiations
+    (k_minedge<COMPACT>: with and without candidates; k_bmin<..>: the full and the plain form)
+    takes their launch-weighted mean."""
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*_pmc.json"), recursive=True)):
         try:
@@ -221,9 +223,13 @@ def load_traffic(workload_tag, kernel):
             continue
         if d.get("workload") != workload_tag:
             continue
-        for key, k in d.get("kernels", {}).items():
-            if _pmc_match(kernel, key) and k and k.get("traffic_bytes_per_launch"):
-                best = dict(k, _path=os.path.relpath(p, ROOT))
+        hits = [k for key, k in d.get("kernels", {}).items()
+                if _pmc_match(kernel, key) and k and k.get("traffic_bytes_per_launch")]
+        if hits:
+            w = [max(1, int(k.get("launches_fetch_pass", 1))) for k in hits]
+            tot = sum(k["traffic_bytes_per_launch"] * wi for k, wi in zip(hits, w))
+            best = {"traffic_bytes_per_launch": tot / sum(w), "launches": sum(w), "instantiations": len(hits),
+                    "_path": os.path.relpath(p, ROOT)}
     return best
 
 
