@@ -2278,6 +2278,9 @@ __global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ sr
   // of filling one bucket each that a single k_bmin workgroup would have to sweep. A record's hot
   // end is marked (bit 31: bucketed solves have n <= 2^28), so k_bmin never takes it as a target.
   if (only_if && !*only_if) return;  // the windowed round ran (k_wmin)
+  // a no-op lookahead round: k_bmin reads no offsets either (its own guard), so nothing is written
+  // (the offset table alone is (nb + 1) x BK_G words: ~0.1 ms on the 16384^2 grids)
+  if (noop) return;
   const uint32_t nhot = hot ? hot[0] : 0u;
   const uint32_t hot0 = nhot ? hot[1] : LABEL_NONE;  // one hot fragment (R-MAT: the giant): a compare
   for (uint32_t i = threadIdx.x; i < HOT_HASH; i += BK_T) s_hl[i] = LABEL_NONE;
