@@ -5103,14 +5103,18 @@ static int run_level_pipelined(ghs_solver *s) {
   uint64_t live_prev = s->cur_arcs, nact_prev = s->level_nact;  // inputs of the next checked round
   uint32_t issued = 0, checked = 0;
   uint64_t last_in = s->level_nact;  // the active input of the last checked round
+  double decay = 2.0;                 // its contraction (input / output fragments), at least 2
   std::vector<unsigned long long> seqs(LEVEL_ROUND_CAP + s->lookahead + 1);
   for (;;) {
     if (issued < checked + 1 + s->lookahead) {
       // the LDS tail: once the bound on the next round's active fragments is small, read the
       // outstanding reports (the exact count), then finish the level there if it fits
+      // (only when the round in flight may leave few enough — predicted with the
+      // last checked round's contraction — so a level contracting slowly above TAIL_MAX keeps its
+      // lookahead)
       if (issued >= 1 && s->nact <= TAIL_TRY && tail_usable(s)) {
-        if (checked < issued) goto check;
-        if (s->nact >= 2 && s->nact <= TAIL_MAX) {
+        if (checked < issued && (double)s->nact / decay <= 2.0 * TAIL_MAX) goto check;
+        if (checked == issued && s->nact >= 2 && s->nact <= TAIL_MAX) {
           s->round = round0 + issued;
           return run_tail(s, last_in);
         }
@@ -5159,6 +5163,7 @@ static int run_level_pipelined(ghs_solver *s) {
       if (r.nact_in == 0) break;  // no edge in this level: its rounds were no-ops (checked stays 0)
     }
     push_stats(s, checked, live_prev, nact_prev, r.edges);
+    if (r.nact_out) decay = std::max(2.0, (double)nact_prev / (double)r.nact_out);
     last_in = nact_prev;
     // the live edges of round k + 1: round 0 does not compact (its input is read again)
     live_prev = checked == 0 ? live_prev : r.live_out;
