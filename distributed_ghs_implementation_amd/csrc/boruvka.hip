@@ -2178,6 +2178,17 @@ constexpr uint32_t BM_T = 1024;       // k_bmin threads
 #endif
 constexpr int BK_TILES = GHS_BK_TILES;  // k_bucket: 4-edge tiles per lane in flight
 
+// The offsets table of a bucketed round, (nb + 1) x BK_G words. Block-major (region g's nb + 1
+// offsets contiguous: k_bucket writes its row with coalesced stores; k_bmin's workgroup t reads one
+// word per region) — GHS_BK_BLOCKMAJOR=0: bucket-major (a bucket's 512 offsets contiguous: k_bmin
+// reads one row, but every k_bucket block writes a strided column, nb + 1 scattered 4-B stores).
+#ifndef GHS_BK_BLOCKMAJOR
+#define GHS_BK_BLOCKMAJOR 1
+#endif
+__device__ __forceinline__ uint64_t bk_off_index(uint32_t t, uint32_t g, uint32_t nb) {
+  return GHS_BK_BLOCKMAJOR ? (uint64_t)g * (nb + 1) + t : (uint64_t)t * BK_G + g;
+}
+
 // a block's share of the T live edges (a multiple of 4: whole 4-entry tiles); region g of the
 // records starts at 2 * quota * g (an edge gives at most two records)
 __device__ __forceinline__ uint64_t bk_quota(uint64_t T) { return ((T + BK_G - 1) / BK_G + 3) & ~3ull; }
@@ -2338,7 +2349,7 @@ __global__ __launch_bounds__(BK_T) void k_bucket(const uint32_t *__restrict__ sr
   }
   if (threadIdx.x == 0) s_h[nb] = tot;
   __syncthreads();
-  for (uint32_t t = threadIdx.x; t <= nb; t += BK_T) O[(uint64_t)t * BK_G + blockIdx.x] = s_h[t];
+  for (uint32_t t = threadIdx.x; t <= nb; t += BK_T) O[bk_off_index(t, blockIdx.x, nb)] = s_h[t];
   __syncthreads();  // the cursors below advance s_h
   // pass B: the records at the cursors of their buckets
   const uint64_t base = 2 * vb;
@@ -2518,8 +2529,8 @@ __global__ __launch_bounds__(BM_T) void k_bmin(const uint4 *__restrict__ rec, co
   const uint32_t t = blockIdx.x;
   uint32_t cnt = 0, st = 0;
   if (threadIdx.x < BK_G && !noop) {
-    st = O[(uint64_t)t * BK_G + threadIdx.x];
-    cnt = O[(uint64_t)(t + 1) * BK_G + threadIdx.x] - st;
+    st = O[bk_off_index(t, threadIdx.x, gridDim.x)];
+    cnt = O[bk_off_index(t + 1, threadIdx.x, gridDim.x)] - st;
   }
   // records before each run (scan of the counts), then the non-empty runs' slots (scan of their flags)
   uint32_t R, NZ;
