@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--no-scaling-base", action="store_true", help="N=1: skip the s26 strong-scaling point")
     ap.add_argument("--options", type=lambda x: int(x, 0), default=0,
                     help="ghs_config_t.options bits for N=1 (A/B of path options; 0 = the default path)")
+    ap.add_argument("--level1", type=float, default=None, help="level plan: level-1 edges per vertex (default auto)")
+    ap.add_argument("--level-growth", type=float, default=None, help="level plan: growth per level (default auto)")
     ap.add_argument("--dedup-max", type=int, default=None,
                     help="ghs_config_t.dedup_max for N=1 (parallel-edge filter at <= F fragments; A/B)")
     ap.add_argument("--coll-timeout", type=int, default=300,
@@ -565,8 +567,10 @@ def run(args, world, rank, dist, dev):
         eng, loop = agreed("engine setup + first solve", lambda: dist_engine(edges, rank, world, dist, args.backend),
                            rank, world, dist, dev)
     else:
-        custom = args.options or args.dedup_max is not None
-        eng = DeviceMST(edges, config=_native.make_config(options=args.options, dedup_max=args.dedup_max)
+        custom = args.options or args.dedup_max is not None or args.level1 is not None or args.level_growth is not None
+        eng = DeviceMST(edges, config=_native.make_config(options=args.options, dedup_max=args.dedup_max,
+                                                          level1_edges_per_vertex=args.level1,
+                                                          level_growth=args.level_growth)
                         if custom else None)
     step = eng.run
     dt_solve = None

@@ -32,6 +32,7 @@ def main():
                          "stepwise protocol) instead of the library loop's reduce-scatter + pair all-gather")
     ap.add_argument("--profile", action="store_true",
                     help="per-launch HIP-event profile of the last rep: kernel ms per round of the max rank")
+    ap.add_argument("--per-rank", action="store_true", help="with --profile: every rank's kernels in level-opening rounds")
     ap.add_argument("--max-levels", type=int, default=None)
     ap.add_argument("--level-growth", type=float, default=None)
     ap.add_argument("--level1", type=float, default=None, help="level-1 edges per vertex")
@@ -220,6 +221,15 @@ def main():
                 print(f"# round {i}: rank {worst} kernels {sum(ks.values()):.3f} ms of {rounds[i]['max_rank_ms']:.3f} | " +
                       " ".join(f"{k}={v:.3f}" for k, v in sorted(ks.items(), key=lambda kv: -kv[1]) if v >= 0.005),
                       file=sys.stderr)
+            if args.per_rank:  # every rank's kernels in the rounds that open a level (balance)
+                for i, per_rank in enumerate(kprof):
+                    if len(rounds[i]["collectives"]) < 2:
+                        continue
+                    for rk in range(W):
+                        ks = per_rank[rk]
+                        print(f"#   round {i} rank {rk}: {sum(ks.values()):.3f} ms | " +
+                              " ".join(f"{k}={v:.3f}" for k, v in sorted(ks.items(), key=lambda kv: -kv[1])[:6]),
+                              file=sys.stderr)
             print("# per solve (max rank per round): " + " ".join(f"{k}={v:.3f}" for k, v in
                                                                   sorted(tot.items(), key=lambda kv: -kv[1])),
                   file=sys.stderr)
