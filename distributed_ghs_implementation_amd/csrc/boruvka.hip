@@ -179,22 +179,35 @@ __device__ __forceinline__ uint32_t block_offsets(uint32_t mine, uint32_t *s_wcn
   return before;
 }
 
+// Wave-exclusive prefix sum of small per-lane counts (x < 2^B) from B ballots: bit k of every
+// lane's count is one 64-bit ballot, and a lane's prefix is the sum over k of 2^k times the set bits
+// below it (mbcnt). No cross-lane data movement — a shuffle scan is six dependent ds_bpermute
+// round trips per tile — and the total is uniform (scalar popcounts).
+template <int B>
+__device__ __forceinline__ uint32_t wave_excl_small(uint32_t x, uint32_t *total) {
+  uint32_t ex = 0, t = 0;
+#pragma unroll
+  for (int k = 0; k < B; ++k) {
+    const uint64_t m = __ballot((x >> k) & 1u);
+    ex += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << k;
+    t += (uint32_t)__popcll(m) << k;
+  }
+  *total = t;
+  return ex;
+}
+
 // Wave-level offsets for a block-wide compaction step: *lane_excl = items of lower lanes of the
 // wave, *wave_before = items of lower waves of the block, *wave_cnt = the wave's items,
-// *total = the block's. Every thread of the block must call it (two barriers).
+// *total = the block's. mine < 8 (a lane's 4-entry tile). Every thread of the block must call it
+// (two barriers).
 template <int NT = BLOCK>
 __device__ __forceinline__ void block_offsets_w(uint32_t mine, uint32_t *s_wcnt, uint32_t *lane_excl,
                                                 uint32_t *wave_before, uint32_t *wave_cnt, uint32_t *total) {
   const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
-  uint32_t incl = mine;
-#pragma unroll
-  for (int d = 1; d < WAVE; d <<= 1) {
-    const uint32_t o = __shfl_up(incl, d);
-    if (lane >= d) incl += o;
-  }
-  *lane_excl = incl - mine;
-  *wave_cnt = __shfl(incl, WAVE - 1);
-  if (lane == WAVE - 1) s_wcnt[wid] = incl;
+  uint32_t wc;
+  *lane_excl = wave_excl_small<3>(mine, &wc);
+  *wave_cnt = wc;
+  if (lane == 0) s_wcnt[wid] = wc;
   __syncthreads();
   uint32_t before = 0, t = 0;
 #pragma unroll
@@ -207,20 +220,28 @@ __device__ __forceinline__ void block_offsets_w(uint32_t mine, uint32_t *s_wcnt,
   __syncthreads();
 }
 
-// Two compaction streams' offsets from ONE scan: the per-lane counts (<= 4 each; a block's
-// totals < 2^16) are packed into the two halves of a 32-bit word, so the level / pending split of
-// a tile costs one shuffle scan and one pair of barriers instead of two.
+// Two compaction streams' offsets with one pair of barriers: the per-lane counts (< 8 each; a
+// block's totals < 2^16) are scanned by ballots and their wave totals packed into the two halves
+// of one 32-bit LDS word, so the level / pending split of a tile costs one cross-wave step.
 struct Offs2 {
   uint32_t lane_excl[2], wave_before[2], wave_cnt[2], total[2];
 };
 __device__ __forceinline__ Offs2 block_offsets_w2(uint32_t mine0, uint32_t mine1, uint32_t *s_wcnt) {
-  uint32_t le, wb, wc, t;
-  block_offsets_w(mine0 | (mine1 << 16), s_wcnt, &le, &wb, &wc, &t);
+  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
   Offs2 o;
-  o.lane_excl[0] = le & 0xffffu;  o.lane_excl[1] = le >> 16;
-  o.wave_before[0] = wb & 0xffffu; o.wave_before[1] = wb >> 16;
-  o.wave_cnt[0] = wc & 0xffffu;   o.wave_cnt[1] = wc >> 16;
-  o.total[0] = t & 0xffffu;       o.total[1] = t >> 16;
+  o.lane_excl[0] = wave_excl_small<3>(mine0, &o.wave_cnt[0]);
+  o.lane_excl[1] = wave_excl_small<3>(mine1, &o.wave_cnt[1]);
+  if (lane == 0) s_wcnt[wid] = o.wave_cnt[0] | (o.wave_cnt[1] << 16);
+  __syncthreads();
+  uint32_t before = 0, t = 0;
+#pragma unroll
+  for (int w = 0; w < BLOCK / WAVE; ++w) {
+    if (w < wid) before += s_wcnt[w];
+    t += s_wcnt[w];
+  }
+  __syncthreads();
+  o.wave_before[0] = before & 0xffffu; o.wave_before[1] = before >> 16;
+  o.total[0] = t & 0xffffu;            o.total[1] = t >> 16;
   return o;
 }
 
@@ -390,7 +411,7 @@ __device__ __forceinline__ void wave_append(WaveStage &ws, WaveOut &wo, const ui
                                             const uint64_t k[4], uint32_t mask, uint32_t *__restrict__ oa,
                                             uint32_t *__restrict__ ob, uint64_t *__restrict__ ok) {
   uint32_t tile;
-  const uint32_t ex = wave_excl_scan((uint32_t)__popc(mask), &tile);
+  const uint32_t ex = wave_excl_small<3>((uint32_t)__popc(mask), &tile);
   if (tile == 0) return;
   if (wo.cnt + tile > WAVE * 4) wave_flush(ws, wo, oa, ob, ok);
   uint32_t p = wo.cnt + ex;
