@@ -3,6 +3,7 @@
 //   contig  : block b owns the contiguous range [b*Q, (b+1)*Q) (the compaction layout)
 //   stride  : grid-stride over 1024-edge tiles (all blocks sweep the arrays together)
 //   contig+scan : contig + a block-wide prefix (2 barriers) per tile, like block_offsets
+//   wave    : each wave owns a contiguous slice (k_select's layout: 256 edges per wave step)
 // Prints GB/s (12 B per edge read).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -16,7 +17,19 @@ __global__ __launch_bounds__(256) void k_read(const uint32_t *__restrict__ a, co
                                               const uint32_t *__restrict__ c, uint64_t M, uint32_t *out) {
   __shared__ uint32_t s[8];
   uint32_t acc = 0;
-  if (MODE == 1) {
+  if (MODE == 3) {
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t W = (uint64_t)gridDim.x * 4, gw = blockIdx.x * 4ull + wid;
+    const uint64_t Q = ((M + W - 1) / W + 255) & ~255ull;
+    const uint64_t vb = Q * gw, ve = vb + Q < M ? vb + Q : M;
+    for (uint64_t v0 = vb; v0 < ve; v0 += 256) {
+      const uint64_t i = v0 + lane * 4;
+      if (i + 4 <= ve) {
+        uint4 x = *(const uint4 *)(a + i), y = *(const uint4 *)(b + i), z = *(const uint4 *)(c + i);
+        acc ^= x.x ^ x.y ^ x.z ^ x.w ^ y.x ^ y.y ^ y.z ^ y.w ^ z.x ^ z.y ^ z.z ^ z.w;
+      }
+    }
+  } else if (MODE == 1) {
     for (uint64_t t = blockIdx.x; t * 1024 < M; t += gridDim.x) {
       const uint64_t i = t * 1024 + threadIdx.x * 4;
       if (i + 4 <= M) {
@@ -57,15 +70,16 @@ int main() {
   CK(hipMalloc(&o, 1 << 26));
   CK(hipMemset(a, 1, M * 4)); CK(hipMemset(b, 2, M * 4)); CK(hipMemset(c, 3, M * 4));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  const char *names[3] = {"contig", "stride", "contig+scan"};
+  const char *names[4] = {"contig", "stride", "contig+scan", "wave"};
   for (int grid : {1024, 2048, 4096, 8192}) {
-    for (int mode = 0; mode < 3; ++mode) {
+    for (int mode = 0; mode < 4; ++mode) {
       float best = 1e9;
       for (int rep = 0; rep < 5; ++rep) {
         CK(hipEventRecord(e0));
         if (mode == 0) k_read<0><<<grid, 256>>>(a, b, c, M, o);
         if (mode == 1) k_read<1><<<grid, 256>>>(a, b, c, M, o);
         if (mode == 2) k_read<2><<<grid, 256>>>(a, b, c, M, o);
+        if (mode == 3) k_read<3><<<grid, 256>>>(a, b, c, M, o);
         CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
         float ms; CK(hipEventElapsedTime(&ms, e0, e1)); if (ms < best) best = ms;
       }
