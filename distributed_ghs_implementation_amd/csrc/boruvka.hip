@@ -4138,11 +4138,20 @@ static bool bucket_geometry(uint32_t n, uint32_t *bs, uint32_t *nb) {
   return true;
 }
 
+// Arrays are staggered by WS_STAGGER bytes: with power-of-two n (R-MAT, 2^k-sided grids) the
+// vertex arrays are power-of-two sized, so lab[v], par[v] and best[v] — which k_jump_ident and
+// the hooks read at the same index — would sit at power-of-two distances and land in the same
+// memory channels. 16384^2 grid, same box (profiles/r05/ab/stagger/): k_jump_ident 4.25 -> 4.00 ms,
+// the step 37.5 -> 37.25 ms (2 repeats each; a 20.6-KiB stagger gave the same jump).
+#ifndef GHS_WS_STAGGER
+#define GHS_WS_STAGGER ((1u << 20) + 1024u)
+#endif
+constexpr size_t WS_STAGGER = GHS_WS_STAGGER;
 static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs_solver *s, char *base) {
   size_t off = 0;
   auto carve = [&](size_t bytes) -> char * {
     char *p = base ? base + off : nullptr;
-    off = align_up(off + bytes, 256);
+    off = align_up(off + bytes, 256) + WS_STAGGER;
     return p;
   };
   const size_t N = (size_t)n;
