@@ -1,8 +1,13 @@
 """Distinct fragment pairs among the LDS tail's records (numpy restatement of level 0 on R-MAT: two
 Boruvka rounds, then the tail's rounds), per 256 consecutive-record blocks: how much a per-block
-(da, db) minimum would shrink the records a tail round streams.  python tools/sim/tail_pairs.py 22"""
-import sys, numpy as np
-sys.path.insert(0,'/root/repo')
+(da, db) minimum would shrink the records a tail round streams. A checker-side analysis (it uses
+the oracle's R-MAT generator):  python tests/tools/tail_pairs.py 22"""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from oracle import oracle as O
 from scipy.sparse import coo_matrix
 from scipy.sparse.csgraph import connected_components
