@@ -230,6 +230,9 @@ def main():
                         print(f"#   round {i} rank {rk}: {sum(ks.values()):.3f} ms | " +
                               " ".join(f"{k}={v:.3f}" for k, v in sorted(ks.items(), key=lambda kv: -kv[1])[:6]),
                               file=sys.stderr)
+            kmax = sum(max(sum(pr[rk].values()) for rk in range(W)) for pr in kprof)
+            print(f"# kernels only: sum over rounds of the max rank's kernel time {kmax:.3f} ms "
+                  f"(the stepwise calls' host round trips are the rest of sum_max_rank_compute_ms)", file=sys.stderr)
             print("# per solve (max rank per round): " + " ".join(f"{k}={v:.3f}" for k, v in
                                                                   sorted(tot.items(), key=lambda kv: -kv[1])),
                   file=sys.stderr)
