@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--edgefactor", type=int, default=16)
     ap.add_argument("--workload", choices=["rmat", "grid", "grid-gradient"], default="rmat")
     ap.add_argument("--grid-k", type=int, default=16384)
+    ap.add_argument("--input", choices=["auto", "csr", "coo"], default="auto",
+                    help="the device-resident input form: CSR (row offsets + v + w, ghs_mst_device_csr, ABI 9) "
+                         "or COO (u + v + w, ghs_mst_device); auto = COO")
     ap.add_argument("--cpu-scale", type=int, default=22, help="R-MAT scale of the serial-Kruskal sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--nx-scale", type=int, default=16, help="R-MAT scale of the NetworkX baseline sample")
@@ -90,14 +93,23 @@ def _first_round(stats, r):
     return r == 0 or stats[r - 1]["level"] != stats[r]["level"]
 
 
+# bytes the canonical passes stream per edge and per vertex row: COO u, v, w = 12 B per edge; CSR
+# (ABI 9) v, w = 8 B per edge + the u32 row offset of every row (run() sets it from the input form)
+STREAM_BYTES = {"edge": 12.0, "row": 0.0}
+
+
+def _stream_bytes(res, n):
+    return STREAM_BYTES["edge"] * res.canon_edges + STREAM_BYTES["row"] * (n + 1)
+
+
 def launch_bytes(rec, stats, res, n, windowed=frozenset()):
     """`windowed`: the rounds whose windowed kernel (k_wmin) did the work — their k_bucket / k_bmin
     launches are the device-side fallback that exited at once (k_select's span flag unset)."""
     k = rec["kernel"]
     if k == "k_select":
-        return 12.0 * res.canon_edges + 16.0 * res.select_out  # u, v, w in; level-0 edges out
+        return _stream_bytes(res, n) + 16.0 * res.select_out  # the list in; level-0 edges out
     if k == "k_filter":
-        return 12.0 * res.canon_edges + 16.0 * res.filter_out  # stream + level-1 and pending edges out
+        return _stream_bytes(res, n) + 16.0 * res.filter_out  # stream + level-1 and pending edges out
     if k == "k_resolve":
         return 8.0 * n + n / 8.0  # lab read + write, giant bitmap
     if k == "k_jump_ident":
@@ -382,6 +394,14 @@ def make_workload(args, world):
         edges = generate_grid(k, 1 if args.workload == "grid-gradient" else 0)
         tag = f"{args.workload}-{k}x{k}"
         cfg = {"workload": tag, "grid_k": k}
+    form = args.input if args.input != "auto" else "coo"
+    if form == "csr":
+        # the north_star's CSR edge list: row offsets (built on the device from the sorted u, outside
+        # the timed region like the generation itself), u released — the solve streams (off, v, w)
+        edges = edges.csr_only()
+        cfg["input"] = "CSR: n+1 u32 row offsets + v + w (u32), the canonical list with u implied (ghs_mst_device_csr)"
+    else:
+        cfg["input"] = "COO: u + v + w (u32), the canonical list (ghs_mst_device)"
     return edges, tag, cfg
 
 
@@ -544,6 +564,8 @@ def run(args, world, rank, dist, dev):
 
     (edges, tag, cfg), gen_s = agreed("generate", gen, rank, world, dist, dev)
     n, m = edges.n, edges.m
+    if edges.off is not None and edges.u is None:  # CSR input: 8 B per edge + 4 B per row streamed
+        STREAM_BYTES.update(edge=8.0, row=4.0 / max(1, world))
     cfg.update({"n": n, "m": m, "partition": f"canonical edge ranges x{world}", "parallelism": f"edges{world}"})
 
     ref = None

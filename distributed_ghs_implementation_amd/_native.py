@@ -46,6 +46,7 @@ EXPORTED_SYMBOLS = (
     "ghs_profile_enable", "ghs_profile_read", "ghs_kernel_name",
     "ghs_comm_unique_id", "ghs_comm_init", "ghs_comm_destroy", "ghs_solver_run", "ghs_mst_emulated",
     "ghs_release_cache", "ghs_slot_retries", "ghs_flags_to_eids",
+    "ghs_mst_device_csr", "ghs_csr_offsets", "ghs_solver_create_csr",
 )
 
 
@@ -98,7 +99,7 @@ class RoundStatsList(collections.abc.Sequence):
         return repr(list(self))
 
 
-ABI_VERSION = 8  # include/ghs_mst.h GHS_MST_ABI_VERSION
+ABI_VERSION = 9  # include/ghs_mst.h GHS_MST_ABI_VERSION
 
 
 class Result(ctypes.Structure):
@@ -283,6 +284,10 @@ def load():
             "ghs_release_cache": (i32, []),
             "ghs_slot_retries": (i32, [P(u64)]),
             "ghs_flags_to_eids": (i32, [vp, u64, u64, vp, u64, P(u64), vp]),
+            # ABI 9: the CSR form of the canonical list
+            "ghs_mst_device_csr": (i32, [u32, u64, vp, vp, vp, vp, P(Config), vp, sz, vp, vp, P(Result), P(RoundStats)]),
+            "ghs_csr_offsets": (i32, [u32, u64, vp, vp, vp]),
+            "ghs_solver_create_csr": (i32, [u32, u64, vp, vp, vp, vp, u64, u64, P(Config), vp, sz, vp, vp, P(vp)]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(L, name)

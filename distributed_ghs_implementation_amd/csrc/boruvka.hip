@@ -307,6 +307,107 @@ __device__ __forceinline__ void st_b64(uint64_t v, __amdgpu_buffer_rsrc_t r, uin
   __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)v, (uint32_t)(v >> 32)}, r, (int)off, 0, 0);
 }
 
+// ------------------------------------------------------------------------------------------
+// CSR input (ABI 9). The canonical list may come as row offsets off[0..n] (u32: m < 2^31) + v + w
+// — the north_star's "CSR edge list in HBM", u implied: edge e of row r has u = r for
+// off[r] <= e < off[r + 1]. The streaming passes then read 8 B per edge plus ~4 B per row instead of
+// 12 B per edge.
+// Per solve, k_csr_trow (one pass over off[], which it also validates) writes trow[t] = the row
+// holding edge E0 + 256 t for every 256-edge tile of the solver's range (trow[ntiles]: the row of its
+// last edge). A streaming wave derives u for a tile [t0, t0 + 256) from R0 = trow[t] and R1 =
+// trow[t + 1] (csr_tile_rows): the rows R0 + 1 .. R1 start inside the tile (or at its end); each
+// writes its id into the LDS slot of its first edge (ds_max: the empty rows before a nonempty one
+// share its slot), and a max-scan over the 256 slots (in-lane over a lane's 4, then a wave DPP scan)
+// gives every edge its row. Slots a tile does not write hold earlier tiles' rows, all <= R0, so they
+// never win the max (a private table is zeroed once per kernel, not per tile). The rows come from
+// 64-row windows of off[]: the first one prefetched a tile ahead, the rest of a tile's windows
+// (R1 - R0 > 64: lattices ~128; the sparse end of an R-MAT list, where high ids store few canonical
+// edges, up to thousands of mostly empty rows per tile) issued 8 at a time — R1 is known up front.
+// (The first version walked windows from R0 until one passed the tile's end, a dependent round trip
+// per 64 rows: the waves owning the list's sparse end made k_select 1.9 ms against COO's 0.7.)
+// A gather of u by edge id (the fragment-form hooks: one per hooked fragment) is a binary search
+// over off[] (csr_row), unless the caller also passed u (Ends).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {  // inclusive max over the wave (gfx9 DPP)
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));  // row_shr:1
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));  // row_shr:2
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));  // row_shr:4
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));  // row_shr:8
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return x;
+}
+// the value of lane - 1 (lane 0: 0)
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);  // wave_shr:1
+}
+
+// the row of edge e: the largest r in [0, n - 1] with off[r] <= e (one thread, binary search)
+__device__ __forceinline__ uint32_t csr_row(const uint32_t *__restrict__ off, uint32_t n, uint32_t e) {
+  uint32_t lo = 0, hi = n ? n - 1 : 0;
+  while (lo < hi) {
+    const uint32_t mid = lo + ((hi - lo + 1) >> 1);
+    if (off[mid] <= e) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// one 64-row window: lane i holds off[base + i] (0xffffffff past off[n]); the load is issued
+// unconditionally (clamped index), so a caller can prefetch it
+__device__ __forceinline__ uint32_t csr_win(const uint32_t *__restrict__ off, uint32_t n, uint32_t base) {
+  const uint32_t r = base + (threadIdx.x & (WAVE - 1));
+  const uint32_t o = off[min(r, n)];
+  return r <= n ? o : 0xffffffffu;
+}
+
+// Rows of the wave tile [t0, t0 + 256): u[j] = the row of edge t0 + 4 * lane + j, from R0 (the row
+// holding t0), R1 (the row holding t0 + 256, or the range's last edge) and w0 = csr_win(off, n,
+// R0 + 1) (prefetched). s_head: the wave's 256-entry LDS table; CLEAR: zeroed first (a table
+// sharing LDS with other per-tile data).
+template <bool CLEAR>
+__device__ __forceinline__ void csr_tile_rows(const uint32_t *__restrict__ off, uint32_t n, uint32_t R0, uint32_t R1,
+                                              uint32_t t0, uint32_t *s_head, uint32_t u[4], uint32_t w0) {
+  const uint32_t lane = threadIdx.x & (WAVE - 1), tend = t0 + 256u;
+  if (CLEAR) {
+    reinterpret_cast<uint4 *>(s_head)[lane] = make_uint4(0u, 0u, 0u, 0u);
+    wave_sync_lds();
+  }
+  // rows starting strictly inside the tile (a row at t0 is R0 itself; rows past R1 start past tend)
+  auto mark = [&](uint32_t o, uint32_t r) {
+    if ((o > t0) & (o < tend)) atomicMax(&s_head[o - t0], r);
+  };
+  mark(w0, R0 + 1 + lane);
+  for (uint32_t base = R0 + 1 + WAVE; base <= R1; base += 8 * WAVE) {  // more than 64 rows: up to 8 windows a trip
+    const uint32_t cnt = min(8u, (R1 - base) / WAVE + 1);  // wave-uniform
+    uint32_t o[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) o[k] = k < cnt ? csr_win(off, n, base + k * WAVE) : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k)
+      if (k < cnt) mark(o[k], base + k * WAVE + lane);
+  }
+  wave_sync_lds();
+  const uint4 h = reinterpret_cast<const uint4 *>(s_head)[lane];
+  const uint32_t x0 = h.x, x1 = max(x0, h.y), x2 = max(x1, h.z), x3 = max(x2, h.w);
+  const uint32_t base = max(R0, wave_shr1(wave_incl_max(x3)));
+  u[0] = max(base, x0);
+  u[1] = max(base, x1);
+  u[2] = max(base, x2);
+  u[3] = max(base, x3);
+}
+
+// canonical endpoints by edge id (the fragment-form hooks, the plan's span sample): u from the
+// caller's u array, or — CSR input without one — a binary search over the row offsets
+struct Ends {
+  const uint32_t *u;    // nullptr: CSR input
+  const uint32_t *off;  // CSR row offsets (n + 1 entries)
+  const uint32_t *v;
+  uint32_t n;
+};
+__device__ __forceinline__ uint32_t end_u(const Ends &E, uint32_t eid) {
+  return E.u ? E.u[eid] : csr_row(E.off, E.n, eid);
+}
+
 struct WaveStage {
   uint32_t a[WAVE * 4];
   uint32_t b[WAVE * 4];
@@ -943,8 +1044,7 @@ __device__ void block_scan_counts(const uint64_t *__restrict__ count, uint32_t n
 
 __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact,
                                                 const uint64_t *__restrict__ best, const uint32_t *__restrict__ lab,
-                                                const uint32_t *__restrict__ eu, const uint32_t *__restrict__ ev,
-                                                uint32_t *__restrict__ par, uint8_t *__restrict__ in_mst,
+                                                const Ends E, uint32_t *__restrict__ par, uint8_t *__restrict__ in_mst,
                                                 unsigned long long *__restrict__ acc /* [0] weight, [1] edges */,
                                                 unsigned long long *__restrict__ err,
                                                 const uint64_t *__restrict__ scan_count, uint32_t scan_n,
@@ -965,7 +1065,7 @@ __global__ __launch_bounds__(BLOCK) void k_hook(const uint32_t *__restrict__ act
       // a level's first round: k_resolve left every label a root (one read, no walk). A dense level
       // (several ranks): an endpoint's level-open root vlab[x] (resolved), its dense label
       // dense_rank(vlab[x]), then the walk through the dense labels
-      uint32_t xa = eu[eid], xb = ev[eid];
+      uint32_t xa = end_u(E, eid), xb = E.v[eid];
       if (dr.bits) {
         xa = dense_rank(dr, vlab[xa]);
         xb = dense_rank(dr, vlab[xb]);
@@ -1200,8 +1300,7 @@ __global__ void k_pad_slots(uint64_t *__restrict__ best, const unsigned long lon
   if (i < padded) best[i] = KEY_NONE;
 }
 
-__global__ void k_hook_owner(const uint64_t *__restrict__ best, uint64_t lo, uint64_t hi,
-                             const uint32_t *__restrict__ eu, const uint32_t *__restrict__ ev,
+__global__ void k_hook_owner(const uint64_t *__restrict__ best, uint64_t lo, uint64_t hi, const Ends E,
                              const uint32_t *__restrict__ vlab, DenseRank dr, uint64_t *__restrict__ pairs,
                              unsigned long long *__restrict__ err) {
   for (uint64_t c = lo + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < hi; c += (uint64_t)gridDim.x * blockDim.x) {
@@ -1209,7 +1308,7 @@ __global__ void k_hook_owner(const uint64_t *__restrict__ best, uint64_t lo, uin
     uint64_t out = KEY_NONE;
     if (k != KEY_NONE) {
       const uint32_t eid = (uint32_t)k;
-      const uint32_t da = dense_rank(dr, vlab[eu[eid]]), db = dense_rank(dr, vlab[ev[eid]]);
+      const uint32_t da = dense_rank(dr, vlab[end_u(E, eid)]), db = dense_rank(dr, vlab[E.v[eid]]);
       if (da != (uint32_t)c && db != (uint32_t)c) atomicOr(err, 2ull);  // the chosen edge must leave c
       out = ((uint64_t)eid << 32) | (da == (uint32_t)c ? db : da);
     }
@@ -1658,12 +1757,12 @@ __global__ __launch_bounds__(BLOCK) void k_resolve(uint32_t n, uint32_t *lab, co
 // evenly spaced sample of the canonical list: weights (the level plan) and, in out[NSAMPLE_W + i],
 // edge spans v - u (the plan's locality test for the bucketed rounds)
 constexpr uint32_t NSAMPLE_W = 16384;  // edges sampled for the level plan
-__global__ void k_sample_weights(uint64_t cnt, const uint32_t *__restrict__ u, const uint32_t *__restrict__ v,
-                                 const uint32_t *__restrict__ w, uint32_t nsamp, uint32_t *__restrict__ out) {
+__global__ void k_sample_weights(uint64_t cnt, const Ends E, const uint32_t *__restrict__ w, uint32_t nsamp,
+                                 uint32_t *__restrict__ out) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsamp; i += gridDim.x * blockDim.x) {
     const uint64_t e = ((uint64_t)i * cnt) / nsamp;
     out[i] = w[e];
-    out[NSAMPLE_W + i] = v[e] - u[e];  // canonical: u < v (unvalidated here: only a heuristic)
+    out[NSAMPLE_W + i] = E.v[e] - end_u(E, (uint32_t)e);  // canonical: u < v (unvalidated here: only a heuristic)
   }
 }
 
@@ -1761,20 +1860,44 @@ __global__ __launch_bounds__(1024) void k_plan(const uint32_t *__restrict__ samp
 // labels are the endpoints); flags both ends active. Nothing else is written: the
 // heavier edges stay where they are until k_filter. Block-private output regions: deterministic,
 // no atomics; the next tile's loads are issued before the current one is compacted.
+// CSR (ABI 9): u is derived from the row offsets (csr_tile_rows, the tiles' rows from k_csr_trow,
+// which validated the offsets: a wave's slice is a multiple of 256 edges, so its tiles are trow's).
 // ------------------------------------------------------------------------------------------
-GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, const uint32_t *__restrict__ eu,
-                                const uint32_t *__restrict__ ev, const uint32_t *__restrict__ ew,
-                                const uint64_t *__restrict__ w_hi_p,
+// trow[t] = the row holding edge E0 + 256 t (t < ntiles), trow[ntiles] = the row of the range's last
+// edge: every nonempty row writes the tile starts inside it (one writer per tile). The same pass
+// validates the offsets (off[0] = 0, nondecreasing, off[n] = m; err bit 8): k_select, the next
+// launch, skips its stream when it is set, so no tile walks rows from a garbage trow.
+__global__ void k_csr_trow(const uint32_t *__restrict__ off, uint32_t n, uint64_t m, uint64_t E0, uint64_t e_hi,
+                           uint32_t *__restrict__ trow, unsigned long long *__restrict__ err) {
+  const uint64_t ntiles = (e_hi - E0 + 255) >> 8;
+  bool bad = false;
+  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t lo = off[r], hi = off[r + 1];
+    bad |= lo > hi;
+    if (lo >= hi || hi <= E0 || lo >= e_hi) continue;  // empty (or invalid), or outside the range
+    const uint64_t a = lo > E0 ? lo - E0 : 0, b = (hi < e_hi ? hi : e_hi) - E0;  // [a, b) relative to E0
+    for (uint64_t t = (a + 255) >> 8; (t << 8) < b; ++t) trow[t] = (uint32_t)r;
+    if (lo < e_hi && e_hi <= hi) trow[ntiles] = (uint32_t)r;  // the row of edge e_hi - 1
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) bad |= (off[0] != 0u) | ((uint64_t)off[n] != m);
+  if (bad) atomicOr(err, 8ull);
+}
+
+template <bool CSR>
+GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t m, uint64_t e_lo, uint64_t e_hi, const uint32_t *__restrict__ eu,
+                                const uint32_t *__restrict__ eoff, const uint32_t *__restrict__ ev,
+                                const uint32_t *__restrict__ ew, const uint64_t *__restrict__ w_hi_p,
                                 uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst, uint64_t *__restrict__ okey,
                                 uint64_t *__restrict__ ostart, uint64_t *__restrict__ ocount,
                                 uint8_t *__restrict__ mark, unsigned long long *__restrict__ err,
                                 const uint64_t *__restrict__ local_flag, uint32_t bs,
-                                unsigned long long *__restrict__ long_flag) {
+                                unsigned long long *__restrict__ long_flag, const uint32_t *__restrict__ trow) {
   const uint64_t w_hi = *w_hi_p;  // the level plan lives on the device (k_plan)
   // a lattice-like plan (k_plan's span sample): note any level-0 edge whose ends lie more than one
   // bucket (2^bs ids) apart — the windowed round 0 (k_wmin) then falls back to k_bucket / k_bmin
   const bool check_span = local_flag && *local_flag;
   __shared__ WaveStage s_stage[BLOCK / WAVE];
+  __shared__ uint32_t s_head[CSR ? BLOCK / WAVE : 1][CSR ? WAVE * 4 : 1];
   // the wave index through readfirstlane: uniform in an SGPR, so every value derived from it
   // (the slice, its buffer descriptors) is scalar — a VGPR descriptor makes hipcc wrap each
   // buffer load in a waterfall loop
@@ -1783,35 +1906,69 @@ GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, cons
   const uint64_t W = (uint64_t)gridDim.x * (BLOCK / WAVE);
   const uint64_t E0 = e_lo & ~3ull;
   const uint64_t T = e_hi - E0;
-  const uint64_t Q = ((T + W - 1) / W + 3) & ~3ull;
+  const uint64_t QA = CSR ? 255 : 3;  // CSR: slices of whole 256-edge tiles (the trow grid)
+  const uint64_t Q = ((T + W - 1) / W + QA) & ~QA;
   const uint64_t vb = Q * gw;
   const uint64_t ve = (vb + Q < T) ? vb + Q : T;
   const uint64_t eb = E0 + vb;  // first edge of this wave
   const uint64_t nbytes = ve > vb ? (ve - vb) * 4 : 0;
-  const __amdgpu_buffer_rsrc_t ru = make_rsrc(eu + eb, nbytes);
+  const __amdgpu_buffer_rsrc_t ru = make_rsrc(CSR ? ev : eu + eb, CSR ? 0 : nbytes);
   const __amdgpu_buffer_rsrc_t rv = make_rsrc(ev + eb, nbytes);
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(ew + eb, nbytes);
+  bool bad = false, far = false;
   // the edge before each lane's tile; offset -4 (the wave's first tile) is out of range of the
   // descriptor and is replaced by the wave's predecessor edge, loaded once
   uint32_t bpa = 0, bpb = 0;
-  if (eb > 0 && ve > vb) {
+  // CSR: the rows holding this tile's first edge and the next tile's (R0, R1), the tile after that's
+  // (R2, a scalar load one tile ahead), the first window of rows after R0 (prefetched), the last
+  // edge's row of the previous tile
+  uint32_t R0 = 0, R1 = 0, R2 = 0, w0 = 0, lastu = 0;
+  uint64_t vend = ve;  // CSR: an offsets error (k_csr_trow) empties the stream
+  if (CSR) {
+    reinterpret_cast<uint4 *>(s_head[wid])[lane] = make_uint4(0u, 0u, 0u, 0u);
+    if (*err & 8ull) vend = vb;
+    const uint64_t ntiles = (T + 255) >> 8;
+    if (vend > vb) {
+      R0 = trow[vb >> 8];
+      R1 = trow[(vb >> 8) + 1];
+      R2 = trow[min((vb >> 8) + 2, ntiles)];
+      w0 = csr_win(eoff, n, R0 + 1);
+    }
+    // edge eb - 1 lies in the same row iff that row began before eb (else in a lower one)
+    if (eb > 0 && vend > vb) {
+      bpa = eoff[R0] < eb ? R0 : R0 - 1u;
+      bpb = ev[eb - 1];
+    }
+  } else if (eb > 0 && ve > vb) {
     bpa = eu[eb - 1];
     bpb = ev[eb - 1];
   }
   const uint32_t lane_off = lane * 16u;  // byte offset of the lane's tile in an iteration
   WaveOut wo;
   wo.pos = vb;
-  bool bad = false, far = false;
-  uint4 ca = ld_b128(ru, lane_off), cb = ld_b128(rv, lane_off), cw = ld_b128(rw, lane_off);
-  uint32_t cpa = ld_b32(ru, lane_off - 4), cpb = ld_b32(rv, lane_off - 4);
+  uint4 ca = CSR ? make_uint4(0u, 0u, 0u, 0u) : ld_b128(ru, lane_off);
+  uint4 cb = ld_b128(rv, lane_off), cw = ld_b128(rw, lane_off);
+  uint32_t cpa = CSR ? 0u : ld_b32(ru, lane_off - 4), cpb = ld_b32(rv, lane_off - 4);
   // Every tile's loads are consumed at the END of the iteration that issued them (the empty asm
   // "uses"): the loop header then receives no pending load from either edge and never drains
   // the (rare, variable) flush stores there.
   asm volatile("" ::"v"(ca.x), "v"(cb.x), "v"(cw.x), "v"(cpa), "v"(cpb));
-  for (uint64_t v0 = vb; v0 < ve; v0 += WAVE * 4) {
+  for (uint64_t v0 = vb; v0 < vend; v0 += WAVE * 4) {
     const uint64_t v = v0 + (uint64_t)lane * 4;
     const uint64_t e0 = E0 + v;
-    const uint32_t a[4] = {ca.x, ca.y, ca.z, ca.w}, b[4] = {cb.x, cb.y, cb.z, cb.w}, w[4] = {cw.x, cw.y, cw.z, cw.w};
+    uint32_t a[4] = {ca.x, ca.y, ca.z, ca.w};
+    const uint32_t b[4] = {cb.x, cb.y, cb.z, cb.w}, w[4] = {cw.x, cw.y, cw.z, cw.w};
+    uint32_t pcsr = 0;
+    if (CSR) {
+      csr_tile_rows<false>(eoff, n, R0, R1, (uint32_t)(E0 + v0), s_head[wid], a, w0);
+      // the next tile: its rows and its first window, in flight during this tile
+      R0 = R1;
+      R1 = R2;
+      R2 = trow[min((v0 >> 8) + 3, (T + 255) >> 8)];
+      w0 = csr_win(eoff, n, R0 + 1);
+      pcsr = lane ? wave_shr1(a[3]) : lastu;
+      lastu = __builtin_amdgcn_readlane(a[3], 63);
+    }
     // lane mask of the tile: edges in [e_lo, ve) (32-bit arithmetic, no branches)
     const uint32_t nv = v < ve ? (uint32_t)((ve - v) < 4 ? (ve - v) : 4) : 0u;
     const uint32_t nskip = e0 < e_lo ? (uint32_t)(e_lo - e0) : 0u;
@@ -1820,13 +1977,13 @@ GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, cons
     for (int j = 0; j < 4; ++j) live[j] = ((uint32_t)j < nv) & ((uint32_t)j >= nskip);
     // next tile (out-of-range offsets read 0)
     const uint32_t noff = (uint32_t)(v0 + WAVE * 4 - vb) * 4u + lane_off;
-    ca = ld_b128(ru, noff);
+    if (!CSR) ca = ld_b128(ru, noff);
     cb = ld_b128(rv, noff);
     cw = ld_b128(rw, noff);
-    const uint32_t npa = ld_b32(ru, noff - 4), npb = ld_b32(rv, noff - 4);
+    const uint32_t npa = CSR ? 0u : ld_b32(ru, noff - 4), npb = ld_b32(rv, noff - 4);
     // u < v < n and (u, v) strictly above the previous edge; bitwise (no short-circuit
     // branches: hipcc turns && / || chains into exec-mask control flow here)
-    uint32_t pa = (v == vb) ? bpa : cpa, pb = (v == vb) ? bpb : cpb;
+    uint32_t pa = (v == vb) ? bpa : (CSR ? pcsr : cpa), pb = (v == vb) ? bpb : cpb;
     const uint32_t first = (e0 == 0) ? 1u : 0u;  // edge 0 has no predecessor
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -1873,7 +2030,14 @@ GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t e_lo, uint64_t e_hi, cons
 // add), so the pass costs stream + probes; splitting level 1 here saves a pass over the pending
 // edges.
 // ------------------------------------------------------------------------------------------
-GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__restrict__ eu,
+// CSR: 8 waves per SIMD forced (GHS_FILTER_CSR_W8: 62 VGPRs + 4 spilled; uncapped the row derivation
+// takes it to 70, i.e. 7 blocks per CU — then the grid is sized to one residency wave instead)
+#ifndef GHS_FILTER_CSR_W8
+#define GHS_FILTER_CSR_W8 1
+#endif
+template <bool CSR>
+__global__ __launch_bounds__(BLOCK, (CSR && GHS_FILTER_CSR_W8) ? 8 : GHS_STREAM_WAVES) __attribute__((amdgpu_num_sgpr(72))) void k_filter(uint32_t n, uint64_t e_lo, uint64_t e_hi, const uint32_t *__restrict__ eu,
+                                const uint32_t *__restrict__ eoff, const uint32_t *__restrict__ trow,
                                 const uint32_t *__restrict__ ev, const uint32_t *__restrict__ ew,
                                 const uint64_t *__restrict__ w_range /* [w_lo, w_hi] */,
                                 const uint64_t *__restrict__ giant_bits,
@@ -1889,12 +2053,14 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
   __shared__ WaveStage s_stage[BLOCK / WAVE];
   const uint64_t E0 = e_lo & ~3ull;
   const uint64_t T = e_hi - E0;
-  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
+  // CSR: block ranges of whole 1024-edge tiles, so every wave's 256-edge part starts on the trow grid
+  const uint64_t QA = CSR ? ARCS_PER_BLOCK - 1 : 3;
+  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + QA) & ~QA;
   const uint64_t vb = Q * blockIdx.x;
   const uint64_t ve = (vb + Q < T) ? vb + Q : T;
   const uint64_t eb = E0 + vb;  // first edge of this block
   const uint64_t nbytes = ve > vb ? (ve - vb) * 4 : 0;
-  const __amdgpu_buffer_rsrc_t ru = make_rsrc(eu + eb, nbytes);
+  const __amdgpu_buffer_rsrc_t ru = make_rsrc(CSR ? ev : eu + eb, CSR ? 0 : nbytes);
   const __amdgpu_buffer_rsrc_t rv = make_rsrc(ev + eb, nbytes);
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(ew + eb, nbytes);
   const uint32_t lane_off = threadIdx.x * 16u;
@@ -1903,11 +2069,35 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
   const uint32_t giant = giant_ptr[0];
   bool touch_giant = false;  // a level edge of this block has an end in the giant
   uint64_t nlev = 0, nrem = 0;
-  uint4 ca = ld_b128_nt(ru, lane_off), cb = ld_b128_nt(rv, lane_off), cw = ld_b128_nt(rw, lane_off);
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+  // CSR: the rows of the wave's part of the tile (k_csr_trow's trow: R0 holds its first edge, R1
+  // its end), the next tile's part's (loaded a tile ahead), and this part's first window (prefetched)
+  const uint64_t ntiles = (T + 255) >> 8;
+  auto trow_at = [&](uint64_t t) -> uint32_t { return trow[t < ntiles ? t : ntiles]; };
+  const uint64_t t0w = (vb >> 8) + wid;  // the wave's part of the block's first tile
+  uint32_t R0 = CSR ? trow_at(t0w) : 0u, R1 = CSR ? trow_at(t0w + 1) : 0u;
+  uint32_t N0 = CSR ? trow_at(t0w + 4) : 0u, N1 = CSR ? trow_at(t0w + 5) : 0u;
+  uint32_t w0 = CSR ? csr_win(eoff, n, R0 + 1) : 0u;
+  uint4 ca = CSR ? make_uint4(0u, 0u, 0u, 0u) : ld_b128_nt(ru, lane_off);
+  uint4 cb = ld_b128_nt(rv, lane_off), cw = ld_b128_nt(rw, lane_off);
   for (uint64_t v0 = vb; v0 < ve; v0 += ARCS_PER_BLOCK) {
     const uint64_t v = v0 + (uint64_t)threadIdx.x * 4;
     const uint64_t e0 = E0 + v;
-    const uint32_t a[4] = {ca.x, ca.y, ca.z, ca.w}, b[4] = {cb.x, cb.y, cb.z, cb.w}, w[4] = {cw.x, cw.y, cw.z, cw.w};
+    uint32_t a[4] = {ca.x, ca.y, ca.z, ca.w};
+    const uint32_t b[4] = {cb.x, cb.y, cb.z, cb.w}, w[4] = {cw.x, cw.y, cw.z, cw.w};
+    if (CSR) {
+      const uint32_t r0 = R0, r1 = R1, w = w0;
+      const uint64_t tw = ((v0 + ARCS_PER_BLOCK) >> 8) + wid;  // the wave's part of the next tile
+      R0 = N0;
+      R1 = N1;
+      w0 = csr_win(eoff, n, R0 + 1);  // the next part's window, in flight during this tile
+      N0 = trow_at(tw + 4);
+      N1 = trow_at(tw + 5);
+      const uint64_t vw = v0 + (uint64_t)wid * (WAVE * 4);  // the wave's part (wave-uniform)
+      // the head table lives in the wave's staging area (free between the tiles' stage_write calls),
+      // so the block stays at 20 KiB of LDS: 8 blocks per CU
+      if (vw < ve) csr_tile_rows<true>(eoff, n, r0, r1, (uint32_t)(E0 + vw), s_stage[wid].a, a, w);
+    }
     const uint32_t nv = v < ve ? (uint32_t)((ve - v) < 4 ? (ve - v) : 4) : 0u;
     const uint32_t nskip = e0 < e_lo ? (uint32_t)(e_lo - e0) : 0u;
     bool out[4];
@@ -1947,7 +2137,7 @@ GHS_STREAM_KERNEL void k_filter(uint64_t e_lo, uint64_t e_hi, const uint32_t *__
 #endif
     // next tile (out-of-range offsets read 0)
     const uint32_t noff = (uint32_t)(v0 + ARCS_PER_BLOCK - vb) * 4u + lane_off;
-    ca = ld_b128_nt(ru, noff);
+    if (!CSR) ca = ld_b128_nt(ru, noff);
     cb = ld_b128_nt(rv, noff);
     cw = ld_b128_nt(rw, noff);
 #pragma unroll
@@ -2734,8 +2924,7 @@ __global__ __launch_bounds__(BM_T) void k_wmin(const uint32_t *__restrict__ src,
 // The hot fragments' CONNECT in a bucketed level-first round (one thread each): a fragment's
 // minimum (reduced by k_bucket) is edge eid; the level's labels are resolved roots, so the other
 // end's label is one read. A mutual pair stays a 2-cycle for the jump, as in k_bmin.
-__global__ void k_hot_hook(const uint32_t *__restrict__ hot, const uint64_t *__restrict__ best,
-                           const uint32_t *__restrict__ eu, const uint32_t *__restrict__ ev,
+__global__ void k_hot_hook(const uint32_t *__restrict__ hot, const uint64_t *__restrict__ best, const Ends E,
                            const uint32_t *__restrict__ lab, uint32_t *__restrict__ par, uint8_t *__restrict__ in_mst,
                            unsigned long long *__restrict__ err) {
   if (threadIdx.x >= hot[0]) return;
@@ -2743,7 +2932,7 @@ __global__ void k_hot_hook(const uint32_t *__restrict__ hot, const uint64_t *__r
   const uint64_t k = best[g];
   if (k == KEY_NONE) return;
   const uint32_t eid = (uint32_t)k;
-  const uint32_t la = lab[eu[eid]], lb = lab[ev[eid]];
+  const uint32_t la = lab[end_u(E, eid)], lb = lab[E.v[eid]];
   if (la != g && lb != g) atomicOr(err, 2ull);
   par[g] = la == g ? lb : la;
   in_mst[eid] = 1;
@@ -3751,6 +3940,33 @@ static inline unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Blocks of ONE residency wave of a fixed-grid streaming kernel on the current device (its occupancy
+// in blocks per CU x the CUs), at most cap. A fixed grid past it runs a second, nearly empty wave of
+// blocks at the end: k_select sits at 7 blocks per CU (its SGPRs) and k_level_pass at 6 (its VGPRs),
+// so their 2048-block grids left 256 / 512 blocks to run alone after the rest. Cached per kernel
+// and device (one occupancy query each).
+#ifndef GHS_RESIDENT_GRIDS
+#define GHS_RESIDENT_GRIDS 0
+#endif
+static unsigned resident_grid(const void *kernel, unsigned block, unsigned cap, bool on = GHS_RESIDENT_GRIDS) {
+  if (!on) return cap;
+  static std::mutex mu;
+  static std::unordered_map<uint64_t, unsigned> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return cap;
+  const uint64_t key = (uint64_t)(uintptr_t)kernel * 64 + (uint64_t)dev;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return std::min(it->second, cap);
+  int nb = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, (int)block, 0) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || nb <= 0 || cus <= 0)
+    return cap;
+  const unsigned g = (unsigned)(nb * cus);
+  cache[key] = g;
+  return std::min(g, cap);
+}
+
 
 }  // namespace ghs
 
@@ -3854,6 +4070,9 @@ struct ghs_solver {
   uint32_t n = 0;
   uint64_t m = 0, e_lo = 0, e_hi = 0;
   const uint32_t *eu = nullptr, *ev = nullptr, *ew = nullptr;
+  const uint32_t *eoff = nullptr;  // CSR input (ABI 9): row offsets, eu == nullptr (or the caller's u for gathers)
+  bool csr = false;
+  uint32_t *trow = nullptr;        // CSR: the row of every 256-edge tile of the range (k_select -> k_filter)
   uint8_t *in_mst = nullptr;
   hipStream_t stream = nullptr;
   ghs_config_t cfg{};
@@ -4020,7 +4239,7 @@ static const char *const KERNEL_NAMES[GHS_K_COUNT] = {
     "k_select", "k_filter", "k_level_pass", "k_seed_runs", "k_minedge<IDENT>", "k_minedge<COMPACT>",
     "k_win", "k_hook", "k_jump_ident", "k_jump", "k_select_lb", "k_resolve", "k_giant", "k_scan_counts",
     "k_plan", "k_init", "k_pack_best", "k_unpack_best", "k_round_report", "k_pack_hook", "k_unpack_hook", "k_dense", "k_flag_bits", "k_bucket", "k_bmin", "k_wstarts", "k_wmin", "k_hot_hook",
-    "k_tail_open", "k_tail_round", "k_tail_hook"};
+    "k_tail_open", "k_tail_round", "k_tail_hook", "k_csr_trow"};
 
 struct KtScope {
   ghs_solver *s;
@@ -4051,6 +4270,8 @@ struct KtScope {
   }
 };
 #define KT(kernel, items) KtScope _kt_scope(s, (kernel), (items))
+
+static inline Ends ends_of(const ghs_solver *s) { return Ends{s->eu, s->eoff, s->ev, s->n}; }
 
 static bool solver_cancelled(const ghs_solver *s) {
   return __atomic_load_n(&s->cancel_flag, __ATOMIC_ACQUIRE) ||
@@ -4149,29 +4370,32 @@ static bool bucket_geometry(uint32_t n, uint32_t *bs, uint32_t *nb) {
 constexpr size_t WS_STAGGER = GHS_WS_STAGGER;
 static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs_solver *s, char *base) {
   size_t off = 0;
-  auto carve = [&](size_t bytes) -> char * {
+  // only the vertex-sized arrays (read at the same index by the jumps and hooks) are staggered
+  // (a stagger after every carve grew every workspace by ~60 MB, tiny graphs included)
+  auto carve = [&](size_t bytes, bool stagger = false) -> char * {
     char *p = base ? base + off : nullptr;
-    off = align_up(off + bytes, 256) + WS_STAGGER;
+    off = align_up(off + bytes, 256) + (stagger ? WS_STAGGER : 0);
     return p;
   };
   const size_t N = (size_t)n;
   // a level's edges (+ padding of the regions, + the heavy copy's last block: < T/256 + 2 groups)
   const uint64_t cap = local_edges + 4 * SEG_MAX + local_edges / 256 + 2 * 2048;
   char *p;
-  p = carve(N * 4); if (s) s->lab = (uint32_t *)p;
-  p = carve(N * 4); if (s) s->par = (uint32_t *)p;
-  p = carve(N * 8); if (s) s->best = (uint64_t *)p;
-  p = carve(N * 4); if (s) s->act[0] = (uint32_t *)p;
-  p = carve(N * 4); if (s) s->act[1] = (uint32_t *)p;
+  const bool stg = N * 4 >= (4u << 20);  // small graphs: no stagger at all
+  p = carve(N * 4, stg); if (s) s->lab = (uint32_t *)p;
+  p = carve(N * 4, stg); if (s) s->par = (uint32_t *)p;
+  p = carve(N * 8, stg); if (s) s->best = (uint64_t *)p;
+  p = carve(N * 4, stg); if (s) s->act[0] = (uint32_t *)p;
+  p = carve(N * 4, stg); if (s) s->act[1] = (uint32_t *)p;
   if (local_edges < m) {  // a rank of a multi-rank solve: the dense-level arrays
-    p = carve(N * 4); if (s) s->dlab = (uint32_t *)p;
-    p = carve(N * 4); if (s) s->dpar = (uint32_t *)p;
-    p = carve((N + 64) * 8); if (s) s->dbest = (uint64_t *)p;  // + padding of the reduce-scatter slots
+    p = carve(N * 4, stg); if (s) s->dlab = (uint32_t *)p;
+    p = carve(N * 4, stg); if (s) s->dpar = (uint32_t *)p;
+    p = carve((N + 64) * 8, stg); if (s) s->dbest = (uint64_t *)p;  // + padding of the reduce-scatter slots
     const size_t W = (N + 63) / 64;
     p = carve(W * 8); if (s) s->drank_bits = (uint64_t *)p;
     p = carve(W * 4); if (s) s->drank_wpre = (uint32_t *)p;
     p = carve(((W + BLOCK - 1) / BLOCK) * 4 + 4); if (s) s->drank_cpre = (uint32_t *)p;
-    p = carve(N * 4); if (s) s->dvtx = (uint32_t *)p;
+    p = carve(N * 4, stg); if (s) s->dvtx = (uint32_t *)p;
   }
   p = carve(N + 1); if (s) s->flags = (uint8_t *)p;  // + the multi-rank error byte flags[n]
   p = carve(((N + 127) / 128) * 16 + 16); if (s) s->bits = (uint64_t *)p;
@@ -4199,8 +4423,9 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
   }
   if (s) s->cap_arcs = cap;
   p = carve(C_COUNT * sizeof(unsigned long long)); if (s) s->cnt = (unsigned long long *)p;
+  p = carve((local_edges / 256 + 8) * 4); if (s) s->trow = (uint32_t *)p;  // CSR: each 256-edge tile's row
   if (local_edges == m) {  // one rank: the LDS tail's arrays (its records go to the idle edge buffer)
-    p = carve(N * 4); if (s) s->tail.dmap = (uint32_t *)p;
+    p = carve(N * 4, stg); if (s) s->tail.dmap = (uint32_t *)p;
     p = carve((size_t)TAIL_G * TAIL_MAX * 8); if (s) s->tail.partial = (uint64_t *)p;
     p = carve((size_t)TAIL_G * TAIL_MAX * 2); if (s) s->tail.poth = (uint16_t *)p;
     for (int b = 0; b < 2; ++b) {
@@ -4330,7 +4555,7 @@ static int plan_levels_enqueue(ghs_solver *s) {
   {
     KT(GHS_K_PLAN, ns);
     if (ns_all)
-      k_sample_weights<<<grid_for(ns_all, 256, 256), 256, 0, s->stream>>>(s->m, s->eu, s->ev, s->ew, ns_all, s->sample);
+      k_sample_weights<<<grid_for(ns_all, 256, 256), 256, 0, s->stream>>>(s->m, ends_of(s), s->ew, ns_all, s->sample);
     k_plan<<<1, 1024, 0, s->stream>>>(s->sample, ns_all, ns, s->n, s->m, L, level1_auto(s->cfg, s->n, s->m),
                                       s->cfg.level_growth, s->d_thr);
   }
@@ -4411,14 +4636,20 @@ static int open_level(ghs_solver *s, bool async_open = false) {
   const uint64_t TC = s->e_hi > s->e_lo ? s->e_hi - (s->e_lo & ~3ull) : 0;  // canonical passes stream [e_lo & ~3, e_hi)
   if (first) {
     // SELECT over the canonical list: level-0 edges only (validates the list)
-    G = grid_for(TC, ARCS_PER_BLOCK, s->seg_g);
+    auto sel = s->csr ? k_select<true> : k_select<false>;
+    G = grid_for(TC, ARCS_PER_BLOCK, resident_grid((const void *)sel, BLOCK, s->seg_g));
     if (TC) {
+      if (s->csr) {  // CSR: every 256-edge tile's row (and the offsets' validation) for both passes
+        KT(GHS_K_CSR_TROW, s->n);
+        k_csr_trow<<<grid_for(s->n, 256, 8192), 256, 0, st>>>(s->eoff, s->n, s->m, s->e_lo & ~3ull, s->e_hi, s->trow,
+                                                             s->cnt + C_ERR);
+      }
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[0], st));
       {
         KT(GHS_K_SELECT, TC);
-        k_select<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range + 1, Y.src, Y.dst, Y.key,
-                                      Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR,
-                                      s->wstart ? s->d_thr + PLAN_LOCAL : nullptr, s->bk_bs, s->cnt + C_LONG);
+        sel<<<G, BLOCK, 0, st>>>(s->n, s->m, s->e_lo, s->e_hi, s->eu, s->eoff, s->ev, s->ew, d_range + 1, Y.src, Y.dst,
+                                 Y.key, Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR,
+                                 s->wstart ? s->d_thr + PLAN_LOCAL : nullptr, s->bk_bs, s->cnt + C_LONG, s->trow);
       }
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[1], st));
       GHS_HIP_CHECK(hipGetLastError());
@@ -4436,12 +4667,14 @@ static int open_level(ghs_solver *s, bool async_open = false) {
     if (!s->pending_built) {
       // FILTER + level split over the canonical list once level 0 is complete: level-1 edges
       // not inside one fragment -> Y; heavier edges not inside the giant -> pending (rem[rout])
-      G = grid_for(TC, ARCS_PER_BLOCK, s->seg_g);
+      auto filt = s->csr ? k_filter<true> : k_filter<false>;
+      G = grid_for(TC, ARCS_PER_BLOCK,
+                   resident_grid((const void *)filt, BLOCK, s->seg_g, GHS_RESIDENT_GRIDS || (s->csr && !GHS_FILTER_CSR_W8)));
       if (TC) {
         GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[2], st));
         {
           KT(GHS_K_FILTER, TC);
-          k_filter<<<G, BLOCK, 0, st>>>(s->e_lo, s->e_hi, s->eu, s->ev, s->ew, d_range, s->bits, s->giant, s->lab,
+          filt<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->eoff, s->trow, s->ev, s->ew, d_range, s->bits, s->giant, s->lab,
                                         Y.src, Y.dst, Y.key, Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key,
                                         RO.seg_start, RO.seg_count, mark);
         }
@@ -4462,7 +4695,7 @@ static int open_level(ghs_solver *s, bool async_open = false) {
     } else {
       // split the pending edges (total on the device): this level's inter-fragment edges -> Y;
       // heavier survivors -> RO regions. Fixed grid: block b owns 1/seg_g of the virtual range.
-      G = s->lp_g;
+      G = resident_grid((const void *)k_level_pass, BLOCK, s->lp_g);
       SegView in{RI.seg_start, RI.seg_prefix, s->rem_nseg};
       {
       KT(GHS_K_LEVEL_PASS, s->rem_total);
@@ -4716,7 +4949,7 @@ static void enqueue_bmin(ghs_solver *s, const uint32_t *a, const uint32_t *b, co
   }
   if (hot) {
     KT(GHS_K_HOT_HOOK, 0);
-    k_hot_hook<<<1, HOT_K, 0, s->stream>>>(hot, s->best, s->eu, s->ev, s->lab, s->par, s->in_mst, s->cnt + C_ERR);
+    k_hot_hook<<<1, HOT_K, 0, s->stream>>>(hot, s->best, ends_of(s), s->lab, s->par, s->in_mst, s->cnt + C_ERR);
   }
 }
 
@@ -4865,13 +5098,13 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
       }
       GHS_HIP_CHECK(hipGetLastError());
       KT(GHS_K_HOOK, 0);
-      k_hook<<<gh, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
+      k_hook<<<gh, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, ends_of(s), s->par, s->in_mst,
                                          s->cnt + C_WEIGHT, s->cnt + C_ERR, nullptr, 0, nullptr, nullptr, false,
                                          s->cnt + C_LIVE, (uint32_t)s->e_lo, (uint32_t)s->e_hi, nullptr, DenseRank());
     } else {
       const ArcBuf *sb = s->scan_pending ? s->scan_buf : nullptr;
       KT(GHS_K_HOOK, 0);
-      k_hook<<<gh, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, s->eu, s->ev, s->par, s->in_mst,
+      k_hook<<<gh, BLOCK, 0, s->stream>>>(act, d_nact, s->best, s->lab, ends_of(s), s->par, s->in_mst,
                                          s->cnt + C_WEIGHT, s->cnt + C_ERR, sb ? sb->seg_count : nullptr, s->cmp_g,
                                          sb ? sb->seg_prefix : nullptr, s->cnt + C_LIVE, s->level_round == 0, nullptr,
                                          (uint32_t)s->e_lo, (uint32_t)s->e_hi, s->level_dense ? s->vlab : nullptr,
@@ -4938,8 +5171,12 @@ static int wait_slot(ghs_solver *s, const RoundSlot *hs, unsigned long long seq,
   unsigned spins = 0;
   bool quiet = true;
   auto last_query = t0;
+  bool retried = false;  // the report's seq landed before a field: counted once per report
   while (!slot_read(hs, seq, out)) {
-    if (__atomic_load_n(&hs->seq, __ATOMIC_RELAXED) == seq) __atomic_fetch_add(&g_slot_retries, 1, __ATOMIC_RELAXED);
+    if (!retried && __atomic_load_n(&hs->seq, __ATOMIC_RELAXED) == seq) {
+      retried = true;
+      __atomic_fetch_add(&g_slot_retries, 1, __ATOMIC_RELAXED);
+    }
     if ((spins & 255) == 0 && solver_cancelled(s)) GHS_FAIL(GHS_E_STATE, "cancelled: another rank of the solve failed");
     if ((++spins & 255) == 0 && quiet)
       quiet = std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(SLOT_QUIET_MS);
@@ -5102,14 +5339,15 @@ static int run_tail(ghs_solver *s, uint64_t prev_in) {
     batch = TAIL_BATCH_NEXT;
     for (; r <= last; ++r) {
       s->round = round0 + r;  // the profile's round index of these launches
-      {
-        KT(GHS_K_TAIL_ROUND, 0);
-        k_tail_round<<<TAIL_G, TAIL_T, 0, st>>>(tb, r, act0, s->lab, s->cnt, err);
-      }
-      if (r < TAIL_ROUNDS_MAX) {
+      // round r - 1's hooks, unless the open's (launched above): a batch ends with a round, not with
+      // its hook kernel, so the round that finishes the level is not followed by a no-op hook launch
+      // when it closes its batch (the hook comes first in the next batch otherwise)
+      if (r > 1) {
         KT(GHS_K_TAIL_HOOK, 0);
-        k_tail_hook<<<hook_g, 256, 0, st>>>(tb, r, s->in_mst, TAIL_G, err);
+        k_tail_hook<<<hook_g, 256, 0, st>>>(tb, r - 1, s->in_mst, TAIL_G, err);
       }
+      KT(GHS_K_TAIL_ROUND, 0);
+      k_tail_round<<<TAIL_G, TAIL_T, 0, st>>>(tb, r, act0, s->lab, s->cnt, err);
     }
     GHS_HIP_CHECK(hipGetLastError());
     const unsigned long long seq = ++s->res->seq;
@@ -5328,17 +5566,21 @@ static int solver_begin(ghs_solver *s) {
 // pool: the one-shot entry point's process-wide host resources (nullptr: the handle owns its own).
 // Passed explicitly, not through a global, so concurrent creators (the multi-rank drivers' threads)
 // never adopt another caller's pinned counters.
-static int solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
-                         uint64_t e_lo, uint64_t e_hi, const ghs_config_t *cfg, void *d_workspace,
+// d_off != nullptr: CSR input (ABI 9) — the row offsets stream in place of u; d_u may then be NULL
+// (gathers of u by edge id search the offsets) or the caller's u (used for those gathers only)
+static int solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_off, const uint32_t *d_v,
+                         const uint32_t *d_w, uint64_t e_lo, uint64_t e_hi, const ghs_config_t *cfg, void *d_workspace,
                          size_t workspace_bytes, uint8_t *d_in_mst, void *stream, HostRes *pool, ghs_solver_t **out) {
   if (!out) GHS_FAIL(GHS_E_ARG, "out is NULL");
   *out = nullptr;
   if (m >= (1ull << 31)) GHS_FAIL(GHS_E_ARG, "m must be < 2^31");
   if (e_lo > e_hi || e_hi > m) GHS_FAIL(GHS_E_ARG, "bad edge range");
   if (cfg && (cfg->num_ranks < 1 || cfg->num_ranks > GHS_MAX_RANKS)) GHS_FAIL(GHS_E_ARG, "num_ranks must be in [1, GHS_MAX_RANKS]");
-  if (m && (!d_u || !d_v || !d_w || !d_in_mst)) GHS_FAIL(GHS_E_ARG, "d_u/d_v/d_w/d_in_mst is NULL");
-  if ((((uintptr_t)d_u) | ((uintptr_t)d_v) | ((uintptr_t)d_w)) & 15)
+  if (m && ((!d_u && !d_off) || !d_v || !d_w || !d_in_mst)) GHS_FAIL(GHS_E_ARG, "d_u (d_off)/d_v/d_w/d_in_mst is NULL");
+  if (d_off && m && n == 0) GHS_FAIL(GHS_E_ARG, "CSR input with edges needs n >= 1");
+  if ((((uintptr_t)(d_off ? nullptr : d_u)) | ((uintptr_t)d_v) | ((uintptr_t)d_w)) & 15)
     GHS_FAIL(GHS_E_ARG, "d_u/d_v/d_w must be 16-byte aligned");
+  if (((uintptr_t)d_off) & 3) GHS_FAIL(GHS_E_ARG, "d_off must be 4-byte aligned");
   const size_t need = workspace_layout(n, m, e_hi - e_lo, nullptr, nullptr);
   if (!d_workspace || workspace_bytes < need)
     GHS_FAIL(GHS_E_NOMEM, "workspace too small: need " + std::to_string(need) + " bytes");
@@ -5349,6 +5591,7 @@ static int solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint
   ghs_solver *s = new ghs_solver();
   s->n = n; s->m = m; s->e_lo = e_lo; s->e_hi = e_hi;
   s->eu = d_u; s->ev = d_v; s->ew = d_w;
+  s->eoff = d_off; s->csr = d_off != nullptr;
   s->in_mst = d_in_mst; s->stream = (hipStream_t)stream;
   if (cfg) s->cfg = *cfg; else default_config(&s->cfg);
   // path options come from the caller's config only (ABI 5): the library reads no environment
@@ -5409,8 +5652,16 @@ static int solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint
 int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
                       uint64_t e_lo, uint64_t e_hi, const ghs_config_t *cfg, void *d_workspace,
                       size_t workspace_bytes, uint8_t *d_in_mst, void *stream, ghs_solver_t **out) {
-  return solver_create(n, m, d_u, d_v, d_w, e_lo, e_hi, cfg, d_workspace, workspace_bytes, d_in_mst, stream, nullptr,
-                       out);
+  return solver_create(n, m, d_u, nullptr, d_v, d_w, e_lo, e_hi, cfg, d_workspace, workspace_bytes, d_in_mst, stream,
+                       nullptr, out);
+}
+
+int ghs_solver_create_csr(uint32_t n, uint64_t m, const uint32_t *d_off, const uint32_t *d_u, const uint32_t *d_v,
+                          const uint32_t *d_w, uint64_t e_lo, uint64_t e_hi, const ghs_config_t *cfg, void *d_workspace,
+                          size_t workspace_bytes, uint8_t *d_in_mst, void *stream, ghs_solver_t **out) {
+  if (m && !d_off) GHS_FAIL(GHS_E_ARG, "d_off is NULL");
+  return solver_create(n, m, d_u, d_off ? d_off : nullptr, d_v, d_w, e_lo, e_hi, cfg, d_workspace, workspace_bytes,
+                       d_in_mst, stream, nullptr, out);
 }
 
 }  // extern "C"
@@ -5420,7 +5671,7 @@ int ghs_solver_create_pooled(uint32_t n, uint64_t m, const uint32_t *d_u, const 
                              size_t workspace_bytes, uint8_t *d_in_mst, void *stream, void *hostres,
                              ghs_solver_t **out) {
   if (!hostres) GHS_FAIL(GHS_E_ARG, "host resources are NULL");
-  return solver_create(n, m, d_u, d_v, d_w, e_lo, e_hi, cfg, d_workspace, workspace_bytes, d_in_mst, stream,
+  return solver_create(n, m, d_u, nullptr, d_v, d_w, e_lo, e_hi, cfg, d_workspace, workspace_bytes, d_in_mst, stream,
                        static_cast<HostRes *>(hostres), out);
 }
 
@@ -5633,7 +5884,7 @@ int ghs_solver_hook_owner(ghs_solver_t *s, uint32_t rank, uint64_t per, uint64_t
   const uint64_t lo = (uint64_t)rank * per, hi = lo + per;
   if (per) {
     KT(GHS_K_PACK_HOOK, per);
-    k_hook_owner<<<grid_for(per, 256, 16384), 256, 0, s->stream>>>(s->best, lo, hi, s->eu, s->ev, s->vlab,
+    k_hook_owner<<<grid_for(per, 256, 16384), 256, 0, s->stream>>>(s->best, lo, hi, ends_of(s), s->vlab,
                                                                    dense_rank_of(s), d_pairs, s->cnt + C_ERR);
     GHS_HIP_CHECK(hipGetLastError());
   }
@@ -5830,7 +6081,7 @@ int ghs_solver_reset(ghs_solver_t *s) {
   // a fresh round state over the same inputs, workspace, knobs and host resources
   ghs_solver t;
   t.n = s->n; t.m = s->m; t.e_lo = s->e_lo; t.e_hi = s->e_hi;
-  t.eu = s->eu; t.ev = s->ev; t.ew = s->ew;
+  t.eu = s->eu; t.ev = s->ev; t.ew = s->ew; t.eoff = s->eoff; t.csr = s->csr;
   t.in_mst = s->in_mst; t.stream = s->stream; t.cfg = s->cfg;
   t.debug = s->debug; t.lookahead = s->lookahead; t.seed_runs = s->seed_runs; t.dedup_max = s->dedup_max;
   t.windowed = s->windowed;
@@ -5866,9 +6117,10 @@ int ghs_solver_destroy(ghs_solver_t *s) {
   return GHS_OK;
 }
 
-int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
-                   const ghs_config_t *cfg, void *d_workspace, size_t workspace_bytes, uint8_t *d_in_mst, void *stream,
-                   ghs_result_t *result, ghs_round_stats_t *stats) {
+// the one-shot solve of ghs_mst_device / ghs_mst_device_csr
+static int mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_off, const uint32_t *d_v,
+                      const uint32_t *d_w, const ghs_config_t *cfg, void *d_workspace, size_t workspace_bytes,
+                      uint8_t *d_in_mst, void *stream, ghs_result_t *result, ghs_round_stats_t *stats) {
   std::lock_guard<std::mutex> lock(g_mutex);
   ghs_solver_t *s = nullptr;
   ghs_config_t c;
@@ -5877,7 +6129,7 @@ int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *
   int rc = GHS_OK;
   HostRes *pool = pooled_res(&rc);
   if (!pool) return rc;
-  rc = solver_create(n, m, d_u, d_v, d_w, 0, m, &c, d_workspace, workspace_bytes, d_in_mst, stream, pool, &s);
+  rc = solver_create(n, m, d_u, d_off, d_v, d_w, 0, m, &c, d_workspace, workspace_bytes, d_in_mst, stream, pool, &s);
   if (rc) return rc;
   while (!rc && s->phase != 2) {
     if (!s->level_open) {
@@ -5893,6 +6145,19 @@ int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *
   if (!rc) rc = ghs_solver_finish(s, result, stats);
   ghs_solver_destroy(s);
   return rc;
+}
+
+int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
+                   const ghs_config_t *cfg, void *d_workspace, size_t workspace_bytes, uint8_t *d_in_mst, void *stream,
+                   ghs_result_t *result, ghs_round_stats_t *stats) {
+  return mst_device(n, m, d_u, nullptr, d_v, d_w, cfg, d_workspace, workspace_bytes, d_in_mst, stream, result, stats);
+}
+
+int ghs_mst_device_csr(uint32_t n, uint64_t m, const uint32_t *d_off, const uint32_t *d_u, const uint32_t *d_v,
+                       const uint32_t *d_w, const ghs_config_t *cfg, void *d_workspace, size_t workspace_bytes,
+                       uint8_t *d_in_mst, void *stream, ghs_result_t *result, ghs_round_stats_t *stats) {
+  if (m && !d_off) GHS_FAIL(GHS_E_ARG, "d_off is NULL");
+  return mst_device(n, m, d_u, d_off, d_v, d_w, cfg, d_workspace, workspace_bytes, d_in_mst, stream, result, stats);
 }
 
 }  // extern "C"

@@ -80,6 +80,9 @@ int ghs_solver_create_pooled(uint32_t n, uint64_t m, const uint32_t *d_u, const 
                              size_t workspace_bytes, uint8_t *d_in_mst, void *stream, void *hostres,
                              ghs_solver_t **out);
 
+// ghs_flags_to_eids' cached temporaries (ingest.hip), freed by ghs_release_cache (multi.hip)
+void ghs_release_eid_temps();
+
 #define GHS_HIP_CHECK(expr)                                                                     \
   do {                                                                                          \
     hipError_t _e = (expr);                                                                     \

@@ -45,6 +45,18 @@ __global__ void k_check_canonical(uint32_t n, uint64_t m, const uint32_t *__rest
   }
 }
 
+// CSR row offsets of a canonical list (ABI 9, ghs_csr_offsets): off[r] = the first edge of row r.
+// Edge e writes the offsets of the rows (u[e - 1], u[e]] (every row from 0 for e = 0, up to n for
+// e = m): each row's entry is written exactly once, by the edge that starts it or by the first
+// edge past it when it is empty. u ascending is required (the solve validates the offsets).
+__global__ void k_csr_offsets(uint32_t n, uint64_t m, const uint32_t *__restrict__ u, uint32_t *__restrict__ off) {
+  for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e <= m; e += (uint64_t)gridDim.x * blockDim.x) {
+    const int64_t lo = e == 0 ? -1 : (int64_t)u[e - 1];
+    const int64_t hi = e == m ? (int64_t)n : (int64_t)min(u[e], n);
+    for (int64_t r = lo + 1; r <= hi; ++r) off[r] = (uint32_t)e;
+  }
+}
+
 // ---- R-MAT ---------------------------------------------------------------------------------
 // Graph500 quadrant probabilities as exact integer thresholds on a uniform 32-bit draw.
 constexpr uint32_t RMAT_TA = (uint32_t)((57ull << 32) / 100);
@@ -238,6 +250,14 @@ int ghs_check_canonical(uint32_t n, uint64_t m, const uint32_t *d_u, const uint3
   return GHS_OK;
 }
 
+int ghs_csr_offsets(uint32_t n, uint64_t m, const uint32_t *d_u, uint32_t *d_off, void *stream) {
+  if (!d_off || (m && !d_u)) GHS_FAIL(GHS_E_ARG, "NULL pointer");
+  if (m >= (1ull << 31)) GHS_FAIL(GHS_E_ARG, "m must be < 2^31");
+  k_csr_offsets<<<grid_cap(m + 1, 256, 16384), 256, 0, (hipStream_t)stream>>>(n, m, d_u, d_off);
+  GHS_HIP_CHECK(hipGetLastError());
+  return GHS_OK;
+}
+
 size_t ghs_rmat_temp_bytes(uint32_t scale, uint32_t edgefactor) {
   const uint64_t T = (uint64_t)edgefactor << scale;
   size_t sort_b = 0;
@@ -283,6 +303,37 @@ struct FlagOne {
   __host__ __device__ uint32_t operator()(uint8_t f) const { return f ? 1u : 0u; }
 };
 
+}  // extern "C"
+
+// ghs_flags_to_eids' per-device temporary storage (grown on demand), freed by ghs_release_cache
+// (it used to be held until the process ended, outside torch's allocator's view)
+namespace {
+struct EidTemp {
+  void *p = nullptr;
+  size_t bytes = 0;
+  uint32_t *h_cnt = nullptr;  // pinned: the selected count
+  uint32_t *d_cnt = nullptr;
+};
+std::mutex g_eid_mu;
+std::unordered_map<int, EidTemp> g_eid_temps;
+}  // namespace
+
+void ghs_release_eid_temps() {
+  std::lock_guard<std::mutex> lock(g_eid_mu);
+  int cur = 0;
+  const bool have = hipGetDevice(&cur) == hipSuccess;
+  for (auto &kv : g_eid_temps) {
+    (void)hipSetDevice(kv.first);
+    if (kv.second.p) (void)hipFree(kv.second.p);
+    if (kv.second.d_cnt) (void)hipFree(kv.second.d_cnt);
+    if (kv.second.h_cnt) (void)hipHostFree(kv.second.h_cnt);
+  }
+  g_eid_temps.clear();
+  if (have) (void)hipSetDevice(cur);
+}
+
+extern "C" {
+
 // The MSF edge ids of a flag range (a rank's own range for collect_results,
 // ghs_implementation_mpi.py:760-779): rocPRIM's flagged select over a counting input. Its temporary
 // storage is kept per device (grown on demand); the count comes back through pinned memory.
@@ -292,18 +343,10 @@ int ghs_flags_to_eids(const uint8_t *d_in_mst, uint64_t lo, uint64_t hi, uint32_
   if (hi < lo || hi >= (1ull << 32)) GHS_FAIL(GHS_E_ARG, "bad range (need lo <= hi < 2^32)");
   *count = 0;
   if (hi == lo) return GHS_OK;
-  struct Temp {
-    void *p = nullptr;
-    size_t bytes = 0;
-    uint32_t *h_cnt = nullptr;  // pinned: the selected count
-    uint32_t *d_cnt = nullptr;
-  };
-  static std::mutex mu;
-  static std::unordered_map<int, Temp> temps;
-  std::lock_guard<std::mutex> lock(mu);
+  std::lock_guard<std::mutex> lock(g_eid_mu);
   int dev = 0;
   GHS_HIP_CHECK(hipGetDevice(&dev));
-  Temp &t = temps[dev];
+  EidTemp &t = g_eid_temps[dev];
   hipStream_t st = (hipStream_t)stream;
   const size_t N = (size_t)(hi - lo);
   rocprim::counting_iterator<uint32_t> in((uint32_t)lo);

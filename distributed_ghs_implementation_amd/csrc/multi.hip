@@ -807,5 +807,6 @@ extern "C" int ghs_release_cache(void) {
   cache_free(g_drv);
   g_drv = nullptr;
   if (have) (void)hipSetDevice(prev);
+  ghs_release_eid_temps();
   return GHS_OK;
 }

@@ -25,19 +25,37 @@ def _stream():
 
 
 class DeviceEdges:
-    """Canonical edge list in HBM: n, u/v/w as int32 tensors holding uint32 bit patterns."""
+    """Canonical edge list in HBM: n, u/v/w as int32 tensors holding uint32 bit patterns. `off`
+    (ABI 9, optional): the CSR row offsets of the same list (n + 1 entries, `with_csr()`); an
+    engine built with csr=True streams (off, v, w) — 8 B per edge instead of 12 — and u may then
+    be dropped (`csr_only()`)."""
 
-    def __init__(self, n, u, v, w):
+    def __init__(self, n, u, v, w, off=None):
         self.n = int(n)
         self.u, self.v, self.w = u, v, w
+        self.off = off
 
     @property
     def m(self):
-        return int(self.u.numel())
+        return int(self.v.numel())
+
+    def with_csr(self):
+        """Add the CSR row offsets (built on the device from the sorted u)."""
+        if self.off is None:
+            L = _native.load()
+            off = torch.empty(self.n + 1, dtype=torch.int32, device=self.device)
+            _native.check(L.ghs_csr_offsets(self.n, self.m, _ptr(self.u), _ptr(off), _stream()))
+            self.off = off
+        return self
+
+    def csr_only(self):
+        """The CSR form alone (u released): off, v, w."""
+        self.with_csr()
+        return DeviceEdges(self.n, None, self.v, self.w, self.off)
 
     @property
     def device(self):
-        return self.u.device
+        return self.v.device
 
     @classmethod
     def from_host(cls, graph, device="cuda"):
@@ -46,9 +64,17 @@ class DeviceEdges:
             return torch.from_numpy(a.view("int32").copy()).to(device)
         return cls(graph.n, dev(graph.u), dev(graph.v), dev(graph.w))
 
+    def u_host(self):
+        """u as a host uint32 array (expanded from the offsets for a CSR-only list)."""
+        import numpy as np
+        if self.u is not None:
+            return self.u.cpu().numpy().view("uint32")
+        off = self.off.cpu().numpy().view("uint32").astype(np.int64)
+        return np.repeat(np.arange(self.n, dtype=np.uint32), np.diff(off))
+
     def to_host(self):
         from .graph import CanonicalGraph
-        return CanonicalGraph(self.n, self.u.cpu().numpy().view("uint32"), self.v.cpu().numpy().view("uint32"),
+        return CanonicalGraph(self.n, self.u_host(), self.v.cpu().numpy().view("uint32"),
                               self.w.cpu().numpy().view("uint32"))
 
 
@@ -96,9 +122,10 @@ def edge_range(m, rank, world):
 
 
 class DeviceMST:
-    """Preallocated single-GPU engine for one DeviceEdges graph (or one rank's edge range)."""
+    """Preallocated single-GPU engine for one DeviceEdges graph (or one rank's edge range).
+    csr=None: the CSR entry (ghs_mst_device_csr) whenever the edges carry offsets."""
 
-    def __init__(self, edges, e_lo=0, e_hi=None, config=None):
+    def __init__(self, edges, e_lo=0, e_hi=None, config=None, csr=None):
         L = self.L = _native.load()
         _native.require_gpu()
         self.edges = edges
@@ -110,15 +137,23 @@ class DeviceMST:
         self.ws_bytes = int(L.ghs_workspace_bytes(n, m, self.e_hi - self.e_lo))
         self.ws = torch.empty(max(self.ws_bytes, 256), dtype=torch.uint8, device=dev)
         self.in_mst = torch.zeros(max(m, 1), dtype=torch.uint8, device=dev)
+        self.csr = (edges.off is not None) if csr is None else bool(csr)
+        if self.csr:
+            edges.with_csr()
 
     def run(self):
         """Canonical edges (HBM) -> in_mst flags + totals. Returns (Result, [round stats])."""
         e = self.edges
         res = _native.Result()
         stats = (_native.RoundStats * _native.GHS_MAX_ROUND_STATS)()
-        _native.check(self.L.ghs_mst_device(e.n, e.m, _ptr(e.u), _ptr(e.v), _ptr(e.w), ctypes.byref(self.config),
-                                            _ptr(self.ws), self.ws_bytes, _ptr(self.in_mst), _stream(),
-                                            ctypes.byref(res), stats))
+        if self.csr:
+            _native.check(self.L.ghs_mst_device_csr(e.n, e.m, _ptr(e.off), _ptr(e.u), _ptr(e.v), _ptr(e.w),
+                                                    ctypes.byref(self.config), _ptr(self.ws), self.ws_bytes,
+                                                    _ptr(self.in_mst), _stream(), ctypes.byref(res), stats))
+        else:
+            _native.check(self.L.ghs_mst_device(e.n, e.m, _ptr(e.u), _ptr(e.v), _ptr(e.w), ctypes.byref(self.config),
+                                                _ptr(self.ws), self.ws_bytes, _ptr(self.in_mst), _stream(),
+                                                ctypes.byref(res), stats))
         return res, _native.RoundStatsList(stats, res.num_stats)
 
     def in_mst_host(self):

@@ -44,9 +44,14 @@ class HipStepper:
         L = self.L = engine.L
         ed = engine.edges
         h = ctypes.c_void_p(0)
-        _native.check(L.ghs_solver_create(ed.n, ed.m, _ptr(ed.u), _ptr(ed.v), _ptr(ed.w), engine.e_lo, engine.e_hi,
-                                          ctypes.byref(engine.config), _ptr(engine.ws), engine.ws_bytes,
-                                          _ptr(engine.in_mst), _stream(), ctypes.byref(h)))
+        if getattr(engine, "csr", False):  # ABI 9: the rank streams (off, v, w)
+            _native.check(L.ghs_solver_create_csr(ed.n, ed.m, _ptr(ed.off), _ptr(ed.u), _ptr(ed.v), _ptr(ed.w),
+                                                  engine.e_lo, engine.e_hi, ctypes.byref(engine.config), _ptr(engine.ws),
+                                                  engine.ws_bytes, _ptr(engine.in_mst), _stream(), ctypes.byref(h)))
+        else:
+            _native.check(L.ghs_solver_create(ed.n, ed.m, _ptr(ed.u), _ptr(ed.v), _ptr(ed.w), engine.e_lo, engine.e_hi,
+                                              ctypes.byref(engine.config), _ptr(engine.ws), engine.ws_bytes,
+                                              _ptr(engine.in_mst), _stream(), ctypes.byref(h)))
         self.h = h
         self.dense = torch.empty(max(ed.n, 1), dtype=torch.int64, device=ed.device)
         self.dense_hook = torch.empty(max(ed.n, 1), dtype=torch.int32, device=ed.device)

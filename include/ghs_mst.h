@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GHS_MST_ABI_VERSION 8
+#define GHS_MST_ABI_VERSION 9
 
 #define GHS_OK 0
 #define GHS_NEED_EXCHANGE 1   /* ghs_solver_minedge on a multi-rank solver opened a level: OR-combine
@@ -181,7 +181,8 @@ int ghs_mst_multi(uint32_t n, uint64_t m, const uint32_t *u, const uint32_t *v, 
  * devices, ranks, n, m); a later call of the same shape allocates nothing (ghs_result_t.reused = 1),
  * a call of another shape or a failed call frees it first. Without the option (ABI 8 default) a
  * call frees its state before returning. ghs_release_cache frees it now (device memory back to the
- * caller; safe to call at any time outside a driver call). */
+ * caller; safe to call at any time outside a driver call), and (ABI 9) ghs_flags_to_eids' cached
+ * temporary storage with it. */
 int ghs_release_cache(void);
 /* ABI 8: the MSF edge ids of the flag range [lo, hi) in order — d_eids[k] = the k-th e with
  * d_in_mst[e] != 0 (uint32; room for `capacity` ids), *count (host) = how many — on the device
@@ -209,6 +210,20 @@ size_t ghs_workspace_bytes(uint32_t n, uint64_t m, uint64_t local_edges);
 int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
                    const ghs_config_t *cfg, void *d_workspace, size_t workspace_bytes, uint8_t *d_in_mst,
                    void *stream, ghs_result_t *result, ghs_round_stats_t *stats);
+
+/* ABI 9: the same canonical list in CSR form — the north_star's "CSR edge list in HBM" and the
+ * reference's per-node neighbour files (create_graph_files.py:56-74: node u lists its neighbours)
+ * with each edge stored once at its smaller end: d_off = n + 1 uint32 row offsets (d_off[0] = 0,
+ * nondecreasing, d_off[n] = m), edge e of row u (d_off[u] <= e < d_off[u + 1]) joins u and d_v[e]
+ * with weight d_w[e]; d_v strictly ascending inside a row, u < d_v[e] < n. eid = e as in the COO
+ * form (same keys, same MSF flags). The streaming passes read 8 B per edge (+ 4 B per row) instead
+ * of 12. d_u may be NULL, or the caller's expanded u (then used only for gathers of u by edge id,
+ * which otherwise search d_off). The offsets are validated with the rest (GHS_E_NONCANON). */
+int ghs_mst_device_csr(uint32_t n, uint64_t m, const uint32_t *d_off, const uint32_t *d_u, const uint32_t *d_v,
+                       const uint32_t *d_w, const ghs_config_t *cfg, void *d_workspace, size_t workspace_bytes,
+                       uint8_t *d_in_mst, void *stream, ghs_result_t *result, ghs_round_stats_t *stats);
+/* d_off (n + 1 uint32) from a canonical COO list's d_u (u ascending), on the device */
+int ghs_csr_offsets(uint32_t n, uint64_t m, const uint32_t *d_u, uint32_t *d_off, void *stream);
 
 /* device-side canonicity check: *ok = 1 iff u < v < n and (u, v) strictly ascending */
 int ghs_check_canonical(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, void *stream, int *ok);
@@ -240,6 +255,10 @@ typedef struct ghs_solver ghs_solver_t;
 int ghs_solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *d_v, const uint32_t *d_w,
                       uint64_t e_lo, uint64_t e_hi, const ghs_config_t *cfg, void *d_workspace,
                       size_t workspace_bytes, uint8_t *d_in_mst, void *stream, ghs_solver_t **out);
+/* ABI 9: a rank of the same loop over the CSR form (d_off, optional d_u; see ghs_mst_device_csr) */
+int ghs_solver_create_csr(uint32_t n, uint64_t m, const uint32_t *d_off, const uint32_t *d_u, const uint32_t *d_v,
+                          const uint32_t *d_w, uint64_t e_lo, uint64_t e_hi, const ghs_config_t *cfg, void *d_workspace,
+                          size_t workspace_bytes, uint8_t *d_in_mst, void *stream, ghs_solver_t **out);
 /* runs the min-edge kernel; *num_active = fragments whose best slot must be all-reduced */
 int ghs_solver_minedge(ghs_solver_t *h, uint64_t *num_active);
 /* the flag array to OR-combine (uint8 MAX all-reduce) after GHS_NEED_EXCHANGE: n fragment flags
@@ -341,7 +360,7 @@ enum ghs_kernel_id {
   GHS_K_WIN, GHS_K_HOOK, GHS_K_JUMP_IDENT, GHS_K_JUMP, GHS_K_SELECT_LB, GHS_K_RESOLVE, GHS_K_GIANT, GHS_K_SCAN,
   GHS_K_PLAN, GHS_K_INIT, GHS_K_PACK, GHS_K_UNPACK, GHS_K_ROUND_REPORT, GHS_K_PACK_HOOK, GHS_K_UNPACK_HOOK,
   GHS_K_DENSE, GHS_K_FLAG_BITS, GHS_K_BUCKET, GHS_K_BMIN, GHS_K_WSTARTS, GHS_K_WMIN, GHS_K_HOT_HOOK,
-  GHS_K_TAIL_OPEN, GHS_K_TAIL_ROUND, GHS_K_TAIL_HOOK, GHS_K_COUNT
+  GHS_K_TAIL_OPEN, GHS_K_TAIL_ROUND, GHS_K_TAIL_HOOK, GHS_K_CSR_TROW /* ABI 9 */, GHS_K_COUNT
 };
 typedef struct ghs_kernel_record {
   uint32_t kernel;  /* ghs_kernel_id */

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi():
     L = _native.load()
-    assert L.ghs_abi_version() == _native.ABI_VERSION == 8
+    assert L.ghs_abi_version() == _native.ABI_VERSION == 9
     assert _native.device_count() >= 0
 
 
@@ -73,8 +73,9 @@ def test_rank_limits_rejected():
 
 
 def test_slot_retries_diagnostic():
-    """ABI 8: the count of round reports re-read for a failed checksum (none without a GPU)."""
-    assert _native.slot_retries() == 0
+    """ABI 8: the count of round reports re-read for a failed checksum (a process-wide counter: any
+    earlier solve in this process may have added to it — ADVICE r05)."""
+    assert _native.slot_retries() >= 0
     L = _native.load()
     assert L.ghs_slot_retries(None) == _native.GHS_E_ARG
 

@@ -239,7 +239,7 @@ def _emulate_ranks(e, world, cfg=None, bitmaps=True, rs=False):
             totals.append((res.total_weight, res.num_mst_edges))
         # owner-written flags: the MSF is the concatenation of the ranks' own slices, and no rank
         # wrote outside its range
-        flags = torch.empty(e.m, dtype=torch.uint8, device=e.u.device)
+        flags = torch.empty(e.m, dtype=torch.uint8, device=e.device)
         for x in engines:
             flags[x.e_lo:x.e_hi] = x.in_mst[x.e_lo:x.e_hi]
             assert bool((x.in_mst[: x.e_lo] == 7).all()) and bool((x.in_mst[x.e_hi: e.m] == 7).all())
