@@ -399,13 +399,26 @@ __device__ __forceinline__ void csr_tile_rows(const uint32_t *__restrict__ off, 
 // canonical endpoints by edge id (the fragment-form hooks, the plan's span sample): u from the
 // caller's u array, or — CSR input without one — a binary search over the row offsets
 struct Ends {
-  const uint32_t *u;    // nullptr: CSR input
-  const uint32_t *off;  // CSR row offsets (n + 1 entries)
+  const uint32_t *u;     // nullptr: CSR input
+  const uint32_t *off;   // CSR row offsets (n + 1 entries)
   const uint32_t *v;
   uint32_t n;
+  const uint32_t *trow;  // CSR: the rows of the solver's 256-edge tiles (k_csr_trow), nullptr before it ran
+  uint64_t E0, ntiles;   // ... its first edge and tile count
 };
 __device__ __forceinline__ uint32_t end_u(const Ends &E, uint32_t eid) {
-  return E.u ? E.u[eid] : csr_row(E.off, E.n, eid);
+  if (E.u) return E.u[eid];
+  // an edge of the solver's range: its tile's rows bound the search (~16 rows at s24: 4 steps, not 24)
+  if (E.trow && eid >= E.E0 && ((eid - E.E0) >> 8) < E.ntiles) {
+    const uint64_t t = (eid - E.E0) >> 8;
+    uint32_t hi = min(E.trow[t + 1], E.n - 1), lo = min(E.trow[t], hi);  // clamped: malformed offsets (err 8)
+    while (lo < hi) {
+      const uint32_t mid = lo + ((hi - lo + 1) >> 1);
+      if (E.off[mid] <= eid) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+  }
+  return csr_row(E.off, E.n, eid);
 }
 
 struct WaveStage {
@@ -1863,23 +1876,86 @@ __global__ __launch_bounds__(1024) void k_plan(const uint32_t *__restrict__ samp
 // CSR (ABI 9): u is derived from the row offsets (csr_tile_rows, the tiles' rows from k_csr_trow,
 // which validated the offsets: a wave's slice is a multiple of 256 edges, so its tiles are trow's).
 // ------------------------------------------------------------------------------------------
-// trow[t] = the row holding edge E0 + 256 t (t < ntiles), trow[ntiles] = the row of the range's last
-// edge: every nonempty row writes the tile starts inside it (one writer per tile). The same pass
-// validates the offsets (off[0] = 0, nondecreasing, off[n] = m; err bit 8): k_select, the next
-// launch, skips its stream when it is set, so no tile walks rows from a garbage trow.
-__global__ void k_csr_trow(const uint32_t *__restrict__ off, uint32_t n, uint64_t m, uint64_t E0, uint64_t e_hi,
-                           uint32_t *__restrict__ trow, unsigned long long *__restrict__ err) {
-  const uint64_t ntiles = (e_hi - E0 + 255) >> 8;
+// One pass over the row offsets of the solver's range [E0, e_hi) (T = e_hi - E0 edges), before
+// k_select:
+//  - trow[t] = the row holding edge E0 + 256 t (t < ntiles), trow[ntiles] = the row of the range's
+//    last edge: every nonempty row writes the tile starts inside it (one writer per tile);
+//  - the offsets' validation (off[0] = 0, nondecreasing, off[n] = m; err bit 8): k_select skips its
+//    stream when it is set, so no tile walks rows from a garbage trow;
+//  - the streaming passes' partitions balanced by cost instead of edge count: k_select's wave slices
+//    (bsel, nsel + 1 bounds, 256-edge tiles) and k_filter's block ranges (bfil, nfil + 1 bounds,
+//    1024-edge tiles). A tile costs its edges and its rows (the windows of row starts it scans): the
+//    end of an R-MAT list holds the high vertex ids, which store few canonical edges — thousands of
+//    mostly empty rows per tile — and with equal edge counts its waves ran ~10x longer than the rest.
+//    Cost = CSR_EDGE_COST per edge + CSR_ROW_COST per row of the range; each row r of [Rb, Re] owns
+//    the cost interval [C_r, C_r + len_r) (its row cost at its start, then its edges), the intervals
+//    tile [0, C_tot), and bound k = the position of cost k * C_tot / N, written by the row whose
+//    interval holds it (one writer per bound), rounded down to the tile grid.
+constexpr uint64_t CSR_EDGE_COST = 2, CSR_ROW_COST = 1;  // a row ~ half an edge: 8 windows (512 rows) a trip vs 256 edges
+// bound k (k < N) sits at cost k * S, S = ceil(Ctot / N): the row whose interval [C, C + len) holds it
+// writes it. k_lo = ceil(C / S) through a double reciprocal, corrected by exact integer products (a
+// 64-bit division per row made this pass ~0.17 ms at s24; C < 2^53)
+__device__ __forceinline__ void csr_bounds(uint64_t C, uint64_t len, uint64_t a, uint64_t S, double invS, uint32_t N,
+                                           uint32_t ts, uint32_t *__restrict__ bound) {
+  uint64_t k = (uint64_t)((double)C * invS);
+  while (k * S < C) ++k;
+  while (k > 0 && (k - 1) * S >= C) --k;
+  for (; k < N && k * S < C + len; ++k) {
+    const uint64_t d = k * S - C;
+    const uint64_t x = d < CSR_ROW_COST ? a : a + (d - CSR_ROW_COST) / CSR_EDGE_COST;
+    bound[k] = (uint32_t)(x / ts * ts);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_csr_trow(const uint32_t *__restrict__ off, uint32_t n, uint64_t m, uint64_t E0,
+                                                  uint64_t e_hi, uint32_t *__restrict__ trow,
+                                                  unsigned long long *__restrict__ err, uint32_t *__restrict__ bsel,
+                                                  uint32_t nsel, uint32_t *__restrict__ bfil, uint32_t nfil) {
+  __shared__ uint32_t s_rb[2];
+  const uint64_t T = e_hi - E0, ntiles = (T + 255) >> 8;
+  // Rb, Re: the rows of the range's first and last edges (wave 0: a 64-ary search each)
+  if (threadIdx.x < WAVE) {
+    const uint32_t lane = threadIdx.x;
+    for (int q = 0; q < 2; ++q) {
+      const uint64_t e = q ? e_hi - 1 : E0;
+      uint32_t lo = 0, c = n ? n : 1;  // candidates [lo, lo + c): off[lo] <= e
+      while (c > 1) {
+        const uint32_t st = (c + WAVE - 1) / WAVE;
+        const bool in = lane * st < c;
+        const uint64_t bm = __ballot(in && off[lo + lane * st] <= e);
+        const uint32_t L = bm ? 63u - (uint32_t)__clzll((long long)bm) : 0u;
+        lo += L * st;
+        c = min(st, c - L * st);
+      }
+      if (lane == 0) s_rb[q] = lo;
+    }
+  }
+  __syncthreads();
+  const uint64_t Rb = s_rb[0], Re = s_rb[1] < Rb ? Rb : s_rb[1];
+  const uint64_t Ctot = CSR_ROW_COST * (Re - Rb + 1) + CSR_EDGE_COST * T;
+  const uint64_t Ssel = (Ctot + nsel - 1) / nsel, Sfil = (Ctot + nfil - 1) / nfil;
+  const double iSsel = 1.0 / (double)Ssel, iSfil = 1.0 / (double)Sfil;
   bool bad = false;
   for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t lo = off[r], hi = off[r + 1];
     bad |= lo > hi;
-    if (lo >= hi || hi <= E0 || lo >= e_hi) continue;  // empty (or invalid), or outside the range
-    const uint64_t a = lo > E0 ? lo - E0 : 0, b = (hi < e_hi ? hi : e_hi) - E0;  // [a, b) relative to E0
+    if (lo > hi || r < Rb || r > Re) continue;  // invalid, or outside the range's rows
+    const uint64_t a = lo > E0 ? (lo < e_hi ? lo : e_hi) - E0 : 0, b = hi > E0 ? (hi < e_hi ? hi : e_hi) - E0 : 0;
+    const uint64_t C = CSR_ROW_COST * (r - Rb) + CSR_EDGE_COST * a, len = CSR_ROW_COST + CSR_EDGE_COST * (b - a);
+    csr_bounds(C, len, a, Ssel, iSsel, nsel, WAVE * 4, bsel);
+    csr_bounds(C, len, a, Sfil, iSfil, nfil, ARCS_PER_BLOCK, bfil);
+    if (a >= b) continue;  // empty (in the range)
     for (uint64_t t = (a + 255) >> 8; (t << 8) < b; ++t) trow[t] = (uint32_t)r;
-    if (lo < e_hi && e_hi <= hi) trow[ntiles] = (uint32_t)r;  // the row of edge e_hi - 1
+    if (b == T) trow[ntiles] = (uint32_t)r;  // the row of edge e_hi - 1
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) bad |= (off[0] != 0u) | ((uint64_t)off[n] != m);
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) bad |= (off[0] != 0u) | ((uint64_t)off[n] != m);
+    // bounds no row owns (cost k * S past the total: small ranges), and the end
+    for (uint64_t k = threadIdx.x; k <= nsel; k += blockDim.x)
+      if (k == nsel || k * Ssel >= Ctot) bsel[k] = (uint32_t)T;
+    for (uint64_t k = threadIdx.x; k <= nfil; k += blockDim.x)
+      if (k == nfil || k * Sfil >= Ctot) bfil[k] = (uint32_t)T;
+  }
   if (bad) atomicOr(err, 8ull);
 }
 
@@ -1891,7 +1967,8 @@ GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t m, uint64_t e_lo, uint64_
                                 uint64_t *__restrict__ ostart, uint64_t *__restrict__ ocount,
                                 uint8_t *__restrict__ mark, unsigned long long *__restrict__ err,
                                 const uint64_t *__restrict__ local_flag, uint32_t bs,
-                                unsigned long long *__restrict__ long_flag, const uint32_t *__restrict__ trow) {
+                                unsigned long long *__restrict__ long_flag, const uint32_t *__restrict__ trow,
+                                const uint32_t *__restrict__ bnd) {
   const uint64_t w_hi = *w_hi_p;  // the level plan lives on the device (k_plan)
   // a lattice-like plan (k_plan's span sample): note any level-0 edge whose ends lie more than one
   // bucket (2^bs ids) apart — the windowed round 0 (k_wmin) then falls back to k_bucket / k_bmin
@@ -1906,10 +1983,10 @@ GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t m, uint64_t e_lo, uint64_
   const uint64_t W = (uint64_t)gridDim.x * (BLOCK / WAVE);
   const uint64_t E0 = e_lo & ~3ull;
   const uint64_t T = e_hi - E0;
-  const uint64_t QA = CSR ? 255 : 3;  // CSR: slices of whole 256-edge tiles (the trow grid)
-  const uint64_t Q = ((T + W - 1) / W + QA) & ~QA;
-  const uint64_t vb = Q * gw;
-  const uint64_t ve = (vb + Q < T) ? vb + Q : T;
+  // CSR: the slices k_csr_trow balanced by cost (whole 256-edge tiles: the trow grid)
+  const uint64_t Q = ((T + W - 1) / W + 3) & ~3ull;
+  const uint64_t vb = CSR ? bnd[gw] : Q * gw;
+  const uint64_t ve = CSR ? bnd[gw + 1] : ((vb + Q < T) ? vb + Q : T);
   const uint64_t eb = E0 + vb;  // first edge of this wave
   const uint64_t nbytes = ve > vb ? (ve - vb) * 4 : 0;
   const __amdgpu_buffer_rsrc_t ru = make_rsrc(CSR ? ev : eu + eb, CSR ? 0 : nbytes);
@@ -1958,17 +2035,6 @@ GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t m, uint64_t e_lo, uint64_
     const uint64_t e0 = E0 + v;
     uint32_t a[4] = {ca.x, ca.y, ca.z, ca.w};
     const uint32_t b[4] = {cb.x, cb.y, cb.z, cb.w}, w[4] = {cw.x, cw.y, cw.z, cw.w};
-    uint32_t pcsr = 0;
-    if (CSR) {
-      csr_tile_rows<false>(eoff, n, R0, R1, (uint32_t)(E0 + v0), s_head[wid], a, w0);
-      // the next tile: its rows and its first window, in flight during this tile
-      R0 = R1;
-      R1 = R2;
-      R2 = trow[min((v0 >> 8) + 3, (T + 255) >> 8)];
-      w0 = csr_win(eoff, n, R0 + 1);
-      pcsr = lane ? wave_shr1(a[3]) : lastu;
-      lastu = __builtin_amdgcn_readlane(a[3], 63);
-    }
     // lane mask of the tile: edges in [e_lo, ve) (32-bit arithmetic, no branches)
     const uint32_t nv = v < ve ? (uint32_t)((ve - v) < 4 ? (ve - v) : 4) : 0u;
     const uint32_t nskip = e0 < e_lo ? (uint32_t)(e_lo - e0) : 0u;
@@ -1981,6 +2047,17 @@ GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t m, uint64_t e_lo, uint64_
     cb = ld_b128(rv, noff);
     cw = ld_b128(rw, noff);
     const uint32_t npa = CSR ? 0u : ld_b32(ru, noff - 4), npb = ld_b32(rv, noff - 4);
+    uint32_t pcsr = 0;
+    if (CSR) {  // after the next tile's stream loads: the rows' LDS / DPP chain runs under them
+      csr_tile_rows<false>(eoff, n, R0, R1, (uint32_t)(E0 + v0), s_head[wid], a, w0);
+      // the next tile: its rows and its first window, in flight during this tile
+      R0 = R1;
+      R1 = R2;
+      R2 = trow[min((v0 >> 8) + 3, (T + 255) >> 8)];
+      w0 = csr_win(eoff, n, R0 + 1);
+      pcsr = lane ? wave_shr1(a[3]) : lastu;
+      lastu = __builtin_amdgcn_readlane(a[3], 63);
+    }
     // u < v < n and (u, v) strictly above the previous edge; bitwise (no short-circuit
     // branches: hipcc turns && / || chains into exec-mask control flow here)
     uint32_t pa = (v == vb) ? bpa : (CSR ? pcsr : cpa), pb = (v == vb) ? bpb : cpb;
@@ -2009,6 +2086,8 @@ GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t m, uint64_t e_lo, uint64_
         mark[b[j]] = 1;
       }
     }
+    // in canonical (eid) order, within and across the output regions: the LDS tail's (w, index)
+    // minima rely on it (k_tail_open checks it under GHS_OPT_CHECK_TOTALS)
     wave_append(s_stage[wid], wo, a, b, key, omask, osrc, odst, okey);
     asm volatile("" ::"v"(ca.x), "v"(cb.x), "v"(cw.x), "v"(cpa), "v"(cpb));  // next tile landed (see above)
   }
@@ -2030,10 +2109,11 @@ GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t m, uint64_t e_lo, uint64_
 // add), so the pass costs stream + probes; splitting level 1 here saves a pass over the pending
 // edges.
 // ------------------------------------------------------------------------------------------
-// CSR: 8 waves per SIMD forced (GHS_FILTER_CSR_W8: 62 VGPRs + 4 spilled; uncapped the row derivation
-// takes it to 70, i.e. 7 blocks per CU — then the grid is sized to one residency wave instead)
+// CSR: 70 VGPRs (the row derivation), i.e. 7 blocks per CU, and the grid sized to one residency wave
+// (7 x 256 blocks); 8 waves forced (GHS_FILTER_CSR_W8=1: 62 VGPRs + 4 spilled) measured slower:
+// R-MAT s24 k_filter 1.85 against 1.65 ms, same box)
 #ifndef GHS_FILTER_CSR_W8
-#define GHS_FILTER_CSR_W8 1
+#define GHS_FILTER_CSR_W8 0
 #endif
 template <bool CSR>
 __global__ __launch_bounds__(BLOCK, (CSR && GHS_FILTER_CSR_W8) ? 8 : GHS_STREAM_WAVES) __attribute__((amdgpu_num_sgpr(72))) void k_filter(uint32_t n, uint64_t e_lo, uint64_t e_hi, const uint32_t *__restrict__ eu,
@@ -2047,17 +2127,18 @@ __global__ __launch_bounds__(BLOCK, (CSR && GHS_FILTER_CSR_W8) ? 8 : GHS_STREAM_
                                 uint64_t *__restrict__ lstart, uint64_t *__restrict__ lcount,
                                 uint32_t *__restrict__ osrc, uint32_t *__restrict__ odst,
                                 uint64_t *__restrict__ okey, uint64_t *__restrict__ ostart,
-                                uint64_t *__restrict__ ocount, uint8_t *__restrict__ mark) {
+                                uint64_t *__restrict__ ocount, uint8_t *__restrict__ mark,
+                                const uint32_t *__restrict__ bnd) {
   const uint64_t w_lo = w_range[0], w_hi = w_range[1];  // the level plan (k_plan)
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
   __shared__ WaveStage s_stage[BLOCK / WAVE];
   const uint64_t E0 = e_lo & ~3ull;
   const uint64_t T = e_hi - E0;
-  // CSR: block ranges of whole 1024-edge tiles, so every wave's 256-edge part starts on the trow grid
-  const uint64_t QA = CSR ? ARCS_PER_BLOCK - 1 : 3;
-  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + QA) & ~QA;
-  const uint64_t vb = Q * blockIdx.x;
-  const uint64_t ve = (vb + Q < T) ? vb + Q : T;
+  // CSR: the block ranges k_csr_trow balanced by cost (whole 1024-edge tiles, so every wave's 256-edge
+  // part starts on the trow grid)
+  const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
+  const uint64_t vb = CSR ? bnd[blockIdx.x] : Q * blockIdx.x;
+  const uint64_t ve = CSR ? bnd[blockIdx.x + 1] : ((vb + Q < T) ? vb + Q : T);
   const uint64_t eb = E0 + vb;  // first edge of this block
   const uint64_t nbytes = ve > vb ? (ve - vb) * 4 : 0;
   const __amdgpu_buffer_rsrc_t ru = make_rsrc(CSR ? ev : eu + eb, CSR ? 0 : nbytes);
@@ -2185,6 +2266,8 @@ __global__ __launch_bounds__(BLOCK, (CSR && GHS_FILTER_CSR_W8) ? 8 : GHS_STREAM_
       }
     }
     const Offs2 o = block_offsets_w2((uint32_t)__popc(lmask), (uint32_t)__popc(rmask), s_wcnt);
+    // in canonical (eid) order, within and across the output regions: the LDS tail's (w, index)
+    // minima rely on it (k_tail_open checks it under GHS_OPT_CHECK_TOTALS)
     stage_write(s_stage[threadIdx.x / WAVE], la, lb, key, lmask, o.lane_excl[0], o.wave_cnt[0], lsrc, ldst, lkey,
                 vb + nlev + o.wave_before[0]);
     stage_write(s_stage[threadIdx.x / WAVE], a, b, key, rmask, o.lane_excl[1], o.wave_cnt[1], osrc, odst, okey,
@@ -2331,6 +2414,8 @@ GHS_STREAM_KERNEL_6 void k_level_pass(const uint32_t *__restrict__ ru, const uin
       }
     }
     const Offs2 o = block_offsets_w2(mlev, mrem, s_wcnt);
+    // in canonical (eid) order, within and across the output regions: the LDS tail's (w, index)
+    // minima rely on it (k_tail_open checks it under GHS_OPT_CHECK_TOTALS)
     stage_write(s_stage[threadIdx.x / WAVE], la, lb, k, lmask, o.lane_excl[0], o.wave_cnt[0], lsrc, ldst, lkey,
                 vb + nlev + o.wave_before[0]);
     stage_write(s_stage[threadIdx.x / WAVE], a, b, k, rmask, o.lane_excl[1], o.wave_cnt[1], ou, ov, okey,
@@ -3092,13 +3177,15 @@ __global__ __launch_bounds__(BLOCK) void k_relabel_dense(uint32_t *__restrict__ 
 }
 
 // level end: every dense fragment's root back to vertex labels
+// write = false: the chains' check alone (the plan's last level, whose vertex labels nothing reads,
+// under GHS_OPT_CHECK_TOTALS — ADVICE r05)
 __global__ void k_dense_close(const uint32_t *__restrict__ vtx, const unsigned long long *__restrict__ d_nact,
                               const uint32_t *__restrict__ dlab, uint32_t *__restrict__ vlab,
-                              unsigned long long *__restrict__ err) {
+                              unsigned long long *__restrict__ err, bool write) {
   const uint64_t nact = *d_nact;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nact; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t r = find_lab(dlab, (uint32_t)i, err);
-    vlab[vtx[i]] = vtx[r];
+    if (write) vlab[vtx[i]] = vtx[r];
   }
 }
 
@@ -3574,8 +3661,11 @@ __device__ __forceinline__ void tail_row_out(const TailBufs tb, const unsigned l
   }
 }
 
+// check (GHS_OPT_CHECK_TOTALS): verify the invariant the (w, index) minima rest on — the
+// block's region holds its records in strictly increasing eid order — after writing it
 __global__ __launch_bounds__(TAIL_T) void k_tail_open(const uint32_t *__restrict__ src, const uint32_t *__restrict__ dst,
-                                                      const uint64_t *__restrict__ key, SegView in, TailBufs tb) {
+                                                      const uint64_t *__restrict__ key, SegView in, TailBufs tb,
+                                                      bool check) {
   __shared__ unsigned long long s_best[TAIL_MAX];
   __shared__ TailStage s_stage[TAIL_T / WAVE];
   __shared__ uint32_t s_wcnt[TAIL_T / WAVE];
@@ -3649,6 +3739,9 @@ __global__ __launch_bounds__(TAIL_T) void k_tail_open(const uint32_t *__restrict
   for (int d = WAVE / 2; d > 0; d >>= 1) live_n += __shfl_xor(live_n, d);
   if ((threadIdx.x & (WAVE - 1)) == 0) atomicAdd(&s_live, live_n);
   __syncthreads();  // every wave's record stores drained: the row reads them back through L2
+  if (check)
+    for (uint32_t i = threadIdx.x + 1; i < out_n; i += TAIL_T)
+      if ((uint32_t)okey[i - 1] >= (uint32_t)okey[i]) atomicOr(&tb.ctl->err, 1u);
   // the block's minima of every dense fragment (round 0: the root list is the identity)
   tail_row_out(tb, s_best, nullptr, F, orec, okey, nullptr);
   if (threadIdx.x == 0) {
@@ -4072,7 +4165,10 @@ struct ghs_solver {
   const uint32_t *eu = nullptr, *ev = nullptr, *ew = nullptr;
   const uint32_t *eoff = nullptr;  // CSR input (ABI 9): row offsets, eu == nullptr (or the caller's u for gathers)
   bool csr = false;
-  uint32_t *trow = nullptr;        // CSR: the row of every 256-edge tile of the range (k_select -> k_filter)
+  uint32_t *trow = nullptr;        // CSR: the row of every 256-edge tile of the range (k_csr_trow)
+  uint32_t *bsel = nullptr, *bfil = nullptr;  // CSR: k_select's / k_filter's cost-balanced partitions
+  unsigned csr_gsel = 0, csr_gfil = 0;        // ... and the grids they were computed for
+  bool trow_ready = false;                    // k_csr_trow ran this solve (ends_of may use trow)
   uint8_t *in_mst = nullptr;
   hipStream_t stream = nullptr;
   ghs_config_t cfg{};
@@ -4271,7 +4367,10 @@ struct KtScope {
 };
 #define KT(kernel, items) KtScope _kt_scope(s, (kernel), (items))
 
-static inline Ends ends_of(const ghs_solver *s) { return Ends{s->eu, s->eoff, s->ev, s->n}; }
+static inline Ends ends_of(const ghs_solver *s) {
+  const uint64_t E0 = s->e_lo & ~3ull, T = s->e_hi > E0 ? s->e_hi - E0 : 0;
+  return Ends{s->eu, s->eoff, s->ev, s->n, s->csr && s->trow_ready ? s->trow : nullptr, E0, (T + 255) >> 8};
+}
 
 static bool solver_cancelled(const ghs_solver *s) {
   return __atomic_load_n(&s->cancel_flag, __ATOMIC_ACQUIRE) ||
@@ -4424,6 +4523,8 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
   if (s) s->cap_arcs = cap;
   p = carve(C_COUNT * sizeof(unsigned long long)); if (s) s->cnt = (unsigned long long *)p;
   p = carve((local_edges / 256 + 8) * 4); if (s) s->trow = (uint32_t *)p;  // CSR: each 256-edge tile's row
+  p = carve((SEG_MAX + 1) * 4); if (s) s->bsel = (uint32_t *)p;             // CSR: k_select's wave slices
+  p = carve((SEG_G + 1) * 4); if (s) s->bfil = (uint32_t *)p;               // CSR: k_filter's block ranges
   if (local_edges == m) {  // one rank: the LDS tail's arrays (its records go to the idle edge buffer)
     p = carve(N * 4, stg); if (s) s->tail.dmap = (uint32_t *)p;
     p = carve((size_t)TAIL_G * TAIL_MAX * 8); if (s) s->tail.partial = (uint64_t *)p;
@@ -4639,17 +4740,26 @@ static int open_level(ghs_solver *s, bool async_open = false) {
     auto sel = s->csr ? k_select<true> : k_select<false>;
     G = grid_for(TC, ARCS_PER_BLOCK, resident_grid((const void *)sel, BLOCK, s->seg_g));
     if (TC) {
-      if (s->csr) {  // CSR: every 256-edge tile's row (and the offsets' validation) for both passes
+      if (s->csr) {
+        // CSR: every 256-edge tile's row, the offsets' validation, and both passes' cost-balanced
+        // partitions (k_select's G x 4 wave slices, k_filter's block ranges for its grid)
+        auto filt = k_filter<true>;
+        s->csr_gsel = G;
+        s->csr_gfil = grid_for(TC, ARCS_PER_BLOCK,
+                               resident_grid((const void *)filt, BLOCK, s->seg_g, GHS_RESIDENT_GRIDS || !GHS_FILTER_CSR_W8));
+        s->trow_ready = true;
         KT(GHS_K_CSR_TROW, s->n);
-        k_csr_trow<<<grid_for(s->n, 256, 8192), 256, 0, st>>>(s->eoff, s->n, s->m, s->e_lo & ~3ull, s->e_hi, s->trow,
-                                                             s->cnt + C_ERR);
+        k_csr_trow<<<grid_for(s->n, 256, 2048), 256, 0, st>>>(s->eoff, s->n, s->m, s->e_lo & ~3ull, s->e_hi, s->trow,
+                                                             s->cnt + C_ERR, s->bsel, G * (BLOCK / WAVE), s->bfil,
+                                                             s->csr_gfil);
       }
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[0], st));
       {
         KT(GHS_K_SELECT, TC);
         sel<<<G, BLOCK, 0, st>>>(s->n, s->m, s->e_lo, s->e_hi, s->eu, s->eoff, s->ev, s->ew, d_range + 1, Y.src, Y.dst,
                                  Y.key, Y.seg_start, Y.seg_count, mark, s->cnt + C_ERR,
-                                 s->wstart ? s->d_thr + PLAN_LOCAL : nullptr, s->bk_bs, s->cnt + C_LONG, s->trow);
+                                 s->wstart ? s->d_thr + PLAN_LOCAL : nullptr, s->bk_bs, s->cnt + C_LONG, s->trow,
+                                 s->bsel);
       }
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[1], st));
       GHS_HIP_CHECK(hipGetLastError());
@@ -4668,15 +4778,14 @@ static int open_level(ghs_solver *s, bool async_open = false) {
       // FILTER + level split over the canonical list once level 0 is complete: level-1 edges
       // not inside one fragment -> Y; heavier edges not inside the giant -> pending (rem[rout])
       auto filt = s->csr ? k_filter<true> : k_filter<false>;
-      G = grid_for(TC, ARCS_PER_BLOCK,
-                   resident_grid((const void *)filt, BLOCK, s->seg_g, GHS_RESIDENT_GRIDS || (s->csr && !GHS_FILTER_CSR_W8)));
+      G = s->csr ? s->csr_gfil : grid_for(TC, ARCS_PER_BLOCK, resident_grid((const void *)filt, BLOCK, s->seg_g));
       if (TC) {
         GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[2], st));
         {
           KT(GHS_K_FILTER, TC);
           filt<<<G, BLOCK, 0, st>>>(s->n, s->e_lo, s->e_hi, s->eu, s->eoff, s->trow, s->ev, s->ew, d_range, s->bits, s->giant, s->lab,
                                         Y.src, Y.dst, Y.key, Y.seg_start, Y.seg_count, RO.src, RO.dst, RO.key,
-                                        RO.seg_start, RO.seg_count, mark);
+                                        RO.seg_start, RO.seg_count, mark, s->bfil);
         }
         GHS_HIP_CHECK(hipGetLastError());
         GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[3], st));
@@ -4772,10 +4881,10 @@ static int dense_close(ghs_solver *s) {
   // s26 x 8 ranks: level 1's close, ~0.2 ms per rank)
   (void)plan_sync(s);
   const bool last = s->level + 2 >= s->thresholds.size();
-  if (!last) {
+  if (!last || s->check_totals) {
     KT(GHS_K_DENSE, s->dense_n);
     k_dense_close<<<grid_for(s->dense_n, 256, 16384), 256, 0, s->stream>>>(s->dvtx, s->cnt + C_NDENSE, s->dlab, s->vlab,
-                                                                           s->cnt + C_ERR);
+                                                                           s->cnt + C_ERR, !last);
   }
   GHS_HIP_CHECK(hipGetLastError());
   s->lab = s->vlab; s->par = s->vpar; s->best = s->vbest;
@@ -5325,7 +5434,7 @@ static int run_tail(ghs_solver *s, uint64_t prev_in) {
     const unsigned long long *d_nprev = prev_ident ? s->cnt + C_N : act_count(s, s->act_cur ^ 1);
     const uint64_t nprev_bound = prev_ident ? s->n : s->level_nact;
     k_tail_labels<<<grid_for(nprev_bound, 256, 8192), 256, 0, st>>>(prev, d_nprev, s->lab, tb);
-    k_tail_open<<<TAIL_G, TAIL_T, 0, st>>>(I.src, I.dst, I.key, in, tb);
+    k_tail_open<<<TAIL_G, TAIL_T, 0, st>>>(I.src, I.dst, I.key, in, tb, s->check_totals);
   }
   {
     KT(GHS_K_TAIL_HOOK, F0);

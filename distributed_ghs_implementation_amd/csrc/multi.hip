@@ -26,6 +26,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -371,9 +372,25 @@ void comm_free(ghs_comm *c) {
   delete c;
 }
 
+// the ranks' edge ranges balanced by the cost density 1 + RANGE_BETA * (1 - e / m) over the canonical
+// list — the closed form of device.py range_split / edge_range (see there), 4-aligned
+#ifndef GHS_RANGE_BETA
+#define GHS_RANGE_BETA 0.2
+#endif
+uint64_t range_split(uint64_t m, int k, int N) {
+  const double b = GHS_RANGE_BETA;
+  if (k <= 0) return 0;
+  if (k >= N) return m;
+  if (b == 0.0) return ((m * (uint64_t)k) / (uint64_t)N) & ~3ull;
+  const double t = (double)k / (double)N * (1.0 + b / 2.0);
+  const double x = ((1.0 + b) - std::sqrt((1.0 + b) * (1.0 + b) - 2.0 * b * t)) / b;
+  const uint64_t e = (uint64_t)(x * (double)m);
+  return (e < m ? e : m) & ~3ull;
+}
 void edge_range(uint64_t m, int r, int N, uint64_t *lo, uint64_t *hi) {
-  *lo = ((m * (uint64_t)r) / (uint64_t)N) & ~3ull;
-  *hi = (r == N - 1) ? m : (((m * (uint64_t)(r + 1)) / (uint64_t)N) & ~3ull);
+  *lo = range_split(m, r, N);
+  *hi = (r == N - 1) ? m : range_split(m, r + 1, N);
+  if (*hi < *lo) *hi = *lo;
 }
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }

@@ -113,12 +113,38 @@ def generate_grid(k, mode=0, wseed=2, device="cuda"):
     return DeviceEdges(k * k, u, v, w)
 
 
-def edge_range(m, rank, world):
-    """Contiguous canonical-edge range owned by `rank` (balanced by edge count, 4-aligned so the
-    16-byte vector loads of the level pass stay aligned)."""
-    lo = ((m * rank) // world) & ~3
-    hi = m if rank == world - 1 else ((m * (rank + 1)) // world) & ~3
-    return lo, hi
+# The ranks' edge ranges are balanced by a cost density over the canonical list instead of by edge
+# count: c(x) = 1 + RANGE_BETA * (1 - x) at relative position x = e / m. A canonical edge is stored at
+# its smaller end, so the list's early edges have small u and their heavier ends spread over the
+# whole vertex range: rank 0's k_filter probes reach all of the giant bitmap (8 MiB at s26, beyond
+# one XCD's L2) and the last rank's only its top part — R-MAT s26 x 8 with equal counts ran k_filter
+# 1.70 ms on rank 0 against 1.16 on rank 7 (profiles/r05/final/emu_s26_w8_per_rank.txt). The same
+# closed form is in csrc/multi.hip (ghs_mst_multi / ghs_mst_emulated). beta = 0.2 measured best over
+# {0, 0.1, 0.2, 0.3} on the s26 x 8 emulation: slowest rank's kernels 6.46 -> 6.08 ms (profiles/r06/).
+RANGE_BETA = 0.2
+
+
+def range_split(m, k, world, beta=None):
+    """The first edge of rank k's range: F(x_k) = k / world * F(1) for F(x) = x + beta (x - x^2 / 2),
+    4-aligned (the 16-byte vector loads of the level pass stay aligned)."""
+    import math
+    b = RANGE_BETA if beta is None else float(beta)
+    if k <= 0:
+        return 0
+    if k >= world:
+        return m
+    if b == 0.0:
+        return ((m * k) // world) & ~3
+    t = k / world * (1.0 + b / 2.0)
+    x = ((1.0 + b) - math.sqrt((1.0 + b) ** 2 - 2.0 * b * t)) / b
+    return min(m, int(x * m)) & ~3
+
+
+def edge_range(m, rank, world, beta=None):
+    """Contiguous canonical-edge range owned by `rank` (range_split: cost-balanced, 4-aligned)."""
+    lo = range_split(m, rank, world, beta)
+    hi = m if rank == world - 1 else range_split(m, rank + 1, world, beta)
+    return lo, max(lo, hi)
 
 
 class DeviceMST:
