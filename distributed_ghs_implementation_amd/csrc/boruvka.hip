@@ -404,12 +404,13 @@ struct Ends {
   const uint32_t *v;
   uint32_t n;
   const uint32_t *trow;  // CSR: the rows of the solver's 256-edge tiles (k_csr_trow), nullptr before it ran
-  uint64_t E0, ntiles;   // ... its first edge and tile count
+  uint64_t E0, E1;       // ... its edges [E0, E1) (trow[ntiles] is the row of edge E1 - 1: edges of the
+                         // last tile past E1 are another rank's, their rows may lie beyond it)
 };
 __device__ __forceinline__ uint32_t end_u(const Ends &E, uint32_t eid) {
   if (E.u) return E.u[eid];
   // an edge of the solver's range: its tile's rows bound the search (~16 rows at s24: 4 steps, not 24)
-  if (E.trow && eid >= E.E0 && ((eid - E.E0) >> 8) < E.ntiles) {
+  if (E.trow && eid >= E.E0 && eid < E.E1) {
     const uint64_t t = (eid - E.E0) >> 8;
     uint32_t hi = min(E.trow[t + 1], E.n - 1), lo = min(E.trow[t], hi);  // clamped: malformed offsets (err 8)
     while (lo < hi) {
@@ -1471,10 +1472,13 @@ __global__ __launch_bounds__(BLOCK) void k_jump(const uint32_t *__restrict__ act
 // consecutive vertices). A vertex that was not a root when the level opened (lab[c] != c) is never
 // a label and is skipped; a root that did not hook only tests its best slot; a root that hooked
 // walks. Mutual pairs and hook counting as in k_jump.
+// lab_init (one rank, level 0's round 0): lab was never initialised (every vertex is a root at the
+// level's open, so it is not read) and this pass writes every vertex's label — the solve's only
+// n-sized label write before level 1 (the iota it replaces and the read cost one lab pass each).
 __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par, uint32_t *__restrict__ lab,
                                                       uint64_t *__restrict__ best, uint8_t *__restrict__ flags,
                                                       unsigned long long *__restrict__ err,
-                                                      unsigned long long *__restrict__ acc) {
+                                                      unsigned long long *__restrict__ acc, bool lab_init) {
   const uint64_t tg = blockIdx.x * (uint64_t)BLOCK + threadIdx.x, S = (uint64_t)gridDim.x * BLOCK;
   unsigned long long wsum = 0, cnt = 0;
   for (uint64_t i0 = tg * 4; i0 - tg * 4 < n; i0 += S * 4) {  // every thread while the chunk starts below n
@@ -1486,7 +1490,7 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
     for (int k = 0; k < 4; ++k) {
       const uint64_t vv = JV(k);
       const bool in = vv < n;
-      lc[k] = in ? lab[vv] : LABEL_NONE;
+      lc[k] = in ? (lab_init ? (uint32_t)vv : lab[vv]) : LABEL_NONE;
       pc[k] = in ? par[vv] : 0u;
       bc[k] = in ? best[vv] : KEY_NONE;
     }
@@ -1540,7 +1544,7 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
         best[c] = KEY_NONE;
         kb |= 1u << (8 * k);
       } else {
-        lab[c] = x[k];
+        if (!lab_init) lab[c] = x[k];
         if (acc) {
           wsum += bc[k] >> 32;
           cnt += 1;
@@ -1549,7 +1553,10 @@ __global__ __launch_bounds__(BLOCK) void k_jump_ident(uint32_t n, uint32_t *par,
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      if (JV(k) < n) flags[JV(k)] = (uint8_t)(kb >> (8 * k));
+      if (JV(k) < n) {
+        flags[JV(k)] = (uint8_t)(kb >> (8 * k));
+        if (lab_init) lab[JV(k)] = (hooked >> k) & 1u ? x[k] : (uint32_t)JV(k);  // coalesced: every vertex
+      }
 #undef JV
   }
   if (acc) add_totals(wsum, cnt, acc);
@@ -4169,6 +4176,7 @@ struct ghs_solver {
   uint32_t *bsel = nullptr, *bfil = nullptr;  // CSR: k_select's / k_filter's cost-balanced partitions
   unsigned csr_gsel = 0, csr_gfil = 0;        // ... and the grids they were computed for
   bool trow_ready = false;                    // k_csr_trow ran this solve (ends_of may use trow)
+  bool lab_lazy = false;                      // one rank: lab not yet initialised (ensure_lab / k_jump_ident)
   uint8_t *in_mst = nullptr;
   hipStream_t stream = nullptr;
   ghs_config_t cfg{};
@@ -4368,8 +4376,7 @@ struct KtScope {
 #define KT(kernel, items) KtScope _kt_scope(s, (kernel), (items))
 
 static inline Ends ends_of(const ghs_solver *s) {
-  const uint64_t E0 = s->e_lo & ~3ull, T = s->e_hi > E0 ? s->e_hi - E0 : 0;
-  return Ends{s->eu, s->eoff, s->ev, s->n, s->csr && s->trow_ready ? s->trow : nullptr, E0, (T + 255) >> 8};
+  return Ends{s->eu, s->eoff, s->ev, s->n, s->csr && s->trow_ready ? s->trow : nullptr, s->e_lo & ~3ull, s->e_hi};
 }
 
 static bool solver_cancelled(const ghs_solver *s) {
@@ -4694,6 +4701,7 @@ static int fail_counters(ghs_solver *s, unsigned long long err, const char *wher
 }
 
 static int open_level_finish(ghs_solver *s);
+static void ensure_lab(ghs_solver *s);
 
 // ---- open the next level: select its edges, set its active list (one host sync) --------------
 // Returns GHS_OK with s->level_open set, with the level skipped (no edges), or — several ranks —
@@ -4710,6 +4718,7 @@ static int open_level(ghs_solver *s, bool async_open = false) {
   ArcBuf &Y = s->buf[1];
 
   if (!first) {
+    ensure_lab(s);
     // find the giant fragment from a sample, compress labels and build its bitmap (on device)
     {
       KT(GHS_K_GIANT, 0);
@@ -5064,9 +5073,17 @@ static void enqueue_bmin(ghs_solver *s, const uint32_t *a, const uint32_t *b, co
 
 static int enqueue_state_init(ghs_solver *s);
 
+// the identity labels, unless already written (solver_begin leaves them to level 0's round 0)
+static void ensure_lab(ghs_solver *s) {
+  if (!s->lab_lazy) return;
+  s->lab_lazy = false;
+  k_iota<<<grid_for(s->n, 256, 8192), 256, 0, s->stream>>>(s->lab, s->n);
+}
+
 static int enqueue_minedge(ghs_solver *s) {
   const bool timed = s->detail || (s->time_rounds && s->level_round >= 1);
   if (timed) record(s, 0);
+  if (s->level != 0 || s->level_round != 0) ensure_lab(s);  // round 0 of level 0 reads no label
   const ArcBuf &I = s->buf[s->cur];
   ArcBuf &O = s->buf[s->cur ^ 1];
   SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
@@ -5182,6 +5199,9 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
         s->cfg.num_ranks <= 1 && s->level_round == 0 && (!s->arcs_known || s->cur_arcs < 8 * bound);
     if (edge_form && s->scan_pending) flush_scan(s);
     const bool dual = !edge_form && s->cfg.num_ranks <= 1 && s->level_round >= 1 && bound >= EDGE_HOOK_MIN_BOUND;
+    // lab stays uninitialised only into the identity jump of a round whose hooks read no label
+    const bool ident_jump = s->act_ident && (s->cfg.num_ranks <= 1 || s->level_dense);
+    if (!(ident_jump && s->level == 0 && s->level_round == 0 && (s->round_bucketed || edge_form))) ensure_lab(s);
     if (s->round_bucketed) {
       // k_bmin hooked every fragment that has an outgoing edge; the jump resolves the mutual
       // pairs and counts the hooks
@@ -5230,7 +5250,8 @@ static int enqueue_contract(ghs_solver *s, RoundSlot *slot = nullptr, unsigned l
       const uint32_t ni = s->level_dense ? (uint32_t)s->dense_n : s->n;
       KT(GHS_K_JUMP_IDENT, ni);
       k_jump_ident<<<grid_for(((uint64_t)ni + 3) / 4, BLOCK, s->jump_ident_g), BLOCK, 0, s->stream>>>(
-          ni, s->par, s->lab, s->best, s->flags, s->cnt + C_ERR, acc);
+          ni, s->par, s->lab, s->best, s->flags, s->cnt + C_ERR, acc, s->lab_lazy);
+      s->lab_lazy = false;
     } else {
       KT(GHS_K_JUMP, 0);
       k_jump<<<g, BLOCK, 0, s->stream>>>(act, d_nact, s->par, s->lab, s->best, s->flags, s->cnt + C_ERR, acc);
@@ -5349,6 +5370,7 @@ static int check_level_totals(ghs_solver *s) {
 }
 
 static void close_level(ghs_solver *s) {
+  ensure_lab(s);  // a level 0 without rounds
   s->level_open = false;
   s->level += 1;
   (void)plan_sync(s);  // on failure thresholds stay empty: no further level
@@ -5393,14 +5415,19 @@ static int decide_bucketed(ghs_solver *s) {
 // once the level is done) behind k_tail_map + k_tail_open, each batch ending with a copy of the
 // control block and its report; reads the tail's per-round stats from that copy and closes the
 // level. Rounds whose launches follow the finishing round exit at once.
-// Tail rounds per batch: the first batch is sized from the level's last observed contraction
-// (F0 fragments shrinking by `decay` per round finish in about log_decay(F0) rounds, plus the
-// finishing one), so few launches run after the level is done; later batches are short.
-constexpr uint32_t TAIL_BATCH_MIN = 2, TAIL_BATCH_MAX = 8, TAIL_BATCH_NEXT = 3;
+// Tail rounds per batch: the first batch is sized from the level's last observed contraction.
+// F0 fragments shrinking by `decay` per round leave <= 1 root after L = log_decay(F0) rounds of
+// hooks (the open's included), so k_tail_round r = ceil(L) is the finishing one and the batch holds
+// exactly the launches the level needs. The contraction slows inside a level (R-MAT s24 level 0:
+// 26x, 19x, 10x, 10x), so half a round of margin — none when the open's hooks alone are expected to
+// finish (F0 <= decay): R-MAT s24 levels 0 and 1 and both tails of the 16384^2 grid then launch no
+// round past the finishing one (profiles/r06/rounds_*.txt). An underestimate costs one more batch.
+constexpr uint32_t TAIL_BATCH_MIN = 1, TAIL_BATCH_MAX = 8, TAIL_BATCH_NEXT = 3;
 
 static uint32_t tail_first_batch(uint64_t F0, uint64_t prev_in) {
   const double decay = std::max(2.0, prev_in > F0 ? (double)prev_in / (double)F0 : 2.0);
-  const double est = std::ceil(std::log((double)F0) / std::log(decay)) + 1.0;
+  const double L = std::log((double)F0) / std::log(decay);
+  const double est = (double)F0 <= decay ? 1.0 : std::ceil(L + 0.5);
   return (uint32_t)std::min<double>(TAIL_BATCH_MAX, std::max<double>(TAIL_BATCH_MIN, est));
 }
 constexpr uint64_t TAIL_TRY = 32ull * TAIL_MAX;  // a bound below this: read the exact count first
@@ -5412,6 +5439,7 @@ static bool tail_usable(const ghs_solver *s) {
 
 static int run_tail(ghs_solver *s, uint64_t prev_in) {
   hipStream_t st = s->stream;
+  ensure_lab(s);
   TailBufs tb = s->tail;
   const ArcBuf &I = s->buf[s->cur], &O = s->buf[s->cur ^ 1];
   tb.rec = O.src;  // the idle edge buffer holds the tail's records
@@ -5452,9 +5480,11 @@ static int run_tail(ghs_solver *s, uint64_t prev_in) {
       // its hook kernel, so the round that finishes the level is not followed by a no-op hook launch
       // when it closes its batch (the hook comes first in the next batch otherwise)
       if (r > 1) {
+        s->round = round0 + r - 1;  // the hooks of round r - 1's stream: that round's launches
         KT(GHS_K_TAIL_HOOK, 0);
         k_tail_hook<<<hook_g, 256, 0, st>>>(tb, r - 1, s->in_mst, TAIL_G, err);
       }
+      s->round = round0 + r;
       KT(GHS_K_TAIL_ROUND, 0);
       k_tail_round<<<TAIL_G, TAIL_T, 0, st>>>(tb, r, act0, s->lab, s->cnt, err);
     }
@@ -5659,7 +5689,10 @@ static int solver_begin(ghs_solver *s) {
         return rc;
       }
     }
-    k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->lab, n);
+    // one rank: level 0's round 0 writes every label in its k_jump_ident (nothing reads lab before
+    // it); any other first reader initialises it through ensure_lab
+    s->lab_lazy = s->cfg.num_ranks <= 1 && !s->dense_mode;
+    if (!s->lab_lazy) k_iota<<<grid_for(n, 256, 8192), 256, 0, s->stream>>>(s->lab, n);
   }
   // only the solver's own edge range: it never writes a flag outside [e_lo, e_hi)
   if (s->e_hi > s->e_lo && (e = hipMemsetAsync(s->in_mst + s->e_lo, 0, s->e_hi - s->e_lo, s->stream)) != hipSuccess) GHS_FAIL(GHS_E_HIP, std::string("memset in_mst: ") + hipGetErrorString(e));

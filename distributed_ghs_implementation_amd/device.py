@@ -120,7 +120,7 @@ def generate_grid(k, mode=0, wseed=2, device="cuda"):
 # one XCD's L2) and the last rank's only its top part — R-MAT s26 x 8 with equal counts ran k_filter
 # 1.70 ms on rank 0 against 1.16 on rank 7 (profiles/r05/final/emu_s26_w8_per_rank.txt). The same
 # closed form is in csrc/multi.hip (ghs_mst_multi / ghs_mst_emulated). beta = 0.2 measured best over
-# {0, 0.1, 0.2, 0.3} on the s26 x 8 emulation: slowest rank's kernels 6.46 -> 6.08 ms (profiles/r06/).
+# {0, 0.2, 0.4} on the s26 x 8 emulation: slowest rank's kernels 6.46 -> 6.08 ms (profiles/r06/).
 RANGE_BETA = 0.2
 
 

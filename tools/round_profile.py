@@ -35,10 +35,16 @@ def main():
         _native.profile_enable(False)
     stats = list(stats)
     per = defaultdict(lambda: defaultdict(float))
-    other = defaultdict(float)
+    last = {}  # each level's last round with stats
+    for i, st in enumerate(stats):
+        last[st["level"]] = i
     for r in recs:
         ok = r["round"] < len(stats) and stats[r["round"]]["level"] == r["level"]
-        key = r["round"] if ok else ("noop", r["level"])
+        # past a level's rounds: the LDS tail's finishing launch (the round after the level's last:
+        # it applies that round's hooks and writes the level's labels) or a launch that found the
+        # level done (a no-op)
+        fin = not ok and r["round"] == last.get(r["level"], -2) + 1
+        key = r["round"] if ok else ("finish" if fin else "noop", r["level"])
         per[key][r["kernel"]] += r["ms"]
     tot = sum(r["ms"] for r in recs)
     print(f"m={e.m} n={e.n} rounds={res.rounds} levels={res.levels} sum of launches {tot:.3f} ms")
@@ -48,7 +54,7 @@ def main():
               f"hooks {st['hooks']:>9d} | " + " ".join(f"{k}={v * 1e3:.0f}" for k, v in sorted(ks.items(), key=lambda kv: -kv[1])))
     for k, ks in per.items():
         if isinstance(k, tuple):
-            print("noop", k, " ".join(f"{a}={v * 1e3:.0f}" for a, v in ks.items()))
+            print(k[0], f"L{k[1]}", " ".join(f"{a}={v * 1e3:.0f}" for a, v in ks.items()))
 
 
 if __name__ == "__main__":
