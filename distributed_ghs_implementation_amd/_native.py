@@ -41,7 +41,8 @@ EXPORTED_SYMBOLS = (
     "ghs_solver_unpack_best", "ghs_solver_best_slots",
     "ghs_solver_contract", "ghs_solver_finish", "ghs_solver_reset", "ghs_solver_cancel", "ghs_solver_destroy",
     "ghs_solver_hook_local", "ghs_solver_unpack_hook",
-    "ghs_solver_hook_slots", "ghs_solver_hook_owner", "ghs_solver_apply_hooks",
+    "ghs_solver_hook_slots", "ghs_solver_hook_owner", "ghs_solver_apply_hooks", "ghs_solver_tail_begin",
+    "ghs_solver_tail_buffers", "ghs_solver_tail_agree", "ghs_solver_tail_round",
     "ghs_rmat_temp_bytes", "ghs_rmat_generate", "ghs_rmat_tuples", "ghs_grid_generate",
     "ghs_profile_enable", "ghs_profile_read", "ghs_kernel_name",
     "ghs_comm_unique_id", "ghs_comm_init", "ghs_comm_destroy", "ghs_solver_run", "ghs_mst_emulated",
@@ -99,7 +100,7 @@ class RoundStatsList(collections.abc.Sequence):
         return repr(list(self))
 
 
-ABI_VERSION = 9  # include/ghs_mst.h GHS_MST_ABI_VERSION
+ABI_VERSION = 10  # include/ghs_mst.h GHS_MST_ABI_VERSION
 
 
 class Result(ctypes.Structure):
@@ -266,6 +267,10 @@ def load():
             "ghs_solver_hook_slots": (i32, [vp, u32, P(vp), P(u64)]),
             "ghs_solver_hook_owner": (i32, [vp, u32, u64, vp]),
             "ghs_solver_apply_hooks": (i32, [vp, vp, P(vp)]),
+            "ghs_solver_tail_begin": (i32, [vp, P(u64)]),
+            "ghs_solver_tail_buffers": (i32, [vp, P(vp), P(vp)]),
+            "ghs_solver_tail_agree": (i32, [vp]),
+            "ghs_solver_tail_round": (i32, [vp, P(i32)]),
             "ghs_solver_reset": (i32, [vp]),
             "ghs_solver_cancel": (i32, [vp]),
             "ghs_solver_destroy": (i32, [vp]),

@@ -3582,10 +3582,20 @@ struct TailBufs {
   uint32_t *droot[2];  // round r's active roots (ascending dense ids): droot[r & 1]
   uint32_t *ghook;     // per dense root: CONNECT target (dense root) of its minimum edge
   uint64_t *gkey;      // per dense root: its minimum key (KEY_NONE: no outgoing edge)
+  uint64_t *gloc;      // several ranks: this rank's own minimum (gkey is then MIN-all-reduced)
   uint32_t *blive;     // per block: live edges of the round it streamed
   uint32_t *bcnt;      // per block: records in its region of the tail buffer
   uint32_t *rec;       // the tail buffer: da | db << 16
   uint64_t *rkey;      //   ... and the key
+};
+
+// A tail in progress (run_tail's batches, or the stepwise ghs_solver_tail_* calls of several ranks)
+struct TailRun {
+  TailBufs tb{};
+  const uint32_t *act0 = nullptr;
+  uint32_t F0 = 0, round0 = 0, lr0 = 0, r = 1;  // r: the next tail round to stream
+  unsigned hook_g = 1;
+  bool multi = false;
 };
 
 __global__ void k_tail_map(const uint32_t *__restrict__ act, const unsigned long long *__restrict__ d_nact, TailBufs tb) {
@@ -3760,8 +3770,11 @@ __global__ __launch_bounds__(TAIL_T) void k_tail_open(const uint32_t *__restrict
 // One active root per slot (root-list order): the blocks' minima reduced (16 row groups per slot)
 // with their other ends, the root's CONNECT target, its MSF flag. Block 0 also totals the
 // streamed round's live edges.
+// several ranks (multi): the minimum is this rank's only — kept in gloc as well, no MSF flag yet
+// (k_tail_xhook writes it once the ranks agree on the minimum)
 __global__ __launch_bounds__(256) void k_tail_hook(TailBufs tb, uint32_t r, uint8_t *__restrict__ in_mst,
-                                                   uint32_t nblocks, unsigned long long *__restrict__ err) {
+                                                   uint32_t nblocks, unsigned long long *__restrict__ err,
+                                                   bool multi) {
   __shared__ unsigned long long s_part[256];
   __shared__ uint32_t s_prow[256];
   TailCtl *c = tb.ctl;
@@ -3812,12 +3825,34 @@ __global__ __launch_bounds__(256) void k_tail_hook(TailBufs tb, uint32_t r, uint
       atomicOr(err, 2ull);
       o = LABEL_NONE;
       m = KEY_NONE;
-    } else {
+    } else if (!multi) {
       in_mst[(uint32_t)m] = 1;  // both members of a mutual pair mark the same edge
     }
   }
   tb.gkey[d] = m;
   tb.ghook[d] = o;
+  if (multi) tb.gloc[d] = m;
+}
+
+// Several ranks, between the MIN all-reduce of gkey and the MAX all-reduce of ghook: a root whose
+// global minimum is this rank's own keeps its CONNECT target (and the owner writes the MSF flag of
+// its own edge); every other root's target is withdrawn (LABEL_NONE = -1 under the int32 MAX), so
+// the all-reduce leaves the owner's target on every rank. Keys are (w << 32 | global eid): unique.
+__global__ __launch_bounds__(256) void k_tail_xhook(TailBufs tb, uint32_t r, uint8_t *__restrict__ in_mst,
+                                                    uint32_t e_lo, uint32_t e_hi) {
+  const TailCtl *c = tb.ctl;
+  if (c->done) return;
+  const uint32_t nroot = (uint32_t)c->nroots[r];
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nroot; i += gridDim.x * blockDim.x) {
+    const uint32_t d = tb.droot[r & 1][i];
+    const uint64_t g = tb.gkey[d];
+    if (g != KEY_NONE && g == tb.gloc[d]) {
+      const uint32_t eid = (uint32_t)g;
+      if (eid >= e_lo && eid < e_hi) in_mst[eid] = 1;
+    } else {
+      tb.ghook[d] = LABEL_NONE;
+    }
+  }
 }
 
 // Every block applies the last round's hooks (identical LDS computation in every block, over the
@@ -4177,6 +4212,9 @@ struct ghs_solver {
   unsigned csr_gsel = 0, csr_gfil = 0;        // ... and the grids they were computed for
   bool trow_ready = false;                    // k_csr_trow ran this solve (ends_of may use trow)
   bool lab_lazy = false;                      // one rank: lab not yet initialised (ensure_lab / k_jump_ident)
+  uint64_t last_nact_in = 0;                  // active fragments at the start of the last reported round
+  bool tail_step = false;                     // a stepwise tail in progress (ghs_solver_tail_begin)
+  TailRun trun;                               // ... its state
   uint8_t *in_mst = nullptr;
   hipStream_t stream = nullptr;
   ghs_config_t cfg{};
@@ -4532,7 +4570,7 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
   p = carve((local_edges / 256 + 8) * 4); if (s) s->trow = (uint32_t *)p;  // CSR: each 256-edge tile's row
   p = carve((SEG_MAX + 1) * 4); if (s) s->bsel = (uint32_t *)p;             // CSR: k_select's wave slices
   p = carve((SEG_G + 1) * 4); if (s) s->bfil = (uint32_t *)p;               // CSR: k_filter's block ranges
-  if (local_edges == m) {  // one rank: the LDS tail's arrays (its records go to the idle edge buffer)
+  {  // the LDS tail's arrays (its records go to the idle edge buffer); several ranks: dense levels
     p = carve(N * 4, stg); if (s) s->tail.dmap = (uint32_t *)p;
     p = carve((size_t)TAIL_G * TAIL_MAX * 8); if (s) s->tail.partial = (uint64_t *)p;
     p = carve((size_t)TAIL_G * TAIL_MAX * 2); if (s) s->tail.poth = (uint16_t *)p;
@@ -4542,6 +4580,7 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
     }
     p = carve(TAIL_MAX * 4); if (s) s->tail.ghook = (uint32_t *)p;
     p = carve(TAIL_MAX * 8); if (s) s->tail.gkey = (uint64_t *)p;
+    p = carve(TAIL_MAX * 8); if (s) s->tail.gloc = (uint64_t *)p;
     p = carve(TAIL_G * 4); if (s) s->tail.blive = (uint32_t *)p;
     p = carve(TAIL_G * 4); if (s) s->tail.bcnt = (uint32_t *)p;
     p = carve(sizeof(TailCtl)); if (s) s->tail.ctl = (TailCtl *)p;
@@ -5350,6 +5389,7 @@ static void push_stats(ghs_solver *s, uint32_t level_round, uint64_t live_in, ui
   st.level_arcs = level_round == 0 ? s->level_arcs : 0;
   st.live_arcs = live_in;
   st.active_components = nact_in;
+  s->last_nact_in = nact_in;
   st.hooks = edges_total - s->edges_before;
   s->edges_before = edges_total;
   s->stats.push_back(st);
@@ -5437,86 +5477,235 @@ static bool tail_usable(const ghs_solver *s) {
          !s->act_ident;
 }
 
-static int run_tail(ghs_solver *s, uint64_t prev_in) {
+// map + labels + open (round 0's stream of the tail)
+static void tail_start(ghs_solver *s, TailRun &t, bool multi) {
   hipStream_t st = s->stream;
   ensure_lab(s);
-  TailBufs tb = s->tail;
+  t.tb = s->tail;
   const ArcBuf &I = s->buf[s->cur], &O = s->buf[s->cur ^ 1];
-  tb.rec = O.src;  // the idle edge buffer holds the tail's records
-  tb.rkey = O.key;
+  t.tb.rec = O.src;  // the idle edge buffer holds the tail's records
+  t.tb.rkey = O.key;
   if (s->scan_pending) flush_scan(s);
-  const uint32_t *act0 = s->act[s->act_cur];
+  t.act0 = s->act[s->act_cur];
   const unsigned long long *d_nact = cur_act_count(s);
   SegView in{I.seg_start, I.seg_prefix, s->cur_nseg};
-  const uint32_t F0 = (uint32_t)s->nact;
-  const unsigned hook_g = (F0 + TAIL_HS - 1) / TAIL_HS;
-  const uint32_t round0 = s->round, lr0 = s->level_round;
-  unsigned long long *err = s->cnt + C_ERR;
-  {
-    KT(GHS_K_TAIL_OPEN, s->arcs_known ? s->cur_arcs : 0);
-    k_tail_map<<<grid_for(F0, 256, 64), 256, 0, st>>>(act0, d_nact, tb);
-    // the labels the edges carry: the previous round's list (after the level's identity round 0:
-    // every vertex)
-    const bool prev_ident = lr0 == 1;
-    const uint32_t *prev = prev_ident ? nullptr : s->act[s->act_cur ^ 1];
-    const unsigned long long *d_nprev = prev_ident ? s->cnt + C_N : act_count(s, s->act_cur ^ 1);
-    const uint64_t nprev_bound = prev_ident ? s->n : s->level_nact;
-    k_tail_labels<<<grid_for(nprev_bound, 256, 8192), 256, 0, st>>>(prev, d_nprev, s->lab, tb);
-    k_tail_open<<<TAIL_G, TAIL_T, 0, st>>>(I.src, I.dst, I.key, in, tb, s->check_totals);
-  }
-  {
-    KT(GHS_K_TAIL_HOOK, F0);
-    k_tail_hook<<<hook_g, 256, 0, st>>>(tb, 0, s->in_mst, TAIL_G, err);
-  }
+  t.F0 = (uint32_t)s->nact;
+  t.hook_g = (t.F0 + TAIL_HS - 1) / TAIL_HS;
+  t.round0 = s->round;
+  t.lr0 = s->level_round;
+  t.r = 1;
+  t.multi = multi;
+  KT(GHS_K_TAIL_OPEN, s->arcs_known ? s->cur_arcs : 0);
+  k_tail_map<<<grid_for(t.F0, 256, 64), 256, 0, st>>>(t.act0, d_nact, t.tb);
+  // the labels the edges carry: the previous round's list (after the level's identity round 0:
+  // every vertex; a dense level's: every dense label)
+  const bool prev_ident = t.lr0 == 1;
+  const uint32_t *prev = prev_ident ? nullptr : s->act[s->act_cur ^ 1];
+  const unsigned long long *d_nprev =
+      prev_ident ? s->cnt + (s->level_dense ? C_NDENSE : C_N) : act_count(s, s->act_cur ^ 1);
+  const uint64_t nprev_bound = prev_ident ? (s->level_dense ? s->dense_n : s->n) : s->level_nact;
+  k_tail_labels<<<grid_for(nprev_bound, 256, 8192), 256, 0, st>>>(prev, d_nprev, s->lab, t.tb);
+  k_tail_open<<<TAIL_G, TAIL_T, 0, st>>>(I.src, I.dst, I.key, in, t.tb, s->check_totals);
+}
+
+// round rr's hooks: every root's minimum over the blocks' rows (several ranks: this rank's own,
+// agreed by tail_agree between the caller's two all-reduces)
+static int tail_hook_local(ghs_solver *s, const TailRun &t, uint32_t rr) {
+  s->round = t.round0 + rr;  // the profile's round index: the round whose stream they reduce
+  KT(GHS_K_TAIL_HOOK, rr ? 0 : t.F0);
+  k_tail_hook<<<t.hook_g, 256, 0, s->stream>>>(t.tb, rr, s->in_mst, TAIL_G, s->cnt + C_ERR, t.multi);
   GHS_HIP_CHECK(hipGetLastError());
-  uint32_t r = 1;  // the next tail round to stream
-  uint32_t batch = tail_first_batch(F0, prev_in);
-  for (;;) {
-    const uint32_t last = std::min(r + batch - 1, TAIL_ROUNDS_MAX);  // the batch's last round
-    batch = TAIL_BATCH_NEXT;
-    for (; r <= last; ++r) {
-      s->round = round0 + r;  // the profile's round index of these launches
-      // round r - 1's hooks, unless the open's (launched above): a batch ends with a round, not with
-      // its hook kernel, so the round that finishes the level is not followed by a no-op hook launch
-      // when it closes its batch (the hook comes first in the next batch otherwise)
-      if (r > 1) {
-        s->round = round0 + r - 1;  // the hooks of round r - 1's stream: that round's launches
-        KT(GHS_K_TAIL_HOOK, 0);
-        k_tail_hook<<<hook_g, 256, 0, st>>>(tb, r - 1, s->in_mst, TAIL_G, err);
-      }
-      s->round = round0 + r;
-      KT(GHS_K_TAIL_ROUND, 0);
-      k_tail_round<<<TAIL_G, TAIL_T, 0, st>>>(tb, r, act0, s->lab, s->cnt, err);
-    }
-    GHS_HIP_CHECK(hipGetLastError());
-    const unsigned long long seq = ++s->res->seq;
-    RoundSlot *dslot = &s->d_slot[seq % SLOT_RING];
-    GHS_HIP_CHECK(hipMemcpyAsync(s->res->h_tail, tb.ctl, sizeof(TailCtl), hipMemcpyDeviceToHost, st));
-    k_tail_report<<<1, 1, 0, st>>>(tb, last, dslot, seq, s->cnt);
-    GHS_HIP_CHECK(hipGetLastError());
-    RoundSlot rep;
-    if (int rc = wait_slot(s, s->h_slot + (seq % SLOT_RING), seq, &rep)) return rc;
-    if (slot_err(rep.err)) return fail_counters(s, slot_err(rep.err), "in the LDS tail");
-    s->rep_weight = rep.weight;
-    s->rep_edges = rep.edges;
-    s->report_final = true;
-    if (s->debug)
-      fprintf(stderr, "[ghs] level %u tail batch report: nact_out %llu edges %llu weight %llu\n", s->level, rep.nact_out,
-              rep.edges, rep.weight);
-    if (rep.nact_out <= 1) break;
-    if (r > TAIL_ROUNDS_MAX) return fail_counters(s, 4, "in the LDS tail (round cap)");
-  }
+  return GHS_OK;
+}
+
+static int tail_agree(ghs_solver *s, const TailRun &t, uint32_t rr) {
+  s->round = t.round0 + rr;
+  KT(GHS_K_TAIL_HOOK, 0);
+  k_tail_xhook<<<t.hook_g, 256, 0, s->stream>>>(t.tb, rr, s->in_mst, (uint32_t)s->e_lo, (uint32_t)s->e_hi);
+  GHS_HIP_CHECK(hipGetLastError());
+  return GHS_OK;
+}
+
+static int tail_round_launch(ghs_solver *s, const TailRun &t, uint32_t r) {
+  s->round = t.round0 + r;
+  KT(GHS_K_TAIL_ROUND, 0);
+  k_tail_round<<<TAIL_G, TAIL_T, 0, s->stream>>>(t.tb, r, t.act0, s->lab, s->cnt, s->cnt + C_ERR);
+  GHS_HIP_CHECK(hipGetLastError());
+  return GHS_OK;
+}
+
+// the control block (and the report, checksummed) behind the tail's launches so far: *nact_out = 0
+// once the level is done
+static int tail_report(ghs_solver *s, const TailRun &t, uint32_t last, unsigned long long *nact_out) {
+  hipStream_t st = s->stream;
+  const unsigned long long seq = ++s->res->seq;
+  RoundSlot *dslot = &s->d_slot[seq % SLOT_RING];
+  GHS_HIP_CHECK(hipMemcpyAsync(s->res->h_tail, t.tb.ctl, sizeof(TailCtl), hipMemcpyDeviceToHost, st));
+  k_tail_report<<<1, 1, 0, st>>>(t.tb, last, dslot, seq, s->cnt);
+  GHS_HIP_CHECK(hipGetLastError());
+  RoundSlot rep;
+  if (int rc = wait_slot(s, s->h_slot + (seq % SLOT_RING), seq, &rep)) return rc;
+  if (slot_err(rep.err)) return fail_counters(s, slot_err(rep.err), "in the LDS tail");
+  s->rep_weight = rep.weight;
+  s->rep_edges = rep.edges;
+  s->report_final = true;
+  if (s->debug)
+    fprintf(stderr, "[ghs] level %u tail report: nact_out %llu edges %llu weight %llu\n", s->level, rep.nact_out,
+            rep.edges, rep.weight);
+  *nact_out = rep.nact_out;
+  return GHS_OK;
+}
+
+// the level is done (the last report read): the tail rounds' stats, then the level's close
+static int tail_finish(ghs_solver *s, const TailRun &t) {
   const TailCtl &c = *s->res->h_tail;
   const uint32_t rounds = std::min(c.rounds, TAIL_ROUNDS_MAX);
-  for (uint32_t t = 0; t < rounds; ++t) push_stats(s, lr0 + t, c.live[t], c.nroots[t], c.edges[t]);
-  s->round = round0 + rounds;
-  s->level_round = lr0 + rounds;
+  for (uint32_t k = 0; k < rounds; ++k) push_stats(s, t.lr0 + k, c.live[k], c.nroots[k], c.edges[k]);
+  s->round = t.round0 + rounds;
+  s->level_round = t.lr0 + rounds;
   s->tail_ran = true;
   if (s->ev_rec.size() > s->round) s->ev_rec.resize(s->round);
   if (int rc = check_level_totals(s)) return rc;
+  if (int rc = dense_close(s)) return rc;
   close_level(s);
   return GHS_OK;
 }
+
+// coll != nullptr: one rank of several (a dense level, ghs_solver_tail_multi) — each round's hooks
+// agree across the ranks through two small all-reduces (MIN of the F0 keys, MAX of the targets)
+static int run_tail(ghs_solver *s, uint64_t prev_in, const GhsTailColl *coll = nullptr) {
+  hipStream_t st = s->stream;
+  TailRun t;
+  tail_start(s, t, coll != nullptr);
+  auto hook = [&](uint32_t rr) -> int {
+    if (int rc = tail_hook_local(s, t, rr)) return rc;
+    if (coll) {
+      if (int rc = coll->min_u64(coll->ctx, t.tb.gkey, t.F0, st)) return rc;
+      if (int rc = tail_agree(s, t, rr)) return rc;
+      if (int rc = coll->max_i32(coll->ctx, reinterpret_cast<int32_t *>(t.tb.ghook), t.F0, st)) return rc;
+    }
+    return GHS_OK;
+  };
+  if (int rc = hook(0)) return rc;
+  uint32_t batch = tail_first_batch(t.F0, prev_in);
+  for (;;) {
+    const uint32_t last = std::min(t.r + batch - 1, TAIL_ROUNDS_MAX);  // the batch's last round
+    batch = TAIL_BATCH_NEXT;
+    for (; t.r <= last; ++t.r) {
+      // round r - 1's hooks, unless the open's (launched above): a batch ends with a round, not with
+      // its hook kernel, so the round that finishes the level is not followed by a no-op hook launch
+      // when it closes its batch (the hook comes first in the next batch otherwise)
+      if (t.r > 1)
+        if (int rc = hook(t.r - 1)) return rc;
+      if (int rc = tail_round_launch(s, t, t.r)) return rc;
+    }
+    unsigned long long nact_out = 0;
+    if (int rc = tail_report(s, t, last, &nact_out)) return rc;
+    if (nact_out <= 1) break;
+    if (t.r > TAIL_ROUNDS_MAX) return fail_counters(s, 4, "in the LDS tail (round cap)");
+  }
+  return tail_finish(s, t);
+}
+
+// The multi-rank loop's LDS tail (ghs_solver_run, multi.hip): at a round >= 1 of a dense level whose
+// active count is at most TAIL_MAX, the rounds still in flight are drained (their reports give the
+// exact count — every rank reads the same reports, so every rank takes the same branch), then the
+// level finishes in run_tail with the ranks' hooks agreed per round. Returns 0 when not applicable,
+// 1 when the level finished (in the drain or the tail), 2 when that ended the solve, or an error.
+int ghs_solver_tail_multi(ghs_solver *s, const GhsTailColl *coll) {
+  if (!s || !coll) return 0;
+  if (s->phase != 0 || !s->level_open || s->cfg.num_ranks <= 1 || !s->level_dense || !s->tail_on || !s->tail.ctl ||
+      s->act_ident || s->level_round < 1 || s->nact > TAIL_MAX)
+    return 0;
+  while (!s->pipe.empty()) {  // the rounds in flight (pipelined contract): their reports, in order
+    const ghs_solver::PipeRound p = s->pipe.front();
+    s->pipe.erase(s->pipe.begin());
+    RoundSlot rep;
+    if (int rc = wait_slot(s, s->h_slot + (p.seq % SLOT_RING), p.seq, &rep)) return rc;
+    if (slot_err(rep.err)) return fail_counters(s, slot_err(rep.err), ("in round " + std::to_string(p.round + 1)).c_str());
+    push_stats(s, p.level_round, s->pipe_live, rep.nact_in, rep.edges);
+    s->pipe_live = rep.live_out;
+    s->pipe_exact = rep.nact_out;
+    s->pipe_exact_lr = p.level_round + 1;
+    s->nact = rep.nact_out;
+    if (rep.nact_out <= 1) {  // the level ended with round p: the rounds enqueued after it are no-ops
+      s->pipe.clear();
+      s->round = p.round + 1;
+      s->level_round = p.level_round + 1;
+      if (int rc = dense_close(s)) return rc;
+      close_level(s);
+      return s->phase == 2 ? 2 : 1;
+    }
+  }
+  if (s->nact < 2) return 0;  // (the synchronous contract closes such a level itself)
+  if (int rc = run_tail(s, s->last_nact_in, coll)) return rc;
+  return s->phase == 2 ? 2 : 1;
+}
+
+static bool tail_step_usable(const ghs_solver *s) {
+  return s->phase == 0 && s->level_open && s->cfg.num_ranks > 1 && s->level_dense && s->tail_on && s->tail.ctl &&
+         !s->act_ident && s->level_round >= 1 && s->nact >= 2 && s->nact <= TAIL_MAX && s->pipe.empty();
+}
+
+extern "C" {
+
+// ---- the stepwise LDS tail (ABI 10; include/ghs_mst.h): the caller's collectives between the calls ----
+int ghs_solver_tail_begin(ghs_solver_t *s, uint64_t *num_fragments) {
+  if (!s || !num_fragments) GHS_FAIL(GHS_E_ARG, "solver/num_fragments is NULL");
+  *num_fragments = 0;
+  if (s->tail_step) GHS_FAIL(GHS_E_STATE, "a tail is already in progress");
+  if (!tail_step_usable(s)) return GHS_OK;
+  s->trun = TailRun();
+  tail_start(s, s->trun, true);
+  if (int rc = tail_hook_local(s, s->trun, 0)) return rc;
+  s->tail_step = true;
+  s->phase = 3;  // (minedge / contract refuse until the tail ends)
+  *num_fragments = s->trun.F0;
+  return GHS_OK;
+}
+
+int ghs_solver_tail_buffers(ghs_solver_t *s, uint64_t **d_keys, int32_t **d_hooks) {
+  if (!s || !d_keys || !d_hooks) GHS_FAIL(GHS_E_ARG, "solver/keys/hooks is NULL");
+  if (!s->tail_step) GHS_FAIL(GHS_E_STATE, "no tail in progress (ghs_solver_tail_begin)");
+  *d_keys = s->tail.gkey;
+  *d_hooks = reinterpret_cast<int32_t *>(s->tail.ghook);
+  return GHS_OK;
+}
+
+int ghs_solver_tail_agree(ghs_solver_t *s) {
+  if (!s) GHS_FAIL(GHS_E_ARG, "solver is NULL");
+  if (!s->tail_step) GHS_FAIL(GHS_E_STATE, "no tail in progress (ghs_solver_tail_begin)");
+  return tail_agree(s, s->trun, s->trun.r - 1);
+}
+
+int ghs_solver_tail_round(ghs_solver_t *s, int *state) {
+  if (!s || !state) GHS_FAIL(GHS_E_ARG, "solver/state is NULL");
+  *state = 0;
+  if (!s->tail_step) GHS_FAIL(GHS_E_STATE, "no tail in progress (ghs_solver_tail_begin)");
+  TailRun &t = s->trun;
+  if (t.r > TAIL_ROUNDS_MAX) {
+    s->tail_step = false;
+    return fail_counters(s, 4, "in the LDS tail (round cap)");
+  }
+  if (int rc = tail_round_launch(s, t, t.r)) return rc;
+  unsigned long long nact_out = 0;
+  if (int rc = tail_report(s, t, t.r, &nact_out)) {
+    s->tail_step = false;
+    return rc;
+  }
+  if (nact_out <= 1) {
+    s->tail_step = false;
+    s->phase = 0;
+    if (int rc = tail_finish(s, t)) return rc;
+    *state = s->phase == 2 ? 2 : 1;
+    return GHS_OK;
+  }
+  if (int rc = tail_hook_local(s, t, t.r)) return rc;
+  ++t.r;
+  return GHS_OK;
+}
+
+}  // extern "C"
 
 
 static int run_level_pipelined(ghs_solver *s) {

@@ -69,6 +69,14 @@ void ghs_solver_set_group_cancel(ghs_solver *s, const int *flag);
 bool ghs_solver_cancelled_of(const ghs_solver *s);
 // the multi-rank round loop's contract: rounds >= 2 of a level pipelined (no host sync)
 int ghs_solver_contract_async(ghs_solver *s, int *done);
+// the multi-rank loop's LDS tail: the collectives it needs, enqueued on the solver's stream
+struct GhsTailColl {
+  void *ctx;
+  int (*min_u64)(void *ctx, uint64_t *buf, size_t count, hipStream_t st);  // in place, MIN
+  int (*max_i32)(void *ctx, int32_t *buf, size_t count, hipStream_t st);   // in place, MAX
+};
+// 0: not applicable (run the round as usual); 1: the level finished; 2: so did the solve; < 0: error
+int ghs_solver_tail_multi(ghs_solver *s, const GhsTailColl *coll);
 const ghs_config_t *ghs_solver_cfg_of(const ghs_solver *s);
 uint32_t ghs_solver_round_of(const ghs_solver *s);
 // pinned host resources of a solver (report ring, counters mirror, events), kept across solves by

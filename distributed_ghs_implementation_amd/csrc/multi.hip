@@ -307,6 +307,13 @@ int run_loop(ghs_solver_t *s, ghs_comm *c) {
     LOOP_CHECK(comm_scratch(c, ghs_solver_n_of(s)));
   }
   const ghs_config_t *cf = ghs_solver_cfg_of(s);
+  const GhsTailColl tcoll{c,
+                          [](void *x, uint64_t *b, size_t n, hipStream_t q) {
+                            return coll_allreduce<uint64_t>(static_cast<ghs_comm *>(x), b, n, q);
+                          },
+                          [](void *x, int32_t *b, size_t n, hipStream_t q) {
+                            return coll_allreduce<int32_t>(static_cast<ghs_comm *>(x), b, n, q);
+                          }};
   for (uint32_t guard = 0;; ++guard) {
     if (guard > 16 * GHS_MAX_ROUND_STATS) {
       ghs::set_error("round cap exceeded");
@@ -317,6 +324,12 @@ int run_loop(ghs_solver_t *s, ghs_comm *c) {
     if (multi && cf->fault_round && cf->fault_rank == (uint32_t)c->rank + 1 && ghs_solver_round_of(s) >= cf->fault_round) {
       ghs::set_error("injected mid-solve failure (fault_round)");
       return loop_fail(c, GHS_E_STATE);
+    }
+    if (multi) {  // a dense level's last rounds in the LDS tail (few active fragments)
+      const int t = ghs_solver_tail_multi(s, &tcoll);
+      if (t < 0) return loop_fail(c, t);
+      if (t == 2) return GHS_OK;
+      if (t == 1) continue;
     }
     uint64_t count = 0;
     int rc = ghs_solver_minedge(s, &count);

@@ -141,6 +141,32 @@ class HipStepper:
         _native.check(self.L.ghs_solver_contract(self.h, ctypes.byref(d)))
         return bool(d.value)
 
+    # ---- the LDS tail of a dense level (ABI 10, include/ghs_mst.h ghs_solver_tail_*) ----
+    def tail_begin(self):
+        """0: no tail now (continue with minedge); else F, the tail's fragments: this rank's round-0
+        minima are in tail_buffers()[0]."""
+        f = ctypes.c_uint64(0)
+        _native.check(self.L.ghs_solver_tail_begin(self.h, ctypes.byref(f)))
+        return int(f.value)
+
+    def tail_buffers(self, F):
+        """(keys: F uint64 as an int64 view — MIN-all-reduce them as UNSIGNED, hooks: F int32 —
+        MAX-all-reduce them), device tensors over the solver's workspace."""
+        k, h = ctypes.c_void_p(0), ctypes.c_void_p(0)
+        _native.check(self.L.ghs_solver_tail_buffers(self.h, ctypes.byref(k), ctypes.byref(h)))
+        dev, ws = self.e.edges.device, self.e.ws
+        return (_device_u8_view(k.value, 8 * F, dev, ws).view(torch.int64),
+                _device_u8_view(h.value, 4 * F, dev, ws).view(torch.int32))
+
+    def tail_agree(self):
+        _native.check(self.L.ghs_solver_tail_agree(self.h))
+
+    def tail_round(self):
+        """0: the next tail round's minima are in the keys; 1: the level is done; 2: the solve is."""
+        st = ctypes.c_int(0)
+        _native.check(self.L.ghs_solver_tail_round(self.h, ctypes.byref(st)))
+        return int(st.value)
+
     def run_native(self, comm):
         """The whole round loop in the library (ghs_solver_run): collectives over `comm` (a
         _native.Comm, RCCL on the solver's stream), one host call per solve."""
@@ -174,6 +200,15 @@ class HipStepper:
             pass
 
 
+def allreduce_min_unsigned(allreduce_min, t):
+    """MIN-all-reduce an int64 view of uint64 values as unsigned (the sign bit flipped around a
+    signed MIN: order-preserving), in place."""
+    sign = torch.tensor(-(1 << 63), dtype=torch.int64, device=t.device)
+    t.bitwise_xor_(sign)
+    allreduce_min(t)
+    t.bitwise_xor_(sign)
+
+
 def run_rounds(stepper, allreduce_min, max_rounds=4096, allreduce_max=None, allgather=None, rs=None):
     """The level loop shared by every backend: (level open: OR the fragment flags), min-edge,
     all-reduce MIN, (a level's first round: owner-computes hook, all-reduce MAX), contract.
@@ -196,7 +231,23 @@ def run_rounds(stepper, allreduce_min, max_rounds=4096, allreduce_max=None, allg
     rs = rs or getattr(allreduce_min, "rs", None)
     gather = allgather or getattr(allreduce_min, "gather", None)
     use_bits = gather is not None and hasattr(stepper, "flag_bits")
+    tail_begin = getattr(stepper, "tail_begin", None)
     while True:
+        # a dense level's LDS tail (ABI 10): per round a MIN of F keys and a MAX of F hooks
+        F = tail_begin() if tail_begin is not None else 0
+        if F:
+            keys, hooks = stepper.tail_buffers(F)
+            while True:
+                allreduce_min_unsigned(allreduce_min, keys)
+                stepper.tail_agree()
+                (allreduce_max or allreduce_min.max)(hooks)
+                state = stepper.tail_round()
+                rounds += 1
+                if state:
+                    break
+            if state == 2:
+                return rounds
+            continue
         count = stepper.minedge()
         while count is None:  # a level opened: its active fragments = flagged on ANY rank
             if use_bits:

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GHS_MST_ABI_VERSION 9
+#define GHS_MST_ABI_VERSION 10
 
 #define GHS_OK 0
 #define GHS_NEED_EXCHANGE 1   /* ghs_solver_minedge on a multi-rank solver opened a level: OR-combine
@@ -307,6 +307,27 @@ int ghs_solver_unpack_hook(ghs_solver_t *h, const int32_t *d_dense);
 int ghs_solver_hook_slots(ghs_solver_t *h, uint32_t nranks, uint64_t **d_slots, uint64_t *padded);
 int ghs_solver_hook_owner(ghs_solver_t *h, uint32_t rank, uint64_t per_rank, uint64_t *d_pairs);
 int ghs_solver_apply_hooks(ghs_solver_t *h, const uint64_t *d_pairs, uint64_t **d_partial);
+/* optional (ABI 10), at the top of the loop (before minedge), several ranks: the LDS tail of a
+ * dense level — its last rounds (ghs_implementation_mpi.py:673-748 once few fragments remain, the
+ * REPORT / CHANGEROOT convergecasts of ghs_implementation.py:235-387) with the fragments renumbered
+ * 0..F-1 and each round's minima kept in LDS, so a round moves 12 bytes per fragment on the wire
+ * instead of a min-edge + hook over n-sized arrays:
+ *   tail_begin(h, &F)              F = 0: not applicable now (call minedge as usual); else the tail
+ *                                  opened and this rank's minima of its round 0 are in `keys`
+ *   loop: tail_buffers(h, &keys, &hooks)    F uint64 keys, F int32 CONNECT targets (device)
+ *     <caller: all-reduce MIN (UNSIGNED 64-bit) of keys[0:F], in place>
+ *     tail_agree(h)                the owner of each minimum keeps its target and writes the MSF
+ *                                  flag of its own edge; the other ranks withdraw theirs (-1)
+ *     <caller: all-reduce MAX (int32) of hooks[0:F], in place>
+ *     tail_round(h, &state)        the hooks applied, the next round streamed (one host sync);
+ *                                  state 0: the next round's minima are in keys (loop); 1: the level
+ *                                  is complete (continue with minedge); 2: so is the solve (finish)
+ * Every rank takes the same branch (the counts are identical on every rank). ghs_solver_run runs the
+ * same tail with its own collectives (several rounds per host sync). */
+int ghs_solver_tail_begin(ghs_solver_t *h, uint64_t *num_fragments);
+int ghs_solver_tail_buffers(ghs_solver_t *h, uint64_t **d_keys, int32_t **d_hooks);
+int ghs_solver_tail_agree(ghs_solver_t *h);
+int ghs_solver_tail_round(ghs_solver_t *h, int *state);
 /* hook + jump + next list; *done = 1 when every level is complete */
 int ghs_solver_contract(ghs_solver_t *h, int *done);
 int ghs_solver_finish(ghs_solver_t *h, ghs_result_t *result, ghs_round_stats_t *stats);

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi():
     L = _native.load()
-    assert L.ghs_abi_version() == _native.ABI_VERSION == 9
+    assert L.ghs_abi_version() == _native.ABI_VERSION == 10
     assert _native.device_count() >= 0
 
 

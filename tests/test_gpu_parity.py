@@ -176,6 +176,32 @@ def _emulate_ranks(e, world, cfg=None, bitmaps=True, rs=False):
     try:
         done = False
         while not done:
+            # a dense level's LDS tail (ABI 10): MIN of the F keys (unsigned), agree, MAX of the hooks
+            F = [s.tail_begin() for s in steppers]
+            assert len(set(F)) == 1
+            if F[0]:
+                bufs = [s.tail_buffers(F[0]) for s in steppers]
+                sign = torch.tensor(-(1 << 63), dtype=torch.int64, device=bufs[0][0].device)
+                while True:
+                    red = bufs[0][0] ^ sign
+                    for k, _ in bufs[1:]:
+                        red = torch.minimum(red, k ^ sign)
+                    red ^= sign
+                    for k, _ in bufs:
+                        k.copy_(red)
+                    for s in steppers:
+                        s.tail_agree()
+                    hmax = bufs[0][1].clone()
+                    for _, h in bufs[1:]:
+                        hmax = torch.maximum(hmax, h)
+                    for _, h in bufs:
+                        h.copy_(hmax)
+                    states = [s.tail_round() for s in steppers]
+                    assert len(set(states)) == 1
+                    if states[0]:
+                        break
+                done = states[0] == 2
+                continue
             counts = [s.minedge() for s in steppers]
             while counts[0] is None:  # a level opened: OR-combine the fragment flags
                 assert all(c is None for c in counts)
@@ -401,6 +427,32 @@ def test_native_loop_emulated_vs_oracle(world, graph, torch_cuda):
     # rounds >= 2 of a level are pipelined (read from the round reports): every round's stats once
     assert sum(st["hooks"] for st in stats) == ref_k or res.rounds > len(stats)
     assert res.rounds == len(stats) or res.rounds > 64
+
+
+@pytest.mark.parametrize("world,graph", [(2, "rmat"), (8, "rmat"), (3, "ties"), (4, "grid"), (5, "grid-gradient"),
+                                         (4, "forest"), (8, "rmat20"), (8, "readme")])
+def test_native_loop_multi_rank_tail_vs_oracle(world, graph, torch_cuda):
+    """The LDS tail in the multi-rank loop (a dense level once <= TAIL_MAX fragments stay active:
+    ghs_solver_tail_multi drains the pipelined rounds, then every tail round's hooks are agreed by
+    a MIN all-reduce of the F0 keys and a MAX all-reduce of the CONNECT targets; the owner rank
+    writes the MSF flag): flags and totals equal oracle Kruskal and the loop without the tail
+    (GHS_OPT_NO_TAIL); pass_flags bit 3 says the tail ran."""
+    from distributed_ghs_implementation_amd import _native
+    from distributed_ghs_implementation_amd.device import emulated_mst
+    ora = _oracle()
+    e = _test_graph(graph)
+    g = e.to_host()
+    ref_in, ref_tw, ref_k = ora.kruskal_c(g.n, g.u, g.v, g.w)
+    res, stats, flags = emulated_mst(e, world)
+    res0, _, flags0 = emulated_mst(e, world, config=_native.make_config(options=_native.OPT_NO_TAIL))
+    for r, f in ((res, flags), (res0, flags0)):
+        assert np.array_equal(f.cpu().numpy().astype(bool), ref_in.astype(bool))
+        assert (r.total_weight, r.num_mst_edges) == (ref_tw, ref_k)
+    assert not res0.pass_flags & 8
+    if graph in ("rmat", "rmat20", "grid", "ties"):
+        assert res.pass_flags & 8
+    assert sum(st["hooks"] for st in stats) == ref_k
+    assert res.rounds == len(stats)
 
 
 @pytest.mark.parametrize("dedup_max", [128, 1000000000])

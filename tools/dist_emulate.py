@@ -86,9 +86,56 @@ def main():
                 s.reset()
         rounds = []
         done = False
+        carry = [0.0] * W  # a tail's finishing round: counted with the next level's first round
         while not done:
-            ms = [0.0] * W
+            ms, carry = carry, [0.0] * W
             coll = []
+            # a dense level's LDS tail (ABI 10): one entry per tail round (its collectives not timed)
+            F = []
+            for r, s in enumerate(steppers):
+                f, t = timed(r, s.tail_begin)
+                F.append(f)
+                ms[r] += t
+            assert len(set(F)) == 1
+            if F[0]:
+                bufs = [s.tail_buffers(F[0]) for s in steppers]
+                sign = torch.tensor(-(1 << 63), dtype=torch.int64, device=bufs[0][0].device)
+                while True:
+                    red = bufs[0][0] ^ sign
+                    for k, _ in bufs[1:]:
+                        red = torch.minimum(red, k ^ sign)
+                    red ^= sign
+                    for k, _ in bufs:
+                        k.copy_(red)
+                    for r, s in enumerate(steppers):
+                        _, t = timed(r, s.tail_agree)
+                        ms[r] += t
+                    hmax = bufs[0][1].clone()
+                    for _, h in bufs[1:]:
+                        hmax = torch.maximum(hmax, h)
+                    for _, h in bufs:
+                        h.copy_(hmax)
+                    coll = [("allreduce_min_u64", F[0] * 8), ("allreduce_max_i32", F[0] * 4)]
+                    states = []
+                    tr = [0.0] * W
+                    for r, s in enumerate(steppers):
+                        st, t = timed(r, s.tail_round)
+                        states.append(st)
+                        tr[r] = t
+                    assert len(set(states)) == 1
+                    if states[0]:  # the finishing round applies the last hooks and closes the level
+                        rounds.append({"max_rank_ms": round(max(ms), 4), "min_rank_ms": round(min(ms), 4),
+                                       "collectives": coll, "tail": True})
+                        carry = tr
+                        break
+                    rounds.append({"max_rank_ms": round(max(ms), 4), "min_rank_ms": round(min(ms), 4),
+                                   "collectives": coll, "tail": True})
+                    ms = tr
+                if states[0] == 2:
+                    rounds.append({"max_rank_ms": round(max(carry), 4), "min_rank_ms": round(min(carry), 4),
+                                   "collectives": [], "tail": True})
+                    done = True
+                continue
             counts = []
             for r, s in enumerate(steppers):
                 c, t = timed(r, s.minedge)
