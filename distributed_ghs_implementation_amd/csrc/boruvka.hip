@@ -312,9 +312,9 @@ __device__ __forceinline__ void st_b64(uint64_t v, __amdgpu_buffer_rsrc_t r, uin
 // — the north_star's "CSR edge list in HBM", u implied: edge e of row r has u = r for
 // off[r] <= e < off[r + 1]. The streaming passes then read 8 B per edge plus ~4 B per row instead of
 // 12 B per edge.
-// Per solve, k_csr_trow (one pass over off[], which it also validates) writes trow[t] = the row
-// holding edge E0 + 256 t for every 256-edge tile of the solver's range (trow[ntiles]: the row of its
-// last edge). A streaming wave derives u for a tile [t0, t0 + 256) from R0 = trow[t] and R1 =
+// Per solve, the CSR pre-pass (k_csr_range, k_csr_check: off[]'s validation, k_csr_tiles,
+// k_csr_bounds: the passes' cost-balanced partitions) writes trow[t] = the row holding edge
+// E0 + 256 t for every 256-edge tile of the solver's range (trow[ntiles]: the row of its last edge). A streaming wave derives u for a tile [t0, t0 + 256) from R0 = trow[t] and R1 =
 // trow[t + 1] (csr_tile_rows): the rows R0 + 1 .. R1 start inside the tile (or at its end); each
 // writes its id into the LDS slot of its first edge (ds_max: the empty rows before a nonempty one
 // share its slot), and a max-scan over the 256 slots (in-lane over a lane's 4, then a wave DPP scan)
@@ -326,7 +326,8 @@ __device__ __forceinline__ void st_b64(uint64_t v, __amdgpu_buffer_rsrc_t r, uin
 // (The first version walked windows from R0 until one passed the tile's end, a dependent round trip
 // per 64 rows: the waves owning the list's sparse end made k_select 1.9 ms against COO's 0.7.)
 // A gather of u by edge id (the fragment-form hooks: one per hooked fragment) is a binary search
-// over off[] (csr_row), unless the caller also passed u (Ends).
+// over the edge's tile rows (trow), or over off[] for another rank's edge (csr_row), unless the
+// caller also passed u (Ends).
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {  // inclusive max over the wave (gfx9 DPP)
   x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));  // row_shr:1
@@ -403,7 +404,7 @@ struct Ends {
   const uint32_t *off;   // CSR row offsets (n + 1 entries)
   const uint32_t *v;
   uint32_t n;
-  const uint32_t *trow;  // CSR: the rows of the solver's 256-edge tiles (k_csr_trow), nullptr before it ran
+  const uint32_t *trow;  // CSR: the rows of the solver's 256-edge tiles (k_csr_tiles), nullptr before it ran
   uint64_t E0, E1;       // ... its edges [E0, E1) (trow[ntiles] is the row of edge E1 - 1: edges of the
                          // last tile past E1 are another rank's, their rows may lie beyond it)
 };
@@ -1880,8 +1881,8 @@ __global__ __launch_bounds__(1024) void k_plan(const uint32_t *__restrict__ samp
 // labels are the endpoints); flags both ends active. Nothing else is written: the
 // heavier edges stay where they are until k_filter. Block-private output regions: deterministic,
 // no atomics; the next tile's loads are issued before the current one is compacted.
-// CSR (ABI 9): u is derived from the row offsets (csr_tile_rows, the tiles' rows from k_csr_trow,
-// which validated the offsets: a wave's slice is a multiple of 256 edges, so its tiles are trow's).
+// CSR (ABI 9): u is derived from the row offsets (csr_tile_rows, the tiles' rows from k_csr_tiles,
+// after k_csr_check validated the offsets: a wave's slice is a multiple of 256 edges, so its tiles are trow's).
 // ------------------------------------------------------------------------------------------
 // One pass over the row offsets of the solver's range [E0, e_hi) (T = e_hi - E0 edges), before
 // k_select:
@@ -1894,76 +1895,107 @@ __global__ __launch_bounds__(1024) void k_plan(const uint32_t *__restrict__ samp
 //    1024-edge tiles). A tile costs its edges and its rows (the windows of row starts it scans): the
 //    end of an R-MAT list holds the high vertex ids, which store few canonical edges — thousands of
 //    mostly empty rows per tile — and with equal edge counts its waves ran ~10x longer than the rest.
-//    Cost = CSR_EDGE_COST per edge + CSR_ROW_COST per row of the range; each row r of [Rb, Re] owns
+//    Cost = CSR_EDGE_COST per edge + a row cost per row of the range; each row r of [Rb, Re] owns
 //    the cost interval [C_r, C_r + len_r) (its row cost at its start, then its edges), the intervals
 //    tile [0, C_tot), and bound k = the position of cost k * C_tot / N, written by the row whose
 //    interval holds it (one writer per bound), rounded down to the tile grid.
-constexpr uint64_t CSR_EDGE_COST = 2, CSR_ROW_COST = 1;  // a row ~ half an edge: 8 windows (512 rows) a trip vs 256 edges
-// bound k (k < N) sits at cost k * S, S = ceil(Ctot / N): the row whose interval [C, C + len) holds it
-// writes it. k_lo = ceil(C / S) through a double reciprocal, corrected by exact integer products (a
-// 64-bit division per row made this pass ~0.17 ms at s24; C < 2^53)
-__device__ __forceinline__ void csr_bounds(uint64_t C, uint64_t len, uint64_t a, uint64_t S, double invS, uint32_t N,
-                                           uint32_t ts, uint32_t *__restrict__ bound) {
-  uint64_t k = (uint64_t)((double)C * invS);
-  while (k * S < C) ++k;
-  while (k > 0 && (k - 1) * S >= C) --k;
-  for (; k < N && k * S < C + len; ++k) {
-    const uint64_t d = k * S - C;
-    const uint64_t x = d < CSR_ROW_COST ? a : a + (d - CSR_ROW_COST) / CSR_EDGE_COST;
-    bound[k] = (uint32_t)(x / ts * ts);
+//    The row costs were measured per pass (R-MAT s24, same box, profiles/r06/csr/): k_select's wave
+//    slices at 2 edges per row (row cost 8) run 0.76 -> 0.58 ms against 0.5 edge (row cost 2), while
+//    k_filter's blocks are best near 0.5 edge per row (1.66 ms; 1.68 at 2 edges, 1.69 at 6).
+#ifndef GHS_CSR_ROW_SEL
+#define GHS_CSR_ROW_SEL 8
+#endif
+#ifndef GHS_CSR_ROW_FIL
+#define GHS_CSR_ROW_FIL 2
+#endif
+constexpr uint64_t CSR_EDGE_COST = 4, CSR_ROW_SEL = GHS_CSR_ROW_SEL, CSR_ROW_FIL = GHS_CSR_ROW_FIL;
+// Rb, Re: the rows of the range's first and last edges (one wave: a 64-ary search each), once per
+// solve, before the row pass and the bounds
+__global__ __launch_bounds__(64) void k_csr_range(const uint32_t *__restrict__ off, uint32_t n, uint64_t E0, uint64_t e_hi,
+                                                 uint32_t *__restrict__ rb) {
+  const uint32_t lane = threadIdx.x;
+  for (int q = 0; q < 2; ++q) {
+    const uint64_t e = q ? e_hi - 1 : E0;
+    uint32_t lo = 0, c = n ? n : 1;  // candidates [lo, lo + c): off[lo] <= e
+    while (c > 1) {
+      const uint32_t st = (c + WAVE - 1) / WAVE;
+      const bool in = lane * st < c;
+      const uint64_t bm = __ballot(in && off[lo + lane * st] <= e);
+      const uint32_t L = bm ? 63u - (uint32_t)__clzll((long long)bm) : 0u;
+      lo += L * st;
+      c = min(st, c - L * st);
+    }
+    if (lane == 0) rb[q] = lo;
   }
 }
 
-__global__ __launch_bounds__(256) void k_csr_trow(const uint32_t *__restrict__ off, uint32_t n, uint64_t m, uint64_t E0,
-                                                  uint64_t e_hi, uint32_t *__restrict__ trow,
-                                                  unsigned long long *__restrict__ err, uint32_t *__restrict__ bsel,
-                                                  uint32_t nsel, uint32_t *__restrict__ bfil, uint32_t nfil) {
-  __shared__ uint32_t s_rb[2];
-  const uint64_t T = e_hi - E0, ntiles = (T + 255) >> 8;
-  // Rb, Re: the rows of the range's first and last edges (wave 0: a 64-ary search each)
-  if (threadIdx.x < WAVE) {
-    const uint32_t lane = threadIdx.x;
-    for (int q = 0; q < 2; ++q) {
-      const uint64_t e = q ? e_hi - 1 : E0;
-      uint32_t lo = 0, c = n ? n : 1;  // candidates [lo, lo + c): off[lo] <= e
-      while (c > 1) {
-        const uint32_t st = (c + WAVE - 1) / WAVE;
-        const bool in = lane * st < c;
-        const uint64_t bm = __ballot(in && off[lo + lane * st] <= e);
-        const uint32_t L = bm ? 63u - (uint32_t)__clzll((long long)bm) : 0u;
-        lo += L * st;
-        c = min(st, c - L * st);
-      }
-      if (lane == 0) s_rb[q] = lo;
-    }
-  }
-  __syncthreads();
-  const uint64_t Rb = s_rb[0], Re = s_rb[1] < Rb ? Rb : s_rb[1];
-  const uint64_t Ctot = CSR_ROW_COST * (Re - Rb + 1) + CSR_EDGE_COST * T;
-  const uint64_t Ssel = (Ctot + nsel - 1) / nsel, Sfil = (Ctot + nfil - 1) / nfil;
-  const double iSsel = 1.0 / (double)Ssel, iSfil = 1.0 / (double)Sfil;
+// The offsets' validation: one coalesced pass over off (off[0] = 0, nondecreasing, off[n] = m).
+__global__ __launch_bounds__(256) void k_csr_check(const uint32_t *__restrict__ off, uint32_t n, uint64_t m,
+                                                   unsigned long long *__restrict__ err) {
   bool bad = false;
-  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t lo = off[r], hi = off[r + 1];
-    bad |= lo > hi;
-    if (lo > hi || r < Rb || r > Re) continue;  // invalid, or outside the range's rows
-    const uint64_t a = lo > E0 ? (lo < e_hi ? lo : e_hi) - E0 : 0, b = hi > E0 ? (hi < e_hi ? hi : e_hi) - E0 : 0;
-    const uint64_t C = CSR_ROW_COST * (r - Rb) + CSR_EDGE_COST * a, len = CSR_ROW_COST + CSR_EDGE_COST * (b - a);
-    csr_bounds(C, len, a, Ssel, iSsel, nsel, WAVE * 4, bsel);
-    csr_bounds(C, len, a, Sfil, iSfil, nfil, ARCS_PER_BLOCK, bfil);
-    if (a >= b) continue;  // empty (in the range)
-    for (uint64_t t = (a + 255) >> 8; (t << 8) < b; ++t) trow[t] = (uint32_t)r;
-    if (b == T) trow[ntiles] = (uint32_t)r;  // the row of edge e_hi - 1
+  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x)
+    bad |= off[r] > off[r + 1];
+  if (blockIdx.x == 0 && threadIdx.x == 0) bad |= (off[0] != 0u) | ((uint64_t)off[n] != m);
+  if (__any(bad) && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(err, 8ull);
+}
+
+// trow: one thread per tile — the row holding edge E0 + 256 t (t = ntiles: the range's last edge)
+// by a binary search over [Rb, Re] (its upper levels are shared by every tile, so they hit in the
+// caches). (A row pass that wrote each row's tiles left the wave of the R-MAT hub rows thousands of
+// tiles behind the rest, and computing the partitions there made it VALU-bound: ~0.1 ms at s24.)
+// Malformed offsets land the searches anywhere in [Rb, Re]; k_select then streams nothing.
+__global__ __launch_bounds__(256) void k_csr_tiles(const uint32_t *__restrict__ off, const uint32_t *__restrict__ rb,
+                                                   uint64_t E0, uint64_t e_hi, uint32_t *__restrict__ trow) {
+  const uint64_t T = e_hi - E0, ntiles = (T + 255) >> 8;
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (t > ntiles) return;
+  const uint64_t e = t < ntiles ? E0 + (t << 8) : e_hi - 1;
+  uint32_t lo = rb[0], hi = rb[1] < lo ? lo : rb[1];  // the last r with off[r] <= e
+  while (lo < hi) {
+    const uint32_t mid = lo + ((hi - lo + 1) >> 1);
+    if (off[mid] <= e) lo = mid; else hi = mid - 1;
   }
-  if (blockIdx.x == 0) {
-    if (threadIdx.x == 0) bad |= (off[0] != 0u) | ((uint64_t)off[n] != m);
-    // bounds no row owns (cost k * S past the total: small ranges), and the end
-    for (uint64_t k = threadIdx.x; k <= nsel; k += blockDim.x)
-      if (k == nsel || k * Ssel >= Ctot) bsel[k] = (uint32_t)T;
-    for (uint64_t k = threadIdx.x; k <= nfil; k += blockDim.x)
-      if (k == nfil || k * Sfil >= Ctot) bfil[k] = (uint32_t)T;
+  trow[t] = lo;
+}
+
+// The streaming passes' partitions: one thread per bound. The cumulative cost C(r) =
+// row_cost (r - Rb) + CSR_EDGE_COST a_r is nondecreasing in r, so bound k — the position of cost
+// k S, S = ceil(C_tot / N) — lies in the last row r with C(r) <= k S (a binary search over
+// [Rb, Re]); inside it, past the row's own cost, at edge a_r + (k S - C(r) - row_cost) / EDGE_COST,
+// rounded down to the pass's tile grid. k = N, and every k with k S >= C_tot, is the range's end.
+// bsel: k_select's nsel + 1 wave-slice bounds (256-edge tiles); bfil: k_filter's nfil + 1 block
+// bounds (1024-edge tiles). Malformed offsets (k_csr_check's err bit 8) make the searches land
+// anywhere in the range, never outside it: k_select then streams nothing.
+__global__ __launch_bounds__(256) void k_csr_bounds(const uint32_t *__restrict__ off, const uint32_t *__restrict__ rb,
+                                                    uint64_t E0, uint64_t e_hi, uint32_t *__restrict__ bsel,
+                                                    uint32_t nsel, uint32_t *__restrict__ bfil, uint32_t nfil) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > nsel + 1 + nfil) return;
+  const bool sel = i <= nsel;
+  const uint32_t k = sel ? i : i - (nsel + 1), N = sel ? nsel : nfil;
+  const uint64_t row = sel ? CSR_ROW_SEL : CSR_ROW_FIL, ts = sel ? WAVE * 4 : ARCS_PER_BLOCK;
+  uint32_t *bound = sel ? bsel : bfil;
+  const uint64_t T = e_hi - E0;
+  const uint32_t Rb = rb[0], Re = rb[1] < Rb ? Rb : rb[1];
+  const uint64_t Ctot = row * (uint64_t)(Re - Rb + 1) + CSR_EDGE_COST * T;
+  const uint64_t S = (Ctot + N - 1) / N, X = (uint64_t)k * S;
+  if (k == N || X >= Ctot) {
+    bound[k] = (uint32_t)T;
+    return;
   }
-  if (bad) atomicOr(err, 8ull);
+  auto pos = [&](uint32_t r) -> uint64_t {  // a_r: the row's first edge of the range, relative to E0
+    const uint64_t o = off[r];
+    return o > E0 ? (o < e_hi ? o : e_hi) - E0 : 0;
+  };
+  uint32_t lo = Rb, hi = Re;  // the last r with C(r) <= X (C(Rb) = 0 <= X)
+  while (lo < hi) {
+    const uint32_t mid = lo + ((hi - lo + 1) >> 1);
+    if (row * (uint64_t)(mid - Rb) + CSR_EDGE_COST * pos(mid) <= X) lo = mid; else hi = mid - 1;
+  }
+  const uint64_t a = pos(lo), d = X - (row * (uint64_t)(lo - Rb) + CSR_EDGE_COST * a);
+  uint64_t x = d < row ? a : a + (d - row) / CSR_EDGE_COST;
+  if (x > T) x = T;
+  bound[k] = (uint32_t)(x / ts * ts);
 }
 
 template <bool CSR>
@@ -1990,7 +2022,7 @@ GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t m, uint64_t e_lo, uint64_
   const uint64_t W = (uint64_t)gridDim.x * (BLOCK / WAVE);
   const uint64_t E0 = e_lo & ~3ull;
   const uint64_t T = e_hi - E0;
-  // CSR: the slices k_csr_trow balanced by cost (whole 256-edge tiles: the trow grid)
+  // CSR: the slices k_csr_bounds balanced by cost (whole 256-edge tiles: the trow grid)
   const uint64_t Q = ((T + W - 1) / W + 3) & ~3ull;
   const uint64_t vb = CSR ? bnd[gw] : Q * gw;
   const uint64_t ve = CSR ? bnd[gw + 1] : ((vb + Q < T) ? vb + Q : T);
@@ -2007,7 +2039,7 @@ GHS_STREAM_KERNEL_6 void k_select(uint32_t n, uint64_t m, uint64_t e_lo, uint64_
   // (R2, a scalar load one tile ahead), the first window of rows after R0 (prefetched), the last
   // edge's row of the previous tile
   uint32_t R0 = 0, R1 = 0, R2 = 0, w0 = 0, lastu = 0;
-  uint64_t vend = ve;  // CSR: an offsets error (k_csr_trow) empties the stream
+  uint64_t vend = ve;  // CSR: an offsets error (k_csr_check) empties the stream
   if (CSR) {
     reinterpret_cast<uint4 *>(s_head[wid])[lane] = make_uint4(0u, 0u, 0u, 0u);
     if (*err & 8ull) vend = vb;
@@ -2141,7 +2173,7 @@ __global__ __launch_bounds__(BLOCK, (CSR && GHS_FILTER_CSR_W8) ? 8 : GHS_STREAM_
   __shared__ WaveStage s_stage[BLOCK / WAVE];
   const uint64_t E0 = e_lo & ~3ull;
   const uint64_t T = e_hi - E0;
-  // CSR: the block ranges k_csr_trow balanced by cost (whole 1024-edge tiles, so every wave's 256-edge
+  // CSR: the block ranges k_csr_bounds balanced by cost (whole 1024-edge tiles, so every wave's 256-edge
   // part starts on the trow grid)
   const uint64_t Q = ((T + gridDim.x - 1) / gridDim.x + 3) & ~3ull;
   const uint64_t vb = CSR ? bnd[blockIdx.x] : Q * blockIdx.x;
@@ -2158,7 +2190,7 @@ __global__ __launch_bounds__(BLOCK, (CSR && GHS_FILTER_CSR_W8) ? 8 : GHS_STREAM_
   bool touch_giant = false;  // a level edge of this block has an end in the giant
   uint64_t nlev = 0, nrem = 0;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
-  // CSR: the rows of the wave's part of the tile (k_csr_trow's trow: R0 holds its first edge, R1
+  // CSR: the rows of the wave's part of the tile (k_csr_tiles' trow: R0 holds its first edge, R1
   // its end), the next tile's part's (loaded a tile ahead), and this part's first window (prefetched)
   const uint64_t ntiles = (T + 255) >> 8;
   auto trow_at = [&](uint64_t t) -> uint32_t { return trow[t < ntiles ? t : ntiles]; };
@@ -4207,10 +4239,10 @@ struct ghs_solver {
   const uint32_t *eu = nullptr, *ev = nullptr, *ew = nullptr;
   const uint32_t *eoff = nullptr;  // CSR input (ABI 9): row offsets, eu == nullptr (or the caller's u for gathers)
   bool csr = false;
-  uint32_t *trow = nullptr;        // CSR: the row of every 256-edge tile of the range (k_csr_trow)
+  uint32_t *trow = nullptr;        // CSR: the row of every 256-edge tile of the range (k_csr_tiles)
   uint32_t *bsel = nullptr, *bfil = nullptr;  // CSR: k_select's / k_filter's cost-balanced partitions
   unsigned csr_gsel = 0, csr_gfil = 0;        // ... and the grids they were computed for
-  bool trow_ready = false;                    // k_csr_trow ran this solve (ends_of may use trow)
+  bool trow_ready = false;                    // k_csr_tiles ran this solve (ends_of may use trow)
   bool lab_lazy = false;                      // one rank: lab not yet initialised (ensure_lab / k_jump_ident)
   uint64_t last_nact_in = 0;                  // active fragments at the start of the last reported round
   bool tail_step = false;                     // a stepwise tail in progress (ghs_solver_tail_begin)
@@ -4568,7 +4600,7 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
   if (s) s->cap_arcs = cap;
   p = carve(C_COUNT * sizeof(unsigned long long)); if (s) s->cnt = (unsigned long long *)p;
   p = carve((local_edges / 256 + 8) * 4); if (s) s->trow = (uint32_t *)p;  // CSR: each 256-edge tile's row
-  p = carve((SEG_MAX + 1) * 4); if (s) s->bsel = (uint32_t *)p;             // CSR: k_select's wave slices
+  p = carve((SEG_MAX + 3) * 4); if (s) s->bsel = (uint32_t *)p;             // CSR: k_select's wave slices (+ Rb, Re)
   p = carve((SEG_G + 1) * 4); if (s) s->bfil = (uint32_t *)p;               // CSR: k_filter's block ranges
   {  // the LDS tail's arrays (its records go to the idle edge buffer); several ranks: dense levels
     p = carve(N * 4, stg); if (s) s->tail.dmap = (uint32_t *)p;
@@ -4797,9 +4829,13 @@ static int open_level(ghs_solver *s, bool async_open = false) {
                                resident_grid((const void *)filt, BLOCK, s->seg_g, GHS_RESIDENT_GRIDS || !GHS_FILTER_CSR_W8));
         s->trow_ready = true;
         KT(GHS_K_CSR_TROW, s->n);
-        k_csr_trow<<<grid_for(s->n, 256, 2048), 256, 0, st>>>(s->eoff, s->n, s->m, s->e_lo & ~3ull, s->e_hi, s->trow,
-                                                             s->cnt + C_ERR, s->bsel, G * (BLOCK / WAVE), s->bfil,
-                                                             s->csr_gfil);
+        uint32_t *rb = s->bsel + SEG_MAX + 1;  // (2 words past k_select's bounds)
+        const uint32_t nsel = G * (BLOCK / WAVE), nfil = s->csr_gfil;
+        k_csr_range<<<1, 64, 0, st>>>(s->eoff, s->n, s->e_lo & ~3ull, s->e_hi, rb);
+        k_csr_check<<<grid_for(s->n, 256 * 8, 2048), 256, 0, st>>>(s->eoff, s->n, s->m, s->cnt + C_ERR);
+        k_csr_tiles<<<(unsigned)((TC + 255) / 256 / 256 + 1), 256, 0, st>>>(s->eoff, rb, s->e_lo & ~3ull, s->e_hi, s->trow);
+        k_csr_bounds<<<(nsel + nfil + 2 + 255) / 256, 256, 0, st>>>(s->eoff, rb, s->e_lo & ~3ull, s->e_hi, s->bsel, nsel,
+                                                                    s->bfil, nfil);
       }
       GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[0], st));
       {
