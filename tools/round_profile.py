@@ -40,10 +40,11 @@ def main():
         last[st["level"]] = i
     for r in recs:
         ok = r["round"] < len(stats) and stats[r["round"]]["level"] == r["level"]
-        # past a level's rounds: the LDS tail's finishing launch (the round after the level's last:
-        # it applies that round's hooks and writes the level's labels) or a launch that found the
-        # level done (a no-op)
-        fin = not ok and r["round"] == last.get(r["level"], -2) + 1
+        # past a level's rounds: the LDS tail's finishing k_tail_round (the round after the level's
+        # last: it applies that round's hooks and writes the level's labels), or a no-op — a tail
+        # launch after the finishing one, or a lookahead round of the pipelined loop enqueued before
+        # the report that ended the level was read (its kernels exit on the device count)
+        fin = not ok and r["round"] == last.get(r["level"], -2) + 1 and r["kernel"] == "k_tail_round"
         key = r["round"] if ok else ("finish" if fin else "noop", r["level"])
         per[key][r["kernel"]] += r["ms"]
     tot = sum(r["ms"] for r in recs)
