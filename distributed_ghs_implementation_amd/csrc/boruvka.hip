@@ -3419,7 +3419,11 @@ __global__ void k_round_report(RoundSlot *slot, unsigned long long seq, const un
 //    re-polled until every tag matches; a granule of another launch carries another tag). No
 //    ticket counter: one device-scope counter costs ~12 ns per arrival (MI355X_MICROARCH.md,
 //    fanin) — 50 us for 4096 tiles, measured.
-//  - pass 2 re-reads the flags and writes the tile's items at its prefix.
+//  - pass 2 takes the keep bits again (from LDS when the tile has at most LB_KEEP_G groups, n <=
+//    2^28 items: pass 1 kept them; else from the flags) and writes the tile's items at its prefix;
+//    each wave owns a contiguous quarter of the tile and places its items by wave scans (the first
+//    version's block-wide scan per 4096-item group cost two barriers each: 128 per tile on the
+//    16384^2 grid's 268M-vertex selects).
 //  - the last tile's prefix + count is the total: that block writes *d_total and, for a round,
 //    the round report (live, active, edges, err, seq) to the pinned slot.
 //  - every spin is bounded: a timeout sets err bit 16 and the block writes nothing.
@@ -3431,6 +3435,7 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 constexpr uint32_t LB_MAX_TILES = 1024;
 constexpr uint32_t LB_GROUP = BLOCK * 16;     // items per group: 16 keep bytes per lane (one 16-B load)
 constexpr uint32_t LB_MAX_SPINS = 1u << 16;   // x (load latency + s_sleep) ~ 0.1 s, never reached in a sane run
+constexpr uint32_t LB_KEEP_G = 64;            // tiles of up to 64 groups keep pass 1's bits in LDS (32 KiB)
 
 __device__ __forceinline__ unsigned long long lb_granule(uint32_t tag, uint32_t v) {
   return ((unsigned long long)tag << 32) | v;
@@ -3488,18 +3493,34 @@ __global__ __launch_bounds__(BLOCK) void k_select_lb(const uint8_t *__restrict__
   __shared__ uint32_t s_wcnt[BLOCK / WAVE];
   __shared__ uint64_t s_excl;
   __shared__ int s_ok;
+  __shared__ uint16_t s_keep[LB_KEEP_G * BLOCK];  // pass 1's keep bits (G <= LB_KEEP_G): no re-read
   const uint32_t t = blockIdx.x;
   const uint64_t count = *d_count;
-  const uint64_t tb = (uint64_t)t * groups * LB_GROUP;  // first item of the tile
-  // groups holding items below the count (block-uniform): a lookahead round's select over an
-  // upper-bound grid finds few or no items and skips the rest of its tile
-  const uint32_t live_groups =
-      tb >= count ? 0u : (uint32_t)umin64((uint64_t)groups, (count - tb + LB_GROUP - 1) / LB_GROUP);
+  // the tile [tb, tb + G * LB_GROUP) as four contiguous wave ranges of G chunks of 1024 items (16
+  // keep bytes per lane per chunk): each wave finds its items' positions with wave scans only (no
+  // block barrier per chunk), in item order
+  const uint32_t lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+  constexpr uint32_t CHUNK = WAVE * 16;
+  const uint64_t tb = (uint64_t)t * groups * LB_GROUP;
+  const uint64_t wb = tb + (uint64_t)wid * groups * CHUNK;  // the wave's first item
+  const uint32_t wl = wb >= count ? 0u : (uint32_t)umin64((uint64_t)groups, (count - wb + CHUNK - 1) / CHUNK);
+  const bool keep_lds = groups <= LB_KEEP_G;
   uint32_t mine = 0;  // kept items of this lane (pass 1)
-  for (uint32_t g = 0; g < live_groups; ++g)
-    mine += __popc(keep_bits16(flags, tb + (uint64_t)g * LB_GROUP + (uint64_t)threadIdx.x * 16, count));
-  uint32_t tot;
-  (void)block_offsets(mine, s_wcnt, &tot);  // block total (barriers inside)
+  for (uint32_t c = 0; c < wl; ++c) {
+    const uint32_t bits = keep_bits16(flags, wb + (uint64_t)c * CHUNK + (uint64_t)lane * 16, count);
+    if (keep_lds) s_keep[(wid * groups + c) * WAVE + lane] = (uint16_t)bits;
+    mine += __popc(bits);
+  }
+#pragma unroll
+  for (int d = WAVE / 2; d > 0; d >>= 1) mine += __shfl_xor(mine, d);
+  if (lane == 0) s_wcnt[wid] = mine;
+  __syncthreads();
+  uint32_t tot = 0, wbefore = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < BLOCK / WAVE; ++w) {
+    wbefore += w < wid ? s_wcnt[w] : 0u;
+    tot += s_wcnt[w];
+  }
   if (threadIdx.x == 0) {
     __hip_atomic_store((gu64 *)state + t, lb_granule(tag, tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_excl = 0;
@@ -3516,20 +3537,25 @@ __global__ __launch_bounds__(BLOCK) void k_select_lb(const uint8_t *__restrict__
   }
   __syncthreads();
   if (!s_ok) return;
-  // pass 2: the keep bytes again (L2-resident) -> out, in item order
-  uint64_t run = s_excl;
-  for (uint32_t g = 0; g < live_groups; ++g) {
-    const uint64_t i0 = tb + (uint64_t)g * LB_GROUP + (uint64_t)threadIdx.x * 16;
-    uint32_t bits = keep_bits16(flags, i0, count);
-    uint32_t gt;
-    const uint32_t before = block_offsets((uint32_t)__popc(bits), s_wcnt, &gt);
-    uint64_t pos = run + before;
+  // pass 2: the keep bits again (LDS, or the flags) -> out, in item order
+  uint64_t run = s_excl + wbefore;
+  for (uint32_t c = 0; c < wl; ++c) {
+    const uint64_t i0 = wb + (uint64_t)c * CHUNK + (uint64_t)lane * 16;
+    uint32_t bits = keep_lds ? (uint32_t)s_keep[(wid * groups + c) * WAVE + lane] : keep_bits16(flags, i0, count);
+    const uint32_t k0 = (uint32_t)__popc(bits);
+    uint32_t incl = k0;
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d);
+      if (lane >= (uint32_t)d) incl += y;
+    }
+    uint64_t pos = run + (incl - k0);
     while (bits) {
       const int k = __ffs(bits) - 1;
       bits &= bits - 1;
       out[pos++] = act ? act[i0 + k] : (uint32_t)(i0 + k);
     }
-    run += gt;
+    run += __shfl(incl, WAVE - 1);
   }
   if (t == gridDim.x - 1 && threadIdx.x < WAVE) {
     // a counting jump ran before (bucketed rounds): its sharded hook totals join the counters
