@@ -361,6 +361,7 @@ def rmat_s26_reference(torch_cuda):
     ref = msf_boruvka(e.n, e.u, e.v, e.w)
     assert torch.equal(flags.bool(), ref), "s26 single-GPU MSF differs from the torch Boruvka checker"
     del ref
+    _oracle_full_size(e, flags, res)
     torch.cuda.empty_cache()
     w = (e.w.to(torch.int64) & 0xFFFFFFFF)
     assert int(flags.sum().item()) == res.num_mst_edges
@@ -781,13 +782,28 @@ def test_device_level_plan_matches_formula(scale, cfg, torch_cuda):
     assert below <= lvl0 <= below + 3 * 4 * 2048
 
 
+def _oracle_full_size(e, flags, res):
+    """The oracle at BASELINE size: oracle/boruvka_omp.c (the all-cores CPU restatement, pinned to
+    canonical Kruskal on every golden fixture and random tie-heavy graphs in tests/test_oracle.py)
+    over the same canonical arrays, flags compared edge for edge, totals with the GPU's."""
+    ora = _oracle()
+    cu, cv, cw = (t.cpu().numpy() for t in (e.u, e.v, e.w))
+    ref, tw, k, _ = ora.boruvka_omp_c(e.n, cu, cv, cw)
+    del cu, cv, cw
+    got = flags.cpu().numpy().astype(bool)
+    assert np.array_equal(got, ref.astype(bool)), "HIP MSF differs from the oracle at full size"
+    assert (tw, k) == (res.total_weight, res.num_mst_edges)
+
+
 def _full_size_checks(e, eng, res, torch):
-    """BASELINE-size checks: independent torch Boruvka (bit-exact), determinism, and a second
-    execution path (one weight level, i.e. no giant filter) giving the same flags."""
+    """BASELINE-size checks: the oracle (bit-exact, all cores), the independent torch Boruvka
+    (bit-exact), determinism, and a second execution path (one weight level, i.e. no giant
+    filter) giving the same flags."""
     from distributed_ghs_implementation_amd import _native
     from distributed_ghs_implementation_amd.device import DeviceMST
     from torch_boruvka import msf_boruvka
     flags = eng.in_mst[: e.m].clone()
+    _oracle_full_size(e, flags, res)
     ref = msf_boruvka(e.n, e.u, e.v, e.w)
     assert torch.equal(flags.bool(), ref), "HIP MSF differs from the torch Boruvka checker"
     del ref
