@@ -50,9 +50,10 @@ def parse():
     ap.add_argument("--edgefactor", type=int, default=16)
     ap.add_argument("--workload", choices=["rmat", "grid", "grid-gradient"], default="rmat")
     ap.add_argument("--grid-k", type=int, default=16384)
-    ap.add_argument("--input", choices=["auto", "csr", "coo"], default="auto",
-                    help="the device-resident input form: CSR (row offsets + v + w, ghs_mst_device_csr, ABI 9) "
-                         "or COO (u + v + w, ghs_mst_device); auto = COO")
+    ap.add_argument("--input", choices=["auto", "csr", "coo", "both"], default="auto",
+                    help="the device-resident input form: CSR (row offsets + v + w, ghs_mst_device_csr, ABI 9), "
+                         "COO (u + v + w, ghs_mst_device) or both (offsets + u + v + w: k_select streams the "
+                         "CSR form, k_filter the COO form); auto = both at N = 1, COO at N > 1")
     ap.add_argument("--cpu-scale", type=int, default=22, help="R-MAT scale of the serial-Kruskal sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--nx-scale", type=int, default=16, help="R-MAT scale of the NetworkX baseline sample")
@@ -94,12 +95,14 @@ def _first_round(stats, r):
 
 
 # bytes the canonical passes stream per edge and per vertex row: COO u, v, w = 12 B per edge; CSR
-# (ABI 9) v, w = 8 B per edge + the u32 row offset of every row (run() sets it from the input form)
-STREAM_BYTES = {"edge": 12.0, "row": 0.0}
+# (ABI 9) v, w = 8 B per edge + the u32 row offset of every row (run() sets them from the input
+# form; with both forms resident k_select streams the CSR form and k_filter the COO form)
+STREAM_BYTES = {"select": (12.0, 0.0), "filter": (12.0, 0.0)}
 
 
-def _stream_bytes(res, n):
-    return STREAM_BYTES["edge"] * res.canon_edges + STREAM_BYTES["row"] * (n + 1)
+def _stream_bytes(res, n, kind):
+    edge, row = STREAM_BYTES[kind]
+    return edge * res.canon_edges + row * (n + 1)
 
 
 def launch_bytes(rec, stats, res, n, windowed=frozenset()):
@@ -107,9 +110,9 @@ def launch_bytes(rec, stats, res, n, windowed=frozenset()):
     launches are the device-side fallback that exited at once (k_select's span flag unset)."""
     k = rec["kernel"]
     if k == "k_select":
-        return _stream_bytes(res, n) + 16.0 * res.select_out  # the list in; level-0 edges out
+        return _stream_bytes(res, n, "select") + 16.0 * res.select_out  # the list in; level-0 edges out
     if k == "k_filter":
-        return _stream_bytes(res, n) + 16.0 * res.filter_out  # stream + level-1 and pending edges out
+        return _stream_bytes(res, n, "filter") + 16.0 * res.filter_out  # stream + level-1 and pending edges out
     if k == "k_resolve":
         return 8.0 * n + n / 8.0  # lab read + write, giant bitmap
     if k == "k_jump_ident":
@@ -381,6 +384,7 @@ def networkx_baseline(scale, edgefactor):
 
 
 def make_workload(args, world):
+    import torch
     from distributed_ghs_implementation_amd.device import generate_grid, generate_rmat
     if args.workload == "rmat":
         # N = 1: the s24 headline (BASELINE config 3); N > 1: strong scaling on s26 (config 4)
@@ -394,8 +398,27 @@ def make_workload(args, world):
         edges = generate_grid(k, 1 if args.workload == "grid-gradient" else 0)
         tag = f"{args.workload}-{k}x{k}"
         cfg = {"workload": tag, "grid_k": k}
-    form = args.input if args.input != "auto" else "coo"
-    if form == "csr":
+    # auto: at N = 1 the north_star's CSR edge list with u kept resident next to it ("both": k_select
+    # streams 8 B/edge from (off, v, w), k_filter 12 from (u, v, w) — 5.15 vs 5.25 ms for COO and 5.19
+    # for CSR alone on s24, profiles/r06/both/); at N > 1 COO (the s26 x 8 emulation's slowest-rank
+    # kernels were no faster with both, and each rank would validate all n + 1 offsets)
+    form = args.input if args.input != "auto" else ("both" if world == 1 else "coo")
+    if form in ("both", "csr"):
+        # the offsets' device build, timed for the record (outside the timed region, like generation)
+        t0 = torch.cuda.Event(enable_timing=True)
+        t1 = torch.cuda.Event(enable_timing=True)
+        t0.record()
+        edges.with_csr()
+        t1.record()
+        torch.cuda.synchronize()
+        cfg["csr_offsets_build_ms"] = round(t0.elapsed_time(t1), 4)
+    if form == "both":
+        # both forms resident: row offsets (built on the device from the sorted u, outside the timed
+        # region) next to u — the solve streams (off, v, w) in k_select and (u, v, w) in k_filter
+        edges = edges.with_csr()
+        cfg["input"] = ("CSR + u: n+1 u32 row offsets + u + v + w (u32), the canonical list in both forms "
+                        "(ghs_mst_device_csr with d_u)")
+    elif form == "csr":
         # the north_star's CSR edge list: row offsets (built on the device from the sorted u, outside
         # the timed region like the generation itself), u released — the solve streams (off, v, w)
         edges = edges.csr_only()
@@ -564,8 +587,9 @@ def run(args, world, rank, dist, dev):
 
     (edges, tag, cfg), gen_s = agreed("generate", gen, rank, world, dist, dev)
     n, m = edges.n, edges.m
-    if edges.off is not None and edges.u is None:  # CSR input: 8 B per edge + 4 B per row streamed
-        STREAM_BYTES.update(edge=8.0, row=4.0 / max(1, world))
+    if edges.off is not None:  # CSR streams: 8 B per edge + 4 B per row (a rank: its share of the rows)
+        csr = (8.0, 4.0 / max(1, world))
+        STREAM_BYTES.update(select=csr, filter=csr if edges.u is None else (12.0, 0.0))
     cfg.update({"n": n, "m": m, "partition": f"canonical edge ranges x{world}", "parallelism": f"edges{world}"})
 
     ref = None

@@ -4895,8 +4895,12 @@ static int open_level(ghs_solver *s, bool async_open = false) {
     if (!s->pending_built) {
       // FILTER + level split over the canonical list once level 0 is complete: level-1 edges
       // not inside one fragment -> Y; heavier edges not inside the giant -> pending (rem[rout])
-      auto filt = s->csr ? k_filter<true> : k_filter<false>;
-      G = s->csr ? s->csr_gfil : grid_for(TC, ARCS_PER_BLOCK, resident_grid((const void *)filt, BLOCK, s->seg_g));
+      // CSR input with the caller's u resident too: the COO form of the filter (the pass is
+      // probe-bound, and deriving u costs it more than the 4 B/edge it saves: R-MAT s24 1.59 vs
+      // 1.62-1.63 ms), while k_select keeps the CSR stream (0.53 vs 0.68 ms)
+      const bool fcsr = s->csr && !s->eu;
+      auto filt = fcsr ? k_filter<true> : k_filter<false>;
+      G = fcsr ? s->csr_gfil : grid_for(TC, ARCS_PER_BLOCK, resident_grid((const void *)filt, BLOCK, s->seg_g));
       if (TC) {
         GHS_HIP_CHECK(hipEventRecord(s->res->pass_ev[2], st));
         {

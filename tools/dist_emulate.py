@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--level1", type=float, default=None, help="level-1 edges per vertex")
     ap.add_argument("--beta", type=float, default=None, help="edge_range's cost slope (device.RANGE_BETA)")
     ap.add_argument("--csr", action="store_true", help="the ranks stream the CSR form (ghs_solver_create_csr)")
+    ap.add_argument("--both", action="store_true",
+                    help="CSR form with u resident too (k_select streams CSR, k_filter COO)")
     args = ap.parse_args()
     import torch
     from distributed_ghs_implementation_amd import _native
@@ -63,6 +65,8 @@ def main():
                               level1_edges_per_vertex=args.level1)
     if args.csr:
         e = e.csr_only()
+    elif args.both:
+        e = e.with_csr()
     engines = [DeviceMST(e, *edge_range(e.m, r, W, args.beta), config=cfg) for r in range(W)]
     steppers = [HipStepper(x) for x in engines]
 
