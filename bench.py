@@ -401,8 +401,12 @@ def make_workload(args, world):
     # auto: at N = 1 the north_star's CSR edge list with u kept resident next to it ("both": k_select
     # streams 8 B/edge from (off, v, w), k_filter 12 from (u, v, w) — 5.15 vs 5.25 ms for COO and 5.19
     # for CSR alone on s24, profiles/r06/both/); at N > 1 COO (the s26 x 8 emulation's slowest-rank
-    # kernels were no faster with both, and each rank would validate all n + 1 offsets)
-    form = args.input if args.input != "auto" else ("both" if world == 1 else "coo")
+    # kernels were no faster with both, and each rank would validate all n + 1 offsets). Below an
+    # average degree of 4 COO too: the CSR pre-pass reads the n + 1 offsets (validation, tile rows)
+    # while k_select saves only 4 - 4n/m B per edge — the 16384^2 grids (m/n = 2) ran 0.2-0.3 ms slower
+    # with both (profiles/r06/both/grid_ab.txt)
+    dense = edges.m >= 4 * edges.n
+    form = args.input if args.input != "auto" else ("both" if world == 1 and dense else "coo")
     if form in ("both", "csr"):
         # the offsets' device build, timed for the record (outside the timed region, like generation)
         t0 = torch.cuda.Event(enable_timing=True)
