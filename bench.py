@@ -213,7 +213,9 @@ def stage1_roofline(records, stats):
 # profile name -> the PMC file's kernel-name prefix (rocprofv3 prints every template argument:
 # k_minedge<false, true, false>; any later template parameter still matches the prefix)
 PMC_NAMES = {"k_minedge<IDENT>": "k_minedge<true, false", "k_minedge<COMPACT>": "k_minedge<false, true",
-             "k_bmin": "k_bmin<", "k_wmin": "k_wmin<"}
+             "k_bmin": "k_bmin<", "k_wmin": "k_wmin<",
+             # the streaming passes' form (<true>: CSR), set from the input the solve streams
+             "k_select": "k_select<false", "k_filter": "k_filter<false"}
 
 
 def _pmc_match(name, key):
@@ -594,6 +596,7 @@ def run(args, world, rank, dist, dev):
     if edges.off is not None:  # CSR streams: 8 B per edge + 4 B per row (a rank: its share of the rows)
         csr = (8.0, 4.0 / max(1, world))
         STREAM_BYTES.update(select=csr, filter=csr if edges.u is None else (12.0, 0.0))
+        PMC_NAMES.update({"k_select": "k_select<true", "k_filter": f"k_filter<{str(edges.u is None).lower()}"})
     cfg.update({"n": n, "m": m, "partition": f"canonical edge ranges x{world}", "parallelism": f"edges{world}"})
 
     ref = None

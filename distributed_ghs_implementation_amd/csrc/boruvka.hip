@@ -2866,12 +2866,15 @@ __global__ __launch_bounds__(BM_T) void k_bmin(const uint4 *__restrict__ rec, co
   __shared__ uint32_t s_pre[BK_G];  // ... and its first index in the bucket's record order
   __shared__ uint32_t s_wsum[BM_T / WAVE];
   if (only_if && !*only_if) return;  // the windowed round ran (k_wmin)
-  const bool noop = guard_nact && *guard_nact <= 1;
-  const uint64_t T = noop ? 0 : in.prefix[in.nseg];
+  // a round enqueued past its level's end (the pipelined loop's lookahead) exits before the block
+  // scans: one bucket per block, n / 2^BS blocks — the 16384^2 gradient grid's no-op k_bmin took
+  // 57 us through them (profiles/r06/final/rounds_grid-gradient.txt)
+  if (guard_nact && *guard_nact <= 1) return;
+  const uint64_t T = in.prefix[in.nseg];
   const uint64_t R2 = 2 * bk_quota(T);  // record region stride
   const uint32_t t = blockIdx.x;
   uint32_t cnt = 0, st = 0;
-  if (threadIdx.x < BK_G && !noop) {
+  if (threadIdx.x < BK_G) {
     st = O[bk_off_index(t, threadIdx.x, gridDim.x)];
     cnt = O[bk_off_index(t + 1, threadIdx.x, gridDim.x)] - st;
   }
@@ -5536,7 +5539,7 @@ static int decide_bucketed(ghs_solver *s) {
 // 26x, 19x, 10x, 10x), so half a round of margin — none when the open's hooks alone are expected to
 // finish (F0 <= decay): R-MAT s24 levels 0 and 1 and both tails of the 16384^2 grid then launch no
 // round past the finishing one (profiles/r06/rounds_*.txt). An underestimate costs one more batch.
-constexpr uint32_t TAIL_BATCH_MIN = 1, TAIL_BATCH_MAX = 8, TAIL_BATCH_NEXT = 3;
+constexpr uint32_t TAIL_BATCH_MIN = 1, TAIL_BATCH_MAX = 8;
 
 static uint32_t tail_first_batch(uint64_t F0, uint64_t prev_in) {
   const double decay = std::max(2.0, prev_in > F0 ? (double)prev_in / (double)F0 : 2.0);
@@ -5664,7 +5667,6 @@ static int run_tail(ghs_solver *s, uint64_t prev_in, const GhsTailColl *coll = n
   uint32_t batch = tail_first_batch(t.F0, prev_in);
   for (;;) {
     const uint32_t last = std::min(t.r + batch - 1, TAIL_ROUNDS_MAX);  // the batch's last round
-    batch = TAIL_BATCH_NEXT;
     for (; t.r <= last; ++t.r) {
       // round r - 1's hooks, unless the open's (launched above): a batch ends with a round, not with
       // its hook kernel, so the round that finishes the level is not followed by a no-op hook launch
@@ -5677,6 +5679,12 @@ static int run_tail(ghs_solver *s, uint64_t prev_in, const GhsTailColl *coll = n
     if (int rc = tail_report(s, t, last, &nact_out)) return rc;
     if (nact_out <= 1) break;
     if (t.r > TAIL_ROUNDS_MAX) return fail_counters(s, 4, "in the LDS tail (round cap)");
+    // the next batch from the batch's last contraction (the report's copy of the control block:
+    // nroots[last] = nact_out roots entering round last's stream, nroots[last - 1] before them),
+    // sized like the first — R-MAT s26 level 0 (1189 -> 106 -> 14 -> 3 roots) then finishes in a
+    // batch of 1 instead of a fixed 3 with two no-op launch pairs
+    const TailCtl &c = *s->res->h_tail;
+    batch = tail_first_batch(nact_out, last >= 1 ? c.nroots[last - 1] : t.F0);
   }
   return tail_finish(s, t);
 }

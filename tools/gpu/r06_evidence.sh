@@ -28,10 +28,11 @@ for spec in ${PMC_SPECS:-rmat:rmat-s24-ef16 grid:grid-16384x16384 grid-gradient:
   wl=${spec%%:*}; tag=${spec#*:}
   TAG=${TAG:-r06final}/pmc_$wl KRE="$KRE" WL=$tag BENCH_ARGS="--workload $wl --no-scaling-base" bash tools/gpu/pmc_traffic.sh; rc=$?; fatal $rc pmc-$wl
 done
-for spec in rmat:24 grid:0 grid-gradient:0; do
+for spec in rmat:24 rmat:26 grid:0 grid-gradient:0; do
   wl=${spec%%:*}; sc=${spec#*:}
   args="--workload $wl"; [ "$wl" = rmat ] && args="$args --scale $sc"
-  timeout -k 10 240 python3 -u tools/round_profile.py $args > "$OUT/rounds_${wl}.txt" 2>&1; rc=$?; fatal $rc rounds-$wl
+  f="$OUT/rounds_${wl}.txt"; [ "$sc" = 26 ] && f="$OUT/rounds_${wl}_s26.txt"
+  timeout -k 10 240 python3 -u tools/round_profile.py $args > "$f" 2>&1; rc=$?; fatal $rc rounds-$wl-$sc
 done
 fi
 echo evidence part ${PART:-1} done

@@ -2,6 +2,7 @@
 round's live edges / active fragments / hooks.
 
     python tools/round_profile.py [--workload rmat|grid|grid-gradient] [--scale 24] [--grid-k 16384]
+                                  [--input auto|coo|csr|both]   (auto: bench.py's N = 1 choice)
 """
 import argparse
 import os
@@ -17,6 +18,7 @@ def main():
     ap.add_argument("--scale", type=int, default=24)
     ap.add_argument("--grid-k", type=int, default=16384)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--input", choices=["auto", "coo", "csr", "both"], default="auto")
     args = ap.parse_args()
     import torch
     from distributed_ghs_implementation_amd import _native
@@ -25,6 +27,11 @@ def main():
         e = generate_rmat(args.scale, 16, seed=1, wseed=2)
     else:
         e = generate_grid(args.grid_k, 1 if args.workload == "grid-gradient" else 0)
+    form = args.input if args.input != "auto" else ("both" if e.m >= 4 * e.n else "coo")
+    if form == "both":
+        e = e.with_csr()
+    elif form == "csr":
+        e = e.csr_only()
     eng = DeviceMST(e)
     eng.run()
     torch.cuda.synchronize()
@@ -48,7 +55,7 @@ def main():
         key = r["round"] if ok else ("finish" if fin else "noop", r["level"])
         per[key][r["kernel"]] += r["ms"]
     tot = sum(r["ms"] for r in recs)
-    print(f"m={e.m} n={e.n} rounds={res.rounds} levels={res.levels} sum of launches {tot:.3f} ms")
+    print(f"input={form} m={e.m} n={e.n} rounds={res.rounds} levels={res.levels} sum of launches {tot:.3f} ms")
     for i, st in enumerate(stats):
         ks = per.get(i, {})
         print(f"r{i:2d} L{st['level']} live {st['live_arcs']:>11d} frags {st['active_components']:>10d} "
