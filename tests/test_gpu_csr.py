@@ -65,15 +65,18 @@ CONFIGS = [dict(max_levels=1), dict(), dict(max_levels=6, level1_edges_per_verte
            dict(max_levels=16, level1_edges_per_vertex=0.01, level_growth=1.5)]
 
 
+@pytest.mark.parametrize("keep_u", [False, True])
 @pytest.mark.parametrize("cfg", CONFIGS)
 @pytest.mark.parametrize("scale", [10, 14, 18])
-def test_csr_rmat_vs_oracle_and_coo(scale, cfg, torch_cuda):
+def test_csr_rmat_vs_oracle_and_coo(scale, cfg, keep_u, torch_cuda):
+    """keep_u: both forms resident (bench.py's N = 1 default): k_select streams the CSR form,
+    k_filter the COO one."""
     from distributed_ghs_implementation_amd import _native
     from distributed_ghs_implementation_amd.device import generate_rmat
     e = generate_rmat(scale, 16, seed=1, wseed=2)
     g = e.to_host()
     c = _native.make_config(**cfg)
-    got = _check(g, e.csr_only(), c)
+    got = _check(g, e.with_csr() if keep_u else e.csr_only(), c)
     coo, _ = _solve(e, c, csr=False)
     assert np.array_equal(got, coo)
 
@@ -221,5 +224,11 @@ def test_csr_rmat_s24_equals_coo(torch_cuda):
     rb, _ = b.run()
     assert torch.equal(fa, b.in_mst[: e.m])
     assert (ra.total_weight, ra.num_mst_edges) == (rb.total_weight, rb.num_mst_edges)
+    del b
+    torch.cuda.empty_cache()
+    h = DeviceMST(e.with_csr())  # both forms (bench.py's N = 1 default): CSR k_select, COO k_filter
+    rh, _ = h.run()
+    assert torch.equal(fa, h.in_mst[: e.m])
+    assert (ra.total_weight, ra.num_mst_edges) == (rh.total_weight, rh.num_mst_edges)
     w = e.w.to(torch.int64) & 0xFFFFFFFF
     assert int(w[fa.bool()].sum().item()) == rb.total_weight
