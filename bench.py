@@ -12,6 +12,10 @@ parameters, unique hashed weights — no dataset download).
          every N solves the same graph, so scaling_base and the N > 1 lines form one curve; a
          step there also gathers the MSF edge ids to rank 0 (the reference's collect_results),
          ms_per_step_solve times the solve alone. "scaling" is "strong" on every line.
+Input form (--input, config.input): at N = 1 on graphs with m >= 4n the canonical list is resident in
+both forms — CSR row offsets (the north_star's "CSR edge list in HBM", built on the device from the
+sorted u before the timed region, config.csr_offsets_build_ms) next to u, v, w: k_select streams
+the CSR form, k_filter the COO form; elsewhere COO (u, v, w).
 Rank 0 prints ONE JSON line. After the timed steps one extra step runs with every kernel launch
 bracketed by HIP events on the solve's stream (libghs_mst.so ghs_profile_enable): `kernels` lists
 every kernel's time per step and achieved GB/s under its algorithmic byte model (launch_bytes),
