@@ -5991,7 +5991,8 @@ static int solver_create(uint32_t n, uint64_t m, const uint32_t *d_u, const uint
   if (cfg && (cfg->num_ranks < 1 || cfg->num_ranks > GHS_MAX_RANKS)) GHS_FAIL(GHS_E_ARG, "num_ranks must be in [1, GHS_MAX_RANKS]");
   if (m && ((!d_u && !d_off) || !d_v || !d_w || !d_in_mst)) GHS_FAIL(GHS_E_ARG, "d_u (d_off)/d_v/d_w/d_in_mst is NULL");
   if (d_off && m && n == 0) GHS_FAIL(GHS_E_ARG, "CSR input with edges needs n >= 1");
-  if ((((uintptr_t)(d_off ? nullptr : d_u)) | ((uintptr_t)d_v) | ((uintptr_t)d_w)) & 15)
+  // (a CSR caller's d_u too: the level-opening filter streams it when present)
+  if ((((uintptr_t)d_u) | ((uintptr_t)d_v) | ((uintptr_t)d_w)) & 15)
     GHS_FAIL(GHS_E_ARG, "d_u/d_v/d_w must be 16-byte aligned");
   if (((uintptr_t)d_off) & 3) GHS_FAIL(GHS_E_ARG, "d_off must be 4-byte aligned");
   const size_t need = workspace_layout(n, m, e_hi - e_lo, nullptr, nullptr);

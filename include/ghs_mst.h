@@ -217,8 +217,10 @@ int ghs_mst_device(uint32_t n, uint64_t m, const uint32_t *d_u, const uint32_t *
  * nondecreasing, d_off[n] = m), edge e of row u (d_off[u] <= e < d_off[u + 1]) joins u and d_v[e]
  * with weight d_w[e]; d_v strictly ascending inside a row, u < d_v[e] < n. eid = e as in the COO
  * form (same keys, same MSF flags). The streaming passes read 8 B per edge (+ 4 B per row) instead
- * of 12. d_u may be NULL, or the caller's expanded u (then used only for gathers of u by edge id,
- * which otherwise search d_off). The offsets are validated with the rest (GHS_E_NONCANON). */
+ * of 12. d_u may be NULL, or the caller's expanded u (16-byte aligned): then gathers of u by edge
+ * id read it instead of searching d_off, and the level-opening filter pass streams (u, v, w) — the
+ * faster form for that pass — while the first pass streams the CSR form. The offsets are validated
+ * with the rest (GHS_E_NONCANON). */
 int ghs_mst_device_csr(uint32_t n, uint64_t m, const uint32_t *d_off, const uint32_t *d_u, const uint32_t *d_v,
                        const uint32_t *d_w, const ghs_config_t *cfg, void *d_workspace, size_t workspace_bytes,
                        uint8_t *d_in_mst, void *stream, ghs_result_t *result, ghs_round_stats_t *stats);
