@@ -389,6 +389,27 @@ def networkx_baseline(scale, edgefactor):
             "seconds": dt, "weight_matches_oracle": tw == ref_tw}
 
 
+def input_form(requested, world, n, m):
+    """The input form the solve streams: `requested` unless "auto" — both forms (CSR offsets + u)
+    at N = 1 when m >= 4n, else COO (reasons at make_workload)."""
+    if requested != "auto":
+        return requested
+    return "both" if world == 1 and m >= 4 * n else "coo"
+
+
+def set_stream_forms(has_off, has_u, world):
+    """The byte model and PMC kernel names of the streaming passes for the resident input: CSR
+    offsets -> k_select streams 8 B/edge + 4 B/row (a rank: its share of the rows); k_filter
+    streams the CSR form only without u."""
+    if not has_off:
+        STREAM_BYTES.update(select=(12.0, 0.0), filter=(12.0, 0.0))
+        PMC_NAMES.update({"k_select": "k_select<false", "k_filter": "k_filter<false"})
+        return
+    csr = (8.0, 4.0 / max(1, world))
+    STREAM_BYTES.update(select=csr, filter=(12.0, 0.0) if has_u else csr)
+    PMC_NAMES.update({"k_select": "k_select<true", "k_filter": f"k_filter<{str(not has_u).lower()}"})
+
+
 def make_workload(args, world):
     import torch
     from distributed_ghs_implementation_amd.device import generate_grid, generate_rmat
@@ -411,8 +432,7 @@ def make_workload(args, world):
     # average degree of 4 COO too: the CSR pre-pass reads the n + 1 offsets (validation, tile rows)
     # while k_select saves only 4 - 4n/m B per edge — the 16384^2 grids (m/n = 2) ran 0.2-0.3 ms slower
     # with both (profiles/r06/both/grid_ab.txt)
-    dense = edges.m >= 4 * edges.n
-    form = args.input if args.input != "auto" else ("both" if world == 1 and dense else "coo")
+    form = input_form(args.input, world, edges.n, edges.m)
     if form in ("both", "csr"):
         # the offsets' device build, timed for the record (outside the timed region, like generation)
         t0 = torch.cuda.Event(enable_timing=True)
@@ -597,10 +617,7 @@ def run(args, world, rank, dist, dev):
 
     (edges, tag, cfg), gen_s = agreed("generate", gen, rank, world, dist, dev)
     n, m = edges.n, edges.m
-    if edges.off is not None:  # CSR streams: 8 B per edge + 4 B per row (a rank: its share of the rows)
-        csr = (8.0, 4.0 / max(1, world))
-        STREAM_BYTES.update(select=csr, filter=csr if edges.u is None else (12.0, 0.0))
-        PMC_NAMES.update({"k_select": "k_select<true", "k_filter": f"k_filter<{str(edges.u is None).lower()}"})
+    set_stream_forms(edges.off is not None, edges.u is not None, world)
     cfg.update({"n": n, "m": m, "partition": f"canonical edge ranges x{world}", "parallelism": f"edges{world}"})
 
     ref = None

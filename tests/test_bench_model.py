@@ -53,3 +53,34 @@ def test_pmc_names_match_templated_kernels():
     assert bench._pmc_match("k_bmin", "k_bmin<13u, false>")
     assert bench._pmc_match("k_minedge<COMPACT>", "k_minedge<false, true, false, true>")
     assert not bench._pmc_match("k_minedge<IDENT>", "k_minedge<false, true, false, true>")
+
+
+def test_auto_input_form():
+    """auto: both forms at N = 1 on graphs with m >= 4n (R-MAT s24: m/n = 15.5), COO on the grids
+    (m/n = 2) and at N > 1; an explicit form is kept."""
+    assert bench.input_form("auto", 1, 1 << 24, 260383859) == "both"
+    assert bench.input_form("auto", 1, 16384 * 16384, 536838144) == "coo"
+    assert bench.input_form("auto", 8, 1 << 26, 1051916369) == "coo"
+    assert bench.input_form("csr", 8, 10, 5) == "csr"
+
+
+class _Cnt:
+    canon_edges = 1000
+    select_out = 10
+    filter_out = 20
+
+
+def test_stream_byte_model_per_form():
+    n = 100
+    try:
+        bench.set_stream_forms(True, True, 1)  # both: CSR select, COO filter
+        assert bench._stream_bytes(_Cnt, n, "select") == 8.0 * 1000 + 4.0 * (n + 1)
+        assert bench._stream_bytes(_Cnt, n, "filter") == 12.0 * 1000
+        assert bench._pmc_match("k_select", "k_select<true>") and bench._pmc_match("k_filter", "k_filter<false>")
+        bench.set_stream_forms(True, False, 4)  # CSR alone, a rank of 4: a quarter of the rows
+        assert bench._stream_bytes(_Cnt, n, "filter") == 8.0 * 1000 + 1.0 * (n + 1)
+        assert bench._pmc_match("k_filter", "k_filter<true>") and not bench._pmc_match("k_filter", "k_filter<false>")
+    finally:
+        bench.set_stream_forms(False, True, 1)
+    assert bench._stream_bytes(_Cnt, n, "select") == 12.0 * 1000
+    assert bench._pmc_match("k_select", "k_select<false>") and not bench._pmc_match("k_select", "k_select<true>")
