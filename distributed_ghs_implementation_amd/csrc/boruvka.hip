@@ -996,14 +996,30 @@ __global__ __launch_bounds__(1024) void k_scan_counts(const uint64_t *__restrict
 // active flags = chunk prefix + word prefix + the flags below x in its 64-bit word. The three
 // tables (12 B per 64 vertices: 12 MB at s26) replace a vertex-sized position map (268 MB) whose
 // random reads went to HBM.
+// pk (k_rank_pack): the same per word in one 16-B entry {bits lo, bits hi, flags below the word}
+// — one random gather per lookup instead of two (bits, wpre; cpre is 4 KiB at s26, cache-resident)
 struct DenseRank {
   const uint64_t *bits = nullptr;  // active flags, 64 vertices per word
   const uint32_t *wpre = nullptr;  // flags below the word, within its chunk of 256 words
   const uint32_t *cpre = nullptr;  // flags below the chunk
+  const uint4 *pk = nullptr;       // packed (nullptr: the three tables)
 };
 __device__ __forceinline__ uint32_t dense_rank(const DenseRank &r, uint32_t x) {
   const uint32_t w = x >> 6;
-  return r.cpre[w >> 8] + r.wpre[w] + (uint32_t)__popcll(r.bits[w] & ((1ull << (x & 63)) - 1));
+  const uint64_t below = (1ull << (x & 63)) - 1;
+  if (r.pk) {
+    const uint4 q = r.pk[w];
+    return q.z + (uint32_t)__popcll((((uint64_t)q.y << 32) | q.x) & below);
+  }
+  return r.cpre[w >> 8] + r.wpre[w] + (uint32_t)__popcll(r.bits[w] & below);
+}
+
+__global__ void k_rank_pack(const uint64_t *__restrict__ bits, const uint32_t *__restrict__ wpre,
+                            const uint32_t *__restrict__ cpre, uint64_t words, uint4 *__restrict__ pk) {
+  for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < words; w += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = bits[w];
+    pk[w] = make_uint4((uint32_t)b, (uint32_t)(b >> 32), cpre[w >> 8] + wpre[w], 0u);
+  }
 }
 
 __device__ __forceinline__ uint32_t find_lab(const uint32_t *__restrict__ lab, uint32_t x,
@@ -4368,6 +4384,7 @@ struct ghs_solver {
   bool words_merged = false;                       // this level's flags arrived as merged words
   bool rank_ready = false;                         // ... and the rank tables are built from them
   uint32_t *drank_wpre = nullptr, *drank_cpre = nullptr;
+  uint4 *drank_pk = nullptr;  // the packed rank table (k_rank_pack; GHS_DENSE_PACK)
   uint64_t *dbest = nullptr;
   uint32_t *vlab = nullptr, *vpar = nullptr;
   uint64_t *flag_bits = nullptr;  // the packed level-open flags (ghs_solver_flag_bits)
@@ -4608,6 +4625,7 @@ static size_t workspace_layout(uint32_t n, uint64_t m, uint64_t local_edges, ghs
     p = carve(W * 8); if (s) s->drank_bits = (uint64_t *)p;
     p = carve(W * 4); if (s) s->drank_wpre = (uint32_t *)p;
     p = carve(((W + BLOCK - 1) / BLOCK) * 4 + 4); if (s) s->drank_cpre = (uint32_t *)p;
+    p = carve(W * 16); if (s) s->drank_pk = (uint4 *)p;
     p = carve(N * 4, stg); if (s) s->dvtx = (uint32_t *)p;
   }
   p = carve(N + 1); if (s) s->flags = (uint8_t *)p;  // + the multi-rank error byte flags[n]
@@ -4959,12 +4977,23 @@ static int open_level(ghs_solver *s, bool async_open = false) {
 }
 
 // ---- dense levels (several ranks; kernels at k_dense_open) ------------------------------------
+#ifndef GHS_DENSE_PACK
+#define GHS_DENSE_PACK 1
+#endif
 static DenseRank dense_rank_of(const ghs_solver *s) {
   DenseRank r;
   r.bits = s->drank_bits;
   r.wpre = s->drank_wpre;
   r.cpre = s->drank_cpre;
+  r.pk = GHS_DENSE_PACK ? s->drank_pk : nullptr;
   return r;
+}
+
+// after k_rank_chunks: the packed table every dense_rank lookup of the level reads
+static void rank_pack(ghs_solver *s, uint64_t words) {
+  if (GHS_DENSE_PACK && s->drank_pk)
+    k_rank_pack<<<grid_for(words, 256, 8192), 256, 0, s->stream>>>(s->drank_bits, s->drank_wpre, s->drank_cpre, words,
+                                                                  s->drank_pk);
 }
 
 static int dense_open(ghs_solver *s) {
@@ -4981,6 +5010,7 @@ static int dense_open(ghs_solver *s) {
     } else {
       k_rank_words<<<chunks, BLOCK, 0, st>>>(s->flags, s->n, s->drank_bits, s->drank_wpre, s->drank_cpre, false);
       k_rank_chunks<<<1, 1024, 0, st>>>(s->drank_cpre, chunks, nullptr);
+      rank_pack(s, words);
       k_dense_open<<<grid_for(nact, 256, 16384), 256, 0, st>>>(s->act[0], s->cnt + C_ACT, s->dvtx, s->dlab,
                                                                s->dpar, s->dbest, s->cnt + C_NDENSE);
     }
@@ -5044,6 +5074,7 @@ static int open_level_finish(ghs_solver *s) {
     const uint32_t chunks = (uint32_t)((words + BLOCK - 1) / BLOCK);
     k_rank_words<<<chunks, BLOCK, 0, st>>>(s->flags, s->n, s->drank_bits, s->drank_wpre, s->drank_cpre, true);
     k_rank_chunks<<<1, 1024, 0, st>>>(s->drank_cpre, chunks, s->cnt + C_ACT);
+    rank_pack(s, words);
     GHS_HIP_CHECK(hipGetLastError());
   } else if (int rc = select_lb(s, nullptr, s->cnt + C_N, s->n, s->act[0], s->cnt + C_ACT)) {
     return rc;
